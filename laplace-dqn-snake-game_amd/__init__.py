@@ -1,0 +1,15 @@
+"""snake_amd — MI355X-native hot path of lucagiorgetti/Laplace-DQN-Snake-game.
+
+Import as `import snake_amd` (the root shim snake_amd.py maps this hyphenated
+directory to that name). All compute runs in libsnakehip.so (HIP, gfx950);
+this package is the host-side mirror of the reference's Julia API.
+"""
+from ._lib import (BufferSizeError, DeviceArray, FoodListExhausted, SnakeHipError,  # noqa: F401
+                   device_count, header_symbols, load)
+from .env import (ALL_ACTIONS, D, L, NULL_ACTION, R, U, SnakeGame, assemble_state_,  # noqa: F401
+                  available_action_codes, available_actions, food_list, reset_, step_,
+                  step_indices_dev, synth_actions_dev, virtual_step)
+from .replay import (ReplayBuffer, empty_buffer_, isfull, isready, sample, stack_exp,  # noqa: F401
+                     store_)
+
+__version__ = "1.0.0"

@@ -1,0 +1,191 @@
+"""ctypes binding of libsnakehip.so (the C ABI in include/snakehip.h).
+
+The shared library is the product: every computation of this package runs in
+it on the GPU. There is no CPU fallback; if the library is missing or no HIP
+device is visible, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsnakehip.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "snakehip.h")
+
+SNK_OK = 0
+SNK_ERR_INVALID = 1
+SNK_ERR_FOOD_EXHAUSTED = 2
+SNK_ERR_HIP = 3
+SNK_ERR_NOMEM = 4
+SNK_ERR_STATE = 5
+SNK_ERR_INTERNAL = 6
+SNK_ACT_INDEX = 0
+SNK_ACT_DIRECTION = 1
+
+
+class SnakeHipError(RuntimeError):
+    """A non-zero status from libsnakehip."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[snk status {code}] {msg}")
+        self.code = code
+
+
+class FoodListExhausted(SnakeHipError):
+    """The reference throws BoundsError here (utils.jl:37 `board[0] = 2`)."""
+
+
+class BufferSizeError(SnakeHipError):
+    """structs.jl:154 `batch_size cannot be greater than the capacity of the buffer.`"""
+
+
+_lib = None
+
+vp = C.c_void_p
+i32, i64, u32, u64, f32, f64 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_float, C.c_double
+P = C.POINTER
+
+# name -> argtypes (restype is int status unless listed in _RESTYPE)
+_PROTOS = {
+    "snk_last_error": [],
+    "snk_version": [P(i32)],
+    "snk_device_count": [P(i32)],
+    "snk_set_device": [i32],
+    "snk_set_stream": [vp],
+    "snk_synchronize": [],
+    "snk_malloc": [P(vp), i64],
+    "snk_free": [vp],
+    "snk_memcpy_h2d": [vp, vp, i64],
+    "snk_memcpy_d2h": [vp, vp, i64],
+    "snk_memset": [vp, i32, i64],
+    "snk_food_list": [i32, u32, i32, vp],
+    "snk_env_create": [P(vp), i64, i32, i32, u32, i32, i32],
+    "snk_env_destroy": [vp],
+    "snk_env_reset": [vp, vp],
+    "snk_env_step": [vp, vp, i32],
+    "snk_env_outputs": [vp, P(vp), P(vp), P(vp), P(vp), P(vp), P(vp)],
+    "snk_env_get_boards": [vp, vp],
+    "snk_env_get_states": [vp, vp],
+    "snk_env_get_scalars": [vp, vp, vp, vp, vp, vp, vp],
+    "snk_env_get_snake": [vp, i64, vp, P(i32)],
+    "snk_env_check_faults": [vp, P(i64)],
+    "snk_env_synth_actions": [vp, u64, vp],
+    "snk_env_info": [vp, P(i64), P(i32), P(i32), P(i64)],
+    "snk_replay_create": [P(vp), i64, i32, i32, i32],
+    "snk_replay_destroy": [vp],
+    "snk_env_step_store": [vp, vp, i32, vp],
+    "snk_replay_store": [vp, i64, vp, vp, vp, vp, vp, vp],
+    "snk_replay_length": [vp, P(i64)],
+    "snk_replay_position": [vp, P(i64)],
+    "snk_replay_empty": [vp],
+    "snk_replay_sample": [vp, u64, u64, vp, P(i32)],
+    "snk_replay_gather": [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp],
+}
+_RESTYPE = {"snk_last_error": C.c_char_p}
+
+
+def header_symbols() -> list[str]:
+    """Every function the C header declares (used by the ABI test)."""
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(snk_[a-z0-9_]+)\s*\(", txt)))
+
+
+def load():
+    """Load libsnakehip.so. torch is imported first when present so that the
+    process holds ONE HIP runtime (torch ships its own libamdhip64)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional plumbing
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(LIB_PATH)
+    for name, args in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPE.get(name, C.c_int)
+    _lib = lib
+    return lib
+
+
+def check(status: int):
+    if status == SNK_OK:
+        return
+    msg = load().snk_last_error().decode(errors="replace")
+    if status == SNK_ERR_FOOD_EXHAUSTED:
+        raise FoodListExhausted(status, msg)
+    if status == SNK_ERR_STATE and "capacity" in msg:
+        raise BufferSizeError(status, msg)
+    raise SnakeHipError(status, msg)
+
+
+def call(name: str, *args):
+    check(getattr(load(), name)(*args))
+
+
+def ptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "host arrays must be C-contiguous"
+    return a.ctypes.data_as(vp)
+
+
+def device_count() -> int:
+    n = i32(0)
+    try:
+        call("snk_device_count", C.byref(n))
+    except SnakeHipError:
+        return 0
+    return n.value
+
+
+class DeviceArray:
+    """A device allocation owned by the library allocator (snk_malloc)."""
+
+    def __init__(self, shape, dtype):
+        self.shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        p = vp()
+        call("snk_malloc", C.byref(p), max(self.nbytes, 1))
+        self.ptr = p
+
+    @classmethod
+    def from_host(cls, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        d = cls(a.shape, a.dtype)
+        d.upload(a)
+        return d
+
+    def upload(self, a: np.ndarray):
+        a = np.ascontiguousarray(a, self.dtype)
+        assert a.nbytes == self.nbytes, (a.nbytes, self.nbytes)
+        call("snk_memcpy_h2d", self.ptr, ptr(a), self.nbytes)
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, self.dtype)
+        call("snk_memcpy_d2h", ptr(out), self.ptr, self.nbytes)
+        return out
+
+    def zero(self):
+        call("snk_memset", self.ptr, 0, self.nbytes)
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and self.ptr.value and _lib is not None:
+            _lib.snk_free(self.ptr)
+            self.ptr = None
+
+
+def view_numpy(dev_ptr: int, shape, dtype) -> np.ndarray:
+    """Copy `shape` elements at a raw device pointer to a new host array."""
+    out = np.empty(shape, dtype)
+    call("snk_memcpy_d2h", ptr(out), vp(dev_ptr), out.nbytes)
+    return out
