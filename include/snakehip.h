@@ -122,6 +122,85 @@ int snk_replay_gather(snk_replay rb, const int64_t *idx_dev, int64_t B, float *s
                       int32_t *actions_dev, float *rewards_dev, float *next_states_dev,
                       uint8_t *dones_dev, uint8_t *mask_dev, uint8_t *dirs_dev);
 
+/* ---------------------------------------------------------------- DQNModel
+ * DQNModel (structs.jl:161-185): q_net, t_net = deepcopy(q_net) and the
+ * RMSProp(lr) state. Parameters cross the ABI in Flux.destructure order
+ * (per layer weight then bias, each column-major; Conv = true convolution). */
+typedef struct snk_dqn_s *snk_dqn;
+
+#define SNK_NET_Q 0          /* q_net */
+#define SNK_NET_TARGET 1     /* t_net */
+#define SNK_NET_OPT_STATE 2  /* RMSProp accumulator (Optimisers `quad`) */
+#define SNK_NET_GRAD 3       /* gradient of the last loss */
+
+/* DQNModel(board_size, 3; lr) with Flux's glorot_uniform init drawn from a
+ * counter RNG seeded by init_seed; RMSProp(lr, rho, eps) = (5e-4, 0.9, 1e-8). */
+int snk_dqn_create(snk_dqn *out, int32_t board_size, int32_t n_frames, float lr, float rho, float eps,
+                   uint64_t init_seed);
+int snk_dqn_destroy(snk_dqn m);
+int snk_dqn_nparams(snk_dqn m, int64_t *P_out);
+/* Flux.destructure / restructure: which = SNK_NET_* */
+int snk_dqn_set_params(snk_dqn m, int32_t which, const float *flux_host);
+int snk_dqn_get_params(snk_dqn m, int32_t which, float *flux_host);
+/* device buffer (packed layout) of a SNK_NET_* vector; for
+ * data-parallel gradient all-reduce and target broadcast */
+int snk_dqn_buffer_ptr(snk_dqn m, int32_t which, float **packed_dev);
+/* update_target_net! (utils.jl:174-177) */
+int snk_dqn_sync_target(snk_dqn m);
+/* m(x): x_dev Float32 (bs,bs,C,B) Julia memory -> q_dev (3,B) */
+int snk_dqn_forward(snk_dqn m, int32_t which, const float *x_dev, int64_t B, float *q_dev);
+/* Q of every env's assemble_state! -> q_dev [n][3] */
+int snk_dqn_forward_env(snk_dqn m, int32_t which, snk_env env, float *q_dev);
+/* epsilon_greedy (utils.jl:153-172) for every env: act_dev [n] action index */
+int snk_dqn_act(snk_dqn m, snk_env env, float epsilon, uint64_t seed, uint8_t *act_dev);
+/* Q of the last forward_env/act call, host [n][3] */
+int snk_dqn_last_q(snk_dqn m, float *q_host, int64_t n);
+/* utils.jl:448-464: TD target on t_net (Float64, suicidal mask -> -100),
+ * Huber loss (delta 1, mean) and its gradient into SNK_NET_GRAD, for the
+ * replay slots idx_dev[B]. loss_host may be NULL (no synchronisation). */
+int snk_dqn_loss_grad(snk_dqn m, snk_replay rb, const int64_t *idx_dev, int64_t B, double gamma,
+                      double *loss_host);
+/* the same for explicit stack_exp tensors (actions 1-based, mask [B][3]) */
+int snk_dqn_loss_grad_batch(snk_dqn m, const float *states_dev, const int32_t *actions_dev,
+                            const float *rewards_dev, const float *next_states_dev, const uint8_t *dones_dev,
+                            const uint8_t *mask_dev, int64_t B, double gamma, double *loss_host);
+/* Flux.update!(opt_state, q_net, grads) with the SNK_NET_GRAD buffer (utils.jl:466) */
+int snk_dqn_apply_grad(snk_dqn m);
+/* loss_grad + apply_grad */
+int snk_dqn_update(snk_dqn m, snk_replay rb, const int64_t *idx_dev, int64_t B, double gamma,
+                   double *loss_host);
+
+/* ---------------------------------------------------------------- trainer
+ * The batched train! loop (utils.jl:420-494) over a batch of envs. */
+typedef struct snk_trainer_s *snk_trainer;
+typedef struct {
+    float epsilon;              /* structs.jl:206 epsilon = 1.0 */
+    float epsilon_end;          /* 0.05 */
+    float decay;                /* 1e-6, subtracted per update (utils.jl:480) */
+    int32_t updates_per_iter;   /* DQN updates per lockstep env step */
+    int64_t target_update_rate; /* 1000 (utils.jl:469) */
+    double gamma;               /* 0.97 (utils.jl:451) */
+    uint64_t seed;              /* counter-RNG seed for actions and sampling */
+    int64_t loss_log_capacity;  /* ring of per-update losses (tr.losses) */
+} snk_trainer_cfg_t;
+typedef struct {
+    int64_t episodes, score_sum, updates, env_steps;
+    double reward_sum, last_loss;
+    float reward_max;
+    int32_t score_max;
+    float epsilon;
+} snk_trainer_stats_t;
+
+int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn m, snk_replay rb, const snk_trainer_cfg_t *cfg);
+int snk_trainer_destroy(snk_trainer t);
+/* iters lockstep iterations; learn = 0 is fill_buffer! (utils.jl:389-402);
+ * use_graph = 1 replays one captured hipGraph per iteration */
+int snk_trainer_run(snk_trainer t, int64_t iters, int32_t learn, int32_t use_graph);
+int snk_trainer_stats(snk_trainer t, snk_trainer_stats_t *out);
+/* tr.losses: loss of update u at host[u % loss_log_capacity] */
+int snk_trainer_losses(snk_trainer t, double *host, int64_t n);
+int snk_trainer_act_ptr(snk_trainer t, uint8_t **act_dev);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,5 +11,8 @@ from .env import (ALL_ACTIONS, D, L, NULL_ACTION, R, U, SnakeGame, assemble_stat
                   step_indices_dev, synth_actions_dev, virtual_step)
 from .replay import (ReplayBuffer, empty_buffer_, isfull, isready, sample, stack_exp,  # noqa: F401
                      store_)
+from ._lib import SNK_NET_GRAD, SNK_NET_OPT_STATE, SNK_NET_Q, SNK_NET_TARGET  # noqa: F401
+from .qnet import DQNModel, nparams, update_target_net_  # noqa: F401
+from .trainer import Trainer, epsilon_greedy, fill_buffer_, play_episode, train_  # noqa: F401
 
 __version__ = "1.0.0"

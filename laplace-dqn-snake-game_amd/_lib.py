@@ -84,7 +84,46 @@ _PROTOS = {
     "snk_replay_empty": [vp],
     "snk_replay_sample": [vp, u64, u64, vp, P(i32)],
     "snk_replay_gather": [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp],
+    "snk_dqn_create": [P(vp), i32, i32, f32, f32, f32, u64],
+    "snk_dqn_destroy": [vp],
+    "snk_dqn_nparams": [vp, P(i64)],
+    "snk_dqn_set_params": [vp, i32, vp],
+    "snk_dqn_get_params": [vp, i32, vp],
+    "snk_dqn_buffer_ptr": [vp, i32, P(vp)],
+    "snk_dqn_sync_target": [vp],
+    "snk_dqn_forward": [vp, i32, vp, i64, vp],
+    "snk_dqn_forward_env": [vp, i32, vp, vp],
+    "snk_dqn_act": [vp, vp, f32, u64, vp],
+    "snk_dqn_last_q": [vp, vp, i64],
+    "snk_dqn_loss_grad": [vp, vp, vp, i64, f64, P(f64)],
+    "snk_dqn_loss_grad_batch": [vp, vp, vp, vp, vp, vp, vp, i64, f64, P(f64)],
+    "snk_dqn_apply_grad": [vp],
+    "snk_dqn_update": [vp, vp, vp, i64, f64, P(f64)],
+    "snk_trainer_create": [P(vp), vp, vp, vp, vp],
+    "snk_trainer_destroy": [vp],
+    "snk_trainer_run": [vp, i64, i32, i32],
+    "snk_trainer_stats": [vp, vp],
+    "snk_trainer_losses": [vp, vp, i64],
+    "snk_trainer_act_ptr": [vp, P(vp)],
 }
+
+SNK_NET_Q = 0
+SNK_NET_TARGET = 1
+SNK_NET_OPT_STATE = 2
+SNK_NET_GRAD = 3
+
+
+class TrainerCfg(C.Structure):
+    """snk_trainer_cfg_t"""
+    _fields_ = [("epsilon", f32), ("epsilon_end", f32), ("decay", f32), ("updates_per_iter", i32),
+                ("target_update_rate", i64), ("gamma", f64), ("seed", u64), ("loss_log_capacity", i64)]
+
+
+class TrainerStats(C.Structure):
+    """snk_trainer_stats_t"""
+    _fields_ = [("episodes", i64), ("score_sum", i64), ("updates", i64), ("env_steps", i64),
+                ("reward_sum", f64), ("last_loss", f64), ("reward_max", f32), ("score_max", i32),
+                ("epsilon", f32)]
 _RESTYPE = {"snk_last_error": C.c_char_p}
 
 

@@ -1,0 +1,31 @@
+// snk_dqn.hpp — DQNModel handle internals shared by snk_dqn.hip / snk_trainer.hip
+#pragma once
+#include "snk_qnet.hpp"
+
+struct snk_dqn_s {
+    snk::QLayout L{};
+    float lr = 5e-4f, rho = 0.9f, eps = 1e-8f;
+    float *theta_q = nullptr, *theta_t = nullptr, *acc = nullptr, *grad = nullptr, *tmp = nullptr;
+    int32_t *perm = nullptr;        // packed index -> Flux.destructure index
+    snk::QWork act, tgt, trn;       // workspaces: acting (n_envs), target net, training batch
+    float *slab = nullptr;
+    int64_t slab_cap = 0;
+    double *loss_dev = nullptr;
+    uint8_t *meta = nullptr;
+    int64_t meta_cap = 0;
+};
+
+namespace snk {
+const EnvDev &env_dev(snk_env h);
+const ReplayDev &replay_dev(snk_replay h);
+int32_t replay_batch(snk_replay h);
+void replay_launch_sample(const ReplayDev &d, int32_t batch, uint64_t seed, uint64_t draw,
+                          const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s);
+BoardSrc src_env(const EnvDev &E);
+BoardSrc src_replay(const ReplayDev &R, const int64_t *idx, int chan0);
+BoardSrc src_float(const QLayout &L, const float *x);
+void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, const HeadArgs &meta, int64_t B,
+                   double gamma, hipStream_t s);
+void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, hipStream_t s);
+void dqn_permute(snk_dqn_s *h, const float *src, float *dst, bool to_packed, hipStream_t s);
+}  // namespace snk

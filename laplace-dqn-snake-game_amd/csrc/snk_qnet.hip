@@ -1,0 +1,546 @@
+// snk_qnet.hip — Q-net forward / backward / RMSProp on gfx950.
+//
+// Forward (structs.jl:168-180 Chain): conv1 on VALU (K = 9*C is tiny), conv2,
+// conv3 and Dense1 as implicit GEMMs on v_mfma_f32_32x32x2_f32, then one
+// wave per sample for Dense2 with a mode-specific epilogue: epsilon_greedy
+// (utils.jl:153-172), the TD target (utils.jl:448-451) or the Huber loss and
+// its gradient (utils.jl:453-458). Backward (Zygote's gradient,
+// utils.jl:461-464) runs the same GEMM engine with data-gradient and
+// weight-gradient loaders; RMSProp (Optimisers.jl, utils.jl:429,466) is
+// element-wise over the packed parameter vector.
+#include <algorithm>
+#include <vector>
+
+#include "snk_qnet.hpp"
+
+namespace snk {
+
+// ---------------------------------------------------------------- layout
+QLayout make_layout(int bs, int C) {
+    QLayout L{};
+    L.bs = bs;
+    L.C = C;
+    L.ncell = bs * bs;
+    L.Wo = bs - 5;
+    L.K1 = L.Wo * L.Wo * 64;
+    int64_t o = 0;
+    L.off_w1 = o; o += 9 * C * 16;
+    L.off_b1 = o; o += 16;
+    L.off_w2 = o; o += 9 * 16 * 32;
+    L.off_b2 = o; o += 32;
+    L.off_w3 = o; o += 36 * 32 * 64;
+    L.off_b3 = o; o += 64;
+    L.off_d1w = o; o += (int64_t)L.K1 * 64;
+    L.off_d1b = o; o += 64;
+    L.off_d2w = o; o += 3 * 64;
+    L.off_d2b = o; o += 3;
+    L.P = o;
+    return L;
+}
+
+void packed_to_flux_index(const QLayout &L, int32_t *perm) {
+    auto conv = [&](int64_t off, int KS, int Cin, int Cout) {
+        // packed W[(kk*Cin + ci)*Cout + co], kk = du + KS*dv  <-  flux w[KS-1-du, KS-1-dv, ci, co]
+        for (int dv = 0; dv < KS; ++dv)
+            for (int du = 0; du < KS; ++du)
+                for (int ci = 0; ci < Cin; ++ci)
+                    for (int co = 0; co < Cout; ++co) {
+                        const int64_t pk = ((int64_t)(du + KS * dv) * Cin + ci) * Cout + co;
+                        const int64_t fx = (KS - 1 - du) + (int64_t)KS * (KS - 1 - dv) + (int64_t)KS * KS * ci +
+                                           (int64_t)KS * KS * Cin * co;
+                        perm[off + pk] = (int32_t)(off + fx);
+                    }
+        const int64_t boff = off + (int64_t)KS * KS * Cin * Cout;
+        for (int co = 0; co < Cout; ++co) perm[boff + co] = (int32_t)(boff + co);
+    };
+    conv(L.off_w1, 3, L.C, 16);
+    conv(L.off_w2, 3, 16, 32);
+    conv(L.off_w3, 6, 32, 64);
+    const int np = L.Wo * L.Wo;
+    // Dense1: packed W[p*64 + c][o] <- flux W[o, p + c*np] (Flux.flatten is column-major (i,j,c))
+    for (int p = 0; p < np; ++p)
+        for (int c = 0; c < 64; ++c)
+            for (int o = 0; o < 64; ++o)
+                perm[L.off_d1w + ((int64_t)p * 64 + c) * 64 + o] = (int32_t)(L.off_d1w + o + ((int64_t)p + (int64_t)c * np) * 64);
+    for (int o = 0; o < 64; ++o) perm[L.off_d1b + o] = (int32_t)(L.off_d1b + o);
+    // Dense2: packed W[a][o] <- flux W[a, o] (column-major a + 3o)
+    for (int a = 0; a < 3; ++a)
+        for (int o = 0; o < 64; ++o) perm[L.off_d2w + a * 64 + o] = (int32_t)(L.off_d2w + a + 3 * o);
+    for (int a = 0; a < 3; ++a) perm[L.off_d2b + a] = (int32_t)(L.off_d2b + a);
+}
+
+// ---------------------------------------------------------------- fast division
+struct FastDiv {  // n / d == (umulhi(n, m) + n) >> s for 0 <= n < 2^31
+    uint32_t d = 1, m = 1, s = 0;
+    FastDiv() = default;
+    explicit FastDiv(uint32_t dd) : d(dd) {
+        s = 0;
+        while ((1u << s) < d) ++s;
+        m = (uint32_t)(((((uint64_t)1) << 32) * ((((uint64_t)1) << s) - d)) / d + 1);
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> s; }
+};
+
+// ---------------------------------------------------------------- A loaders
+template <int CIN, int KS, int PAD>
+struct AConvFwd {  // row m=(s,pout), k=(kk,ci): x[s][pin][ci]
+    const float *x;
+    int H, HO;
+    FastDiv dHO2, dHO;
+    struct Ctx { const float *xs; int i, j; bool ok; };
+    __device__ Ctx row(int m, int M) const {
+        Ctx c;
+        c.ok = m < M;
+        const int mm = c.ok ? m : 0;
+        const int s = (int)dHO2.div(mm);
+        const int p = mm - s * HO * HO;
+        c.j = (int)dHO.div(p);
+        c.i = p - c.j * HO;
+        c.xs = x + (int64_t)s * H * H * CIN;
+        return c;
+    }
+    __device__ __forceinline__ float load(const Ctx &c, int k, int) const {
+        const int kk = k / CIN, ci = k - kk * CIN;
+        const int dv = kk / KS, du = kk - dv * KS;
+        const int xi = c.i + du - PAD, xj = c.j + dv - PAD;
+        return (c.ok && xi >= 0 && xi < H && xj >= 0 && xj < H) ? c.xs[(xi + xj * H) * CIN + ci] : 0.0f;
+    }
+};
+
+template <int COUT, int KS, int PAD>
+struct AConvDx {  // row m=(s,pin), k=(kk,co): dz[s][pout = pin - (du,dv) + PAD][co]
+    const float *dz;
+    int H, HO;
+    FastDiv dH2, dH;
+    struct Ctx { const float *zs; int i, j; bool ok; };
+    __device__ Ctx row(int m, int M) const {
+        Ctx c;
+        c.ok = m < M;
+        const int mm = c.ok ? m : 0;
+        const int s = (int)dH2.div(mm);
+        const int p = mm - s * H * H;
+        c.j = (int)dH.div(p);
+        c.i = p - c.j * H;
+        c.zs = dz + (int64_t)s * HO * HO * COUT;
+        return c;
+    }
+    __device__ __forceinline__ float load(const Ctx &c, int k, int) const {
+        const int kk = k / COUT, co = k - kk * COUT;
+        const int dv = kk / KS, du = kk - dv * KS;
+        const int oi = c.i - du + PAD, oj = c.j - dv + PAD;
+        return (c.ok && oi >= 0 && oi < HO && oj >= 0 && oj < HO) ? c.zs[(oi + oj * HO) * COUT + co] : 0.0f;
+    }
+};
+
+template <int CIN, int KS, int PAD>
+struct AConvDw {  // row m=(kk,ci) (m == KS*KS*CIN: bias row of ones), k = r = (s,pout)
+    const float *x;
+    int H, HO;
+    int64_t R;
+    FastDiv dHO2, dHO;
+    struct Ctx { int du, dv, ci; bool ok, bias; };
+    __device__ Ctx row(int m, int M) const {
+        Ctx c;
+        c.ok = m < M;
+        c.bias = m == KS * KS * CIN;
+        const int kk = m / CIN;
+        c.ci = m - kk * CIN;
+        c.dv = kk / KS;
+        c.du = kk - c.dv * KS;
+        return c;
+    }
+    __device__ __forceinline__ float load(const Ctx &c, int k, int) const {
+        if (!c.ok || k >= R) return 0.0f;
+        if (c.bias) return 1.0f;
+        const int s = (int)dHO2.div(k);
+        const int p = k - s * HO * HO;
+        const int j = (int)dHO.div(p), i = p - j * HO;
+        const int xi = i + c.du - PAD, xj = j + c.dv - PAD;
+        return (xi >= 0 && xi < H && xj >= 0 && xj < H) ? x[((int64_t)s * H * H + xi + xj * H) * CIN + c.ci] : 0.0f;
+    }
+};
+
+struct ABoardDw {  // conv1 weight gradient: row m=(kk,c) (+bias row), k = r = (s,p)
+    BoardSrc src;
+    int bs, C;
+    int64_t R;
+    FastDiv dN, dB;
+    struct Ctx { int du, dv, c; bool ok, bias; };
+    __device__ Ctx row(int m, int M) const {
+        Ctx x;
+        x.ok = m < M;
+        x.bias = m == 9 * C;
+        const int kk = m / C;
+        x.c = m - kk * C;
+        x.dv = kk / 3;
+        x.du = kk - x.dv * 3;
+        return x;
+    }
+    __device__ __forceinline__ float load(const Ctx &x, int k, int) const {
+        if (!x.ok || k >= R) return 0.0f;
+        if (x.bias) return 1.0f;
+        const int s = (int)dN.div(k);
+        const int p = k - s * bs * bs;
+        const int j = (int)dB.div(p), i = p - j * bs;
+        const int xi = i + x.du - 1, xj = j + x.dv - 1;
+        return (xi >= 0 && xi < bs && xj >= 0 && xj < bs) ? src.load(s, x.c, xi + xj * bs) : 0.0f;
+    }
+};
+
+struct ARowMajor {  // A[m][k] = a[m*ld + k]
+    const float *a;
+    int K, ld;
+    struct Ctx { const float *p; bool ok; };
+    __device__ Ctx row(int m, int M) const { return Ctx{a + (int64_t)(m < M ? m : 0) * ld, m < M}; }
+    __device__ __forceinline__ float load(const Ctx &c, int k, int) const { return (c.ok && k < K) ? c.p[k] : 0.0f; }
+};
+
+struct ADenseDw {  // row m = input feature (m == KW: bias ones), k = sample r: a[r*KW + m]
+    const float *a;
+    int KW;
+    int64_t R;
+    struct Ctx { int m; bool ok, bias; };
+    __device__ Ctx row(int m, int M) const { return Ctx{m, m < M, m == KW}; }
+    __device__ __forceinline__ float load(const Ctx &c, int k, int) const {
+        if (!c.ok || k >= R) return 0.0f;
+        return c.bias ? 1.0f : a[(int64_t)k * KW + c.m];
+    }
+};
+
+// ---------------------------------------------------------------- launch helpers
+static void choose_split(int64_t waves, int64_t K, int &ks, int &kchunk) {
+    const int64_t target = 2048;
+    int64_t want = std::max<int64_t>(1, target / std::max<int64_t>(1, waves));
+    const int64_t maxks = std::max<int64_t>(1, K / 64);
+    int64_t k = std::min(want, maxks);
+    int64_t chunk = (K + k - 1) / k;
+    chunk = (chunk + 1) & ~int64_t(1);
+    ks = (int)((K + chunk - 1) / chunk);
+    kchunk = (int)chunk;
+}
+
+template <int NT, class AL, class BL, class EP>
+static void gemm(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int64_t K, int ks, int kchunk,
+                 hipStream_t s) {
+    dim3 grid((unsigned)ceil_div(M, 128), (unsigned)ceil_div(N, NT * 32), (unsigned)ks);
+    gemm_kernel<NT><<<grid, 256, 0, s>>>(al, bl, ep, (int)M, (int)K, kchunk);
+    launch_check("gemm_kernel");
+}
+
+// ---------------------------------------------------------------- conv1 (VALU)
+template <int C>
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(BoardSrc src, const float *__restrict__ w,
+                                                        const float *__restrict__ b, float *__restrict__ y,
+                                                        int64_t S, int bs) {
+    __shared__ float sw[9 * C * 16 + 16];
+    for (int i = threadIdx.x; i < 9 * C * 16; i += blockDim.x) sw[i] = w[i];
+    if (threadIdx.x < 16) sw[9 * C * 16 + threadIdx.x] = b[threadIdx.x];
+    __syncthreads();
+    const int ncell = bs * bs;
+    const int64_t total = S * ncell;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = q / ncell;
+        const int p = (int)(q - s * ncell);
+        const int j = p / bs, i = p - j * bs;
+        float acc[16];
+#pragma unroll
+        for (int co = 0; co < 16; ++co) acc[co] = sw[9 * C * 16 + co];
+#pragma unroll
+        for (int kk = 0; kk < 9; ++kk) {
+            const int du = kk % 3, dv = kk / 3;
+            const int xi = i + du - 1, xj = j + dv - 1;
+            if (xi < 0 || xi >= bs || xj < 0 || xj >= bs) continue;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const float v = src.load(s, c, xi + xj * bs);
+#pragma unroll
+                for (int co = 0; co < 16; ++co) acc[co] = __builtin_fmaf(v, sw[(kk * C + c) * 16 + co], acc[co]);
+            }
+        }
+        float4 *o = reinterpret_cast<float4 *>(y + q * 16);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            o[v] = make_float4(fmaxf(acc[4 * v], 0.f), fmaxf(acc[4 * v + 1], 0.f), fmaxf(acc[4 * v + 2], 0.f),
+                               fmaxf(acc[4 * v + 3], 0.f));
+    }
+}
+
+// ---------------------------------------------------------------- heads
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ slab, int ks, int64_t S,
+                                                   const float *__restrict__ theta, QLayout L,
+                                                   float *__restrict__ h1o, float *__restrict__ qo, HeadArgs ha) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= S) return;
+    float h = theta[L.off_d1b + lane];
+    for (int z = 0; z < ks; ++z) h += slab[((int64_t)z * S + s) * 64 + lane];
+    h = h > 0.0f ? h : 0.0f;
+    h1o[s * 64 + lane] = h;
+    float q[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) q[a] = theta[L.off_d2b + a] + wave_sum(theta[L.off_d2w + a * 64 + lane] * h);
+    if (lane != 0) return;
+    qo[s * 3 + 0] = q[0];
+    qo[s * 3 + 1] = q[1];
+    qo[s * 3 + 2] = q[2];
+    if (MODE == HEAD_ACT) {
+        // utils.jl:161-169: Float32(rand()) < epsilon ? rand(av) : av[argmax(Q)]
+        const uint64_t t = *ha.tptr;
+        const float eps = ha.eps_dev ? *ha.eps_dev : ha.epsilon;
+        const float u = rng_uniform(rng_hash(ha.seed, (uint64_t)s, t));
+        int a;
+        if (u < eps) {
+            a = (int)((rng_hash(ha.seed ^ 0xA5A5A5A5A5A5A5A5ULL, (uint64_t)s, t) >> 32) % 3);
+        } else {
+            a = 0;  // argmax: first maximum
+            if (q[1] > q[a]) a = 1;
+            if (q[2] > q[a]) a = 2;
+        }
+        ha.act[s] = (uint8_t)a;
+    } else if (MODE == HEAD_TARGET) {
+        // utils.jl:448-451 (Float64 promotion of the 0.97 literal)
+        const int64_t m = ha.idx ? ha.idx[s] : s;
+        const uint8_t mk = ha.mask[m];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float v = ((mk >> a) & 1) ? -100.0f : q[a];
+            mx = v > mx ? v : mx;
+        }
+        ha.target[s] = (double)ha.rew[m] + ha.gamma * (double)mx * (double)(1 - (int)ha.done[m]);
+    } else if (MODE == HEAD_LOSS) {
+        // utils.jl:453-458 Flux.huber_loss(delta = 1, agg = mean), its gradient
+        const int64_t m = ha.idx ? ha.idx[s] : s;
+        const int a = ha.act_idx[m] % 3;
+        const double e = (double)q[a] - ha.target[s];
+        const double ae = fabs(e);
+        ha.loss[s] = ae < 1.0 ? 0.5 * e * e : ae - 0.5;
+        const double g = (ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / (double)ha.B;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ha.dq[s * 3 + k] = k == a ? (float)g : 0.0f;
+    }
+}
+
+// backward of Dense2 + relu: dz1[s][o] = (h1 > 0) * sum_a dq[s][a] W2[a][o]
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float *__restrict__ dq, const float *__restrict__ h1,
+                                                       const float *__restrict__ theta, QLayout L, int64_t S,
+                                                       float *__restrict__ dz1) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= S) return;
+    const float *w2 = theta + L.off_d2w;
+    const float g = dq[s * 3] * w2[lane] + dq[s * 3 + 1] * w2[64 + lane] + dq[s * 3 + 2] * w2[128 + lane];
+    dz1[s * 64 + lane] = h1[s * 64 + lane] > 0.0f ? g : 0.0f;
+}
+
+// Dense2 weight/bias gradient: 195 outputs, reduction over S
+__global__ void d2_grad_kernel(const float *__restrict__ dq, const float *__restrict__ h1, int64_t S, QLayout L,
+                               float *__restrict__ grad) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 195) return;
+    float acc = 0.0f;
+    if (t < 192) {
+        const int a = t / 64, o = t - a * 64;
+        for (int64_t s = 0; s < S; ++s) acc = __builtin_fmaf(dq[s * 3 + a], h1[s * 64 + o], acc);
+        grad[L.off_d2w + t] = acc;
+    } else {
+        const int a = t - 192;
+        for (int64_t s = 0; s < S; ++s) acc += dq[s * 3 + a];
+        grad[L.off_d2b + a] = acc;
+    }
+}
+
+__global__ void slab_reduce_kernel(const float *__restrict__ slab, int ks, int64_t MN, float *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += (int64_t)gridDim.x * blockDim.x) {
+        float v = 0.0f;
+        for (int z = 0; z < ks; ++z) v += slab[(int64_t)z * MN + i];
+        out[i] = v;
+    }
+}
+
+__global__ void rmsprop_kernel(int64_t P, float *__restrict__ theta, float *__restrict__ acc,
+                               const float *__restrict__ grad, float eta, float rho, float eps) {
+    const float omr = 1.0f - rho;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+        const float g = grad[i];
+        const float qd = rho * acc[i] + omr * (g * g);
+        acc[i] = qd;
+        theta[i] = theta[i] - (g * eta) / (__fsqrt_rn(qd) + eps);
+    }
+}
+
+__global__ void loss_mean_kernel(const double *__restrict__ loss, int64_t B, double *__restrict__ out) {
+    __shared__ double sh[256];
+    double v = 0.0;
+    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) v += loss[i];
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = sh[0] / (double)B;
+}
+
+// ---------------------------------------------------------------- workspace
+void qwork_free(QWork &w) {
+    for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a3, (void *)w.slab, (void *)w.h1, (void *)w.q,
+                    (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.target,
+                    (void *)w.loss})
+        dfree(p);
+    w = QWork{};
+}
+
+static int d1_split(const QLayout &L, int64_t S, int &kchunk) {
+    int ks;
+    choose_split(ceil_div(S, 32), L.K1, ks, kchunk);
+    return ks;
+}
+
+void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
+    int kc;
+    const int64_t need_slab = (int64_t)d1_split(L, S, kc) * S * 64;
+    if (S <= w.cap && need_slab <= w.slab_floats && (!train || w.has_train)) return;
+    (void)hipStreamSynchronize(stream());
+    const int64_t cap = std::max(S, w.cap);
+    const int64_t slab = std::max({need_slab, w.slab_floats, (int64_t)d1_split(L, cap, kc) * cap * 64});
+    const bool tr = train || w.has_train;
+    qwork_free(w);
+    w.cap = cap;
+    w.slab_floats = slab;
+    w.a1 = dalloc<float>((size_t)cap * L.ncell * 16);
+    w.a2 = dalloc<float>((size_t)cap * L.ncell * 32);
+    w.a3 = dalloc<float>((size_t)cap * L.K1);
+    w.slab = dalloc<float>((size_t)slab);
+    w.h1 = dalloc<float>((size_t)cap * 64);
+    w.q = dalloc<float>((size_t)cap * 3);
+    if (tr) {
+        w.has_train = 1;
+        w.dq = dalloc<float>((size_t)cap * 3);
+        w.dz1 = dalloc<float>((size_t)cap * 64);
+        w.dz3 = dalloc<float>((size_t)cap * L.K1);
+        w.dz2 = dalloc<float>((size_t)cap * L.ncell * 32);
+        w.dzc1 = dalloc<float>((size_t)cap * L.ncell * 16);
+        w.target = dalloc<double>(cap);
+        w.loss = dalloc<double>(cap);
+    }
+}
+
+// ---------------------------------------------------------------- forward
+void qnet_forward(const QLayout &L, const float *th, const BoardSrc &src, int64_t S, QWork &w, HeadMode mode,
+                  const HeadArgs &ha, hipStream_t s) {
+    const int bs = L.bs, nc = L.ncell;
+    {
+        const int64_t total = S * nc;
+        const int grid = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
+        if (L.C == 1)
+            conv1_fwd_kernel<1><<<grid, 256, 0, s>>>(src, th + L.off_w1, th + L.off_b1, w.a1, S, bs);
+        else
+            conv1_fwd_kernel<2><<<grid, 256, 0, s>>>(src, th + L.off_w1, th + L.off_b1, w.a1, S, bs);
+        launch_check("conv1_fwd_kernel");
+    }
+    {   // conv2: M = S*bs^2, K = 9*16, N = 32
+        AConvFwd<16, 3, 1> al{w.a1, bs, bs, FastDiv(nc), FastDiv(bs)};
+        gemm<1>(al, BRowMajor{th + L.off_w2, 144, 32}, EpBiasRelu{w.a2, th + L.off_b2, (int)(S * nc), 32, 1},
+                S * nc, 32, 144, 1, 144, s);
+    }
+    {   // conv3: M = S*Wo^2, K = 36*32, N = 64
+        const int no = L.Wo * L.Wo;
+        AConvFwd<32, 6, 0> al{w.a2, bs, L.Wo, FastDiv(no), FastDiv(L.Wo)};
+        gemm<2>(al, BRowMajor{th + L.off_w3, 1152, 64}, EpBiasRelu{w.a3, th + L.off_b3, (int)(S * no), 64, 1},
+                S * no, 64, 1152, 1, 1152, s);
+    }
+    int kc;
+    const int ks = d1_split(L, S, kc);
+    // Dense1 (split-K partial sums; bias + relu in the head)
+    gemm<2>(ARowMajor{w.a3, L.K1, L.K1}, BRowMajor{th + L.off_d1w, L.K1, 64}, EpSlab{w.slab, (int)S, 64}, S, 64,
+            L.K1, ks, kc, s);
+    const int grid = ceil_div(S, 4);
+    switch (mode) {
+        case HEAD_Q: head_kernel<HEAD_Q><<<grid, 256, 0, s>>>(w.slab, ks, S, th, L, w.h1, w.q, ha); break;
+        case HEAD_ACT: head_kernel<HEAD_ACT><<<grid, 256, 0, s>>>(w.slab, ks, S, th, L, w.h1, w.q, ha); break;
+        case HEAD_TARGET: head_kernel<HEAD_TARGET><<<grid, 256, 0, s>>>(w.slab, ks, S, th, L, w.h1, w.q, ha); break;
+        case HEAD_LOSS: head_kernel<HEAD_LOSS><<<grid, 256, 0, s>>>(w.slab, ks, S, th, L, w.h1, w.q, ha); break;
+    }
+    launch_check("head_kernel");
+}
+
+// ---------------------------------------------------------------- backward
+struct BwdPlan {
+    int ks_d1, kc_d1, ks_c3, kc_c3, ks_c2, kc_c2, ks_c1, kc_c1;
+};
+static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
+    BwdPlan p;
+    choose_split(ceil_div(L.K1 + 1, 32), S, p.ks_d1, p.kc_d1);
+    choose_split(ceil_div(1153, 32) * 1, S * L.Wo * L.Wo, p.ks_c3, p.kc_c3);
+    choose_split(ceil_div(145, 32), S * L.ncell, p.ks_c2, p.kc_c2);
+    choose_split(ceil_div(9 * L.C + 1, 32), S * L.ncell, p.ks_c1, p.kc_c1);
+    return p;
+}
+int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S) {
+    const BwdPlan p = bwd_plan(L, S);
+    int64_t m = (int64_t)p.ks_d1 * (L.K1 + 1) * 64;
+    m = std::max(m, (int64_t)p.ks_c3 * 1153 * 64);
+    m = std::max(m, (int64_t)p.ks_c2 * 145 * 32);
+    m = std::max(m, (int64_t)p.ks_c1 * (9 * L.C + 1) * 16);
+    return m;
+}
+
+static void reduce_into(const float *slab, int ks, int64_t MN, float *out, hipStream_t s) {
+    slab_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(MN, 256), 2048), 256, 0, s>>>(slab, ks, MN, out);
+    launch_check("slab_reduce_kernel");
+}
+
+void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64_t S, QWork &w, float *grad,
+                   float *slab, int64_t slab_cap, hipStream_t s) {
+    const BwdPlan p = bwd_plan(L, S);
+    SNK_CHECK(slab_cap >= qnet_backward_slab_floats(L, S), SNK_ERR_INTERNAL, "backward slab too small");
+    const int bs = L.bs, nc = L.ncell, no = L.Wo * L.Wo;
+    head_bwd_kernel<<<ceil_div(S, 4), 256, 0, s>>>(w.dq, w.h1, th, L, S, w.dz1);
+    launch_check("head_bwd_kernel");
+    d2_grad_kernel<<<1, 256, 0, s>>>(w.dq, w.h1, S, L, grad);
+    launch_check("d2_grad_kernel");
+    // Dense1: dW (+ bias row) and dX (relu mask on a3)
+    gemm<2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, EpSlab{slab, L.K1 + 1, 64}, L.K1 + 1, 64, S, p.ks_d1,
+            p.kc_d1, s);
+    reduce_into(slab, p.ks_d1, (int64_t)(L.K1 + 1) * 64, grad + L.off_d1w, s);
+    gemm<2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + L.off_d1w, 64, L.K1, 64}, EpReluMask{w.dz3, w.a3, (int)S, L.K1},
+            S, L.K1, 64, 1, 64, s);
+    // conv3: dW over rows (s, pout); dX onto the 12x12x32 input (relu mask on a2)
+    gemm<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64},
+            EpSlab{slab, 1153, 64}, 1153, 64, S * no, p.ks_c3, p.kc_c3, s);
+    reduce_into(slab, p.ks_c3, 1153 * 64, grad + L.off_w3, s);
+    gemm<1>(AConvDx<64, 6, 0>{w.dz3, bs, L.Wo, FastDiv(nc), FastDiv(bs)}, BConvT<32, 64>{th + L.off_w3, 2304},
+            EpReluMask{w.dz2, w.a2, (int)(S * nc), 32}, S * nc, 32, 2304, 1, 2304, s);
+    // conv2
+    gemm<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32},
+            EpSlab{slab, 145, 32}, 145, 32, S * nc, p.ks_c2, p.kc_c2, s);
+    reduce_into(slab, p.ks_c2, 145 * 32, grad + L.off_w2, s);
+    gemm<1>(AConvDx<32, 3, 1>{w.dz2, bs, bs, FastDiv(nc), FastDiv(bs)}, BConvT<16, 32>{th + L.off_w2, 288},
+            EpReluMask{w.dzc1, w.a1, (int)(S * nc), 16}, S * nc, 16, 288, 1, 288, s);
+    // conv1 (weights only)
+    gemm<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
+            EpSlab{slab, 9 * L.C + 1, 16}, 9 * L.C + 1, 16, S * nc, p.ks_c1, p.kc_c1, s);
+    reduce_into(slab, p.ks_c1, (int64_t)(9 * L.C + 1) * 16, grad + L.off_w1, s);
+}
+
+void rmsprop_launch(int64_t P, float *theta, float *acc, const float *grad, float eta, float rho, float eps,
+                    hipStream_t s) {
+    rmsprop_kernel<<<(unsigned)std::min<int64_t>(ceil_div(P, 256), 2048), 256, 0, s>>>(P, theta, acc, grad, eta,
+                                                                                        rho, eps);
+    launch_check("rmsprop_kernel");
+}
+
+void loss_mean_launch(const double *loss, int64_t B, double *out, hipStream_t s) {
+    loss_mean_kernel<<<1, 256, 0, s>>>(loss, B, out);
+    launch_check("loss_mean_kernel");
+}
+
+}  // namespace snk

@@ -1,0 +1,98 @@
+// snk_qnet.hpp — the DQNModel Q-net on the device (structs.jl:161-180).
+//
+//   Conv(3x3, C=>16, relu, pad 1) -> Conv(3x3, 16=>32, relu, pad 1)
+//   -> Conv(6x6, 32=>64, relu) -> flatten -> Dense(64*(bs-5)^2 => 64, relu)
+//   -> Dense(64 => 3)
+//
+// Parameters live on the device in a PACKED order (a per-section permutation
+// of Flux.destructure's order, same section sizes and offsets): each conv
+// weight is the GEMM matrix W[k][co] with k = (kk*Cin + ci), kk = du + KS*dv
+// the input offset of a TRUE convolution (Flux flips the kernel:
+// W[kk][ci][co] = w_flux[KS-1-du, KS-1-dv, ci, co]), immediately followed by
+// its bias (so a weight-gradient GEMM with an extra all-ones row writes
+// weight and bias gradients as one contiguous block); Dense1 is
+// W[p*64 + c][o] matching the device activation layout [s][p][c].
+// Activations: [sample][position p = i + j*H (column-major)][channel].
+#pragma once
+#include "snk_gemm.hpp"
+#include "snk_internal.hpp"
+
+namespace snk {
+
+struct QLayout {
+    int bs, C, ncell, Wo, K1;   // K1 = Wo*Wo*64 (Dense1 fan-in)
+    int64_t off_w1, off_b1, off_w2, off_b2, off_w3, off_b3, off_d1w, off_d1b, off_d2w, off_d2b, P;
+};
+QLayout make_layout(int bs, int C);
+// flux index of every packed index (host)
+void packed_to_flux_index(const QLayout &L, int32_t *perm);
+
+// Source of the Q-net input planes: env frame ring, replay slots, or a
+// float tensor in Julia (bs,bs,C,B) memory.
+struct BoardSrc {
+    const int8_t *base = nullptr;
+    const float *fbase = nullptr;
+    const int64_t *idx = nullptr;   // replay slot per sample
+    const int64_t *tptr = nullptr;  // env frame-ring step counter
+    int pitch = 0, C = 1, ncell = 0, chan0 = 0, replay_nf = 0;
+    __device__ __forceinline__ float load(int64_t s, int c, int cell) const {
+        if (fbase) return fbase[(s * C + c) * ncell + cell];
+        const int8_t *p;
+        if (idx) {
+            p = base + idx[s] * (int64_t)replay_nf * pitch + (int64_t)(c + chan0) * pitch;
+        } else {
+            const int64_t t = *tptr;
+            const int slot = (int)((t + 3 - (C - 1 - c)) % 3);
+            p = base + (s * 3 + slot) * (int64_t)pitch;
+        }
+        return (float)p[cell];
+    }
+};
+
+// Device workspace for one batch geometry
+struct QWork {
+    int64_t cap = 0, slab_floats = 0;
+    float *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *slab = nullptr, *h1 = nullptr, *q = nullptr;
+    // training only
+    float *dq = nullptr, *dz1 = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dzc1 = nullptr;
+    double *target = nullptr, *loss = nullptr;
+    int has_train = 0;
+};
+
+void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train);
+void qwork_free(QWork &w);
+
+// Head epilogues
+enum HeadMode { HEAD_Q = 0, HEAD_ACT = 1, HEAD_TARGET = 2, HEAD_LOSS = 3 };
+struct HeadArgs {
+    // ACT
+    uint8_t *act = nullptr;
+    float epsilon = 0.0f;
+    uint64_t seed = 0;
+    const int64_t *tptr = nullptr;
+    const float *eps_dev = nullptr;   // if set, epsilon read from the device
+    // TARGET / LOSS (replay metadata by slot)
+    const int64_t *idx = nullptr;
+    const float *rew = nullptr;
+    const uint8_t *done = nullptr;
+    const uint8_t *mask = nullptr;
+    const uint8_t *act_idx = nullptr;
+    double gamma = 0.97;
+    double *target = nullptr;
+    double *loss = nullptr;
+    float *dq = nullptr;
+    int64_t B = 0;
+};
+
+// forward: q[S][3] into w.q (and w.h1); mode-specific epilogue
+void qnet_forward(const QLayout &L, const float *theta, const BoardSrc &src, int64_t S, QWork &w,
+                  HeadMode mode, const HeadArgs &ha, hipStream_t s);
+// backward of the loss whose dq sits in w.dq (after HEAD_LOSS): grad (packed) overwritten
+void qnet_backward(const QLayout &L, const float *theta, const BoardSrc &src, int64_t S, QWork &w,
+                   float *grad, float *slab, int64_t slab_cap, hipStream_t s);
+int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S);
+void rmsprop_launch(int64_t P, float *theta, float *acc, const float *grad, float eta, float rho, float eps,
+                    hipStream_t s);
+void loss_mean_launch(const double *loss, int64_t B, double *out, hipStream_t s);
+
+}  // namespace snk

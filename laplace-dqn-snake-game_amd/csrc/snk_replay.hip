@@ -46,8 +46,9 @@ __global__ void replay_gather_kernel(ReplayDev R, const int64_t *__restrict__ id
 // Floyd's algorithm: a uniformly random B-subset of [0, len). One wave; lane 0
 // draws sequentially against an open-addressing set in LDS.
 __global__ void replay_sample_kernel(const int64_t *__restrict__ count, int64_t cap, int32_t batch,
-                                     uint64_t seed, uint64_t draw, int64_t *__restrict__ out,
-                                     int32_t *__restrict__ b_out) {
+                                     uint64_t seed, uint64_t draw, const int64_t *__restrict__ draw_dev,
+                                     int64_t *__restrict__ out, int32_t *__restrict__ b_out) {
+    if (draw_dev) draw = (uint64_t)*draw_dev;
     constexpr int HS = 8192;
     __shared__ int64_t set[HS];
     const int64_t len = min(*count, cap);
@@ -242,8 +243,8 @@ extern "C" int snk_replay_empty(snk_replay h) {
 
 namespace snk {
 void replay_launch_sample(const ReplayDev &d, int32_t batch, uint64_t seed, uint64_t draw,
-                          int64_t *idx, int32_t *b_dev, hipStream_t s) {
-    replay_sample_kernel<<<1, 64, 0, s>>>(d.count, d.cap, batch, seed, draw, idx, b_dev);
+                          const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s) {
+    replay_sample_kernel<<<1, 64, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev);
     launch_check("replay_sample_kernel");
 }
 }  // namespace snk
@@ -255,7 +256,7 @@ extern "C" int snk_replay_sample(snk_replay h, uint64_t seed, uint64_t draw, int
         int64_t len = 0;
         if (snk_replay_length(h, &len) != SNK_OK) throw Error{SNK_ERR_HIP};
         SNK_CHECK(len > 0, SNK_ERR_STATE, "cannot sample an empty buffer");
-        replay_launch_sample(h->d, h->batch_size, seed, draw, idx_dev, nullptr, stream());
+        replay_launch_sample(h->d, h->batch_size, seed, draw, nullptr, idx_dev, nullptr, stream());
         if (B_out) *B_out = (int32_t)std::min<int64_t>(h->batch_size, len);
         SNK_HIP(hipStreamSynchronize(stream()));
     });

@@ -1,0 +1,264 @@
+// snk_trainer.hip — the batched train! loop (utils.jl:420-494) on the device.
+//
+// One iteration = one lockstep step of every env:
+//   epsilon_greedy over all envs (Q forward + head)  (utils.jl:153-172)
+//   step! + virtual_step + store!                    (utils.jl:100-132, 267-277)
+//   episode statistics of finished games             (utils.jl:478)
+//   `updates_per_iter` DQN updates: sample, TD target, Huber, backward,
+//   RMSProp, update_target_net! at nb % rate == 0, epsilon decay
+//                                                    (utils.jl:442-481)
+// Every counter the loop needs (env step, replay count, update count,
+// epsilon) lives in device memory, so an iteration is a fixed launch sequence
+// that is captured once into a hipGraph and replayed.
+#include <algorithm>
+#include <vector>
+
+#include "snk_dqn.hpp"
+
+namespace snk {
+
+struct alignas(16) TrainStats {
+    int64_t episodes;      // finished episodes
+    int64_t score_sum;
+    int64_t updates;       // nb (utils.jl:431)
+    int64_t env_steps;
+    double reward_sum;     // sum of finished episode rewards
+    double last_loss;
+    float reward_max;
+    int32_t score_max;
+    float epsilon;         // tr.epsilon (utils.jl:480)
+    int32_t pad;
+};
+
+__global__ __launch_bounds__(1024) void episode_stats_kernel(const uint8_t *__restrict__ done,
+                                                             const float *__restrict__ ep_reward,
+                                                             const uint8_t *__restrict__ score, int64_t n,
+                                                             TrainStats *st) {
+    __shared__ double s_r[1024];
+    __shared__ int64_t s_n[1024], s_s[1024];
+    __shared__ float s_m[1024];
+    __shared__ int32_t s_sm[1024];
+    double r = 0.0;
+    int64_t cnt = 0, ssum = 0;
+    float mx = -INFINITY;
+    int32_t smx = 0;
+    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
+        if (done[e]) {
+            const float v = ep_reward[e];
+            r += (double)v;
+            cnt += 1;
+            ssum += score[e];
+            mx = fmaxf(mx, v);
+            smx = max(smx, (int32_t)score[e]);
+        }
+    }
+    const int t = threadIdx.x;
+    s_r[t] = r; s_n[t] = cnt; s_s[t] = ssum; s_m[t] = mx; s_sm[t] = smx;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (t < o) {
+            s_r[t] += s_r[t + o];
+            s_n[t] += s_n[t + o];
+            s_s[t] += s_s[t + o];
+            s_m[t] = fmaxf(s_m[t], s_m[t + o]);
+            s_sm[t] = max(s_sm[t], s_sm[t + o]);
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        st->episodes += s_n[0];
+        st->reward_sum += s_r[0];
+        st->score_sum += s_s[0];
+        if (s_n[0] > 0) {
+            st->reward_max = fmaxf(st->reward_max, s_m[0]);
+            st->score_max = max(st->score_max, s_sm[0]);
+        }
+        st->env_steps += n;
+    }
+}
+
+__global__ void post_update_kernel(TrainStats *st, const double *loss, double *log, int64_t log_cap, float decay,
+                                   float eps_end) {
+    if (threadIdx.x != 0) return;
+    const double l = *loss;
+    st->last_loss = l;
+    if (log) log[st->updates % log_cap] = l;          // track_loss! (utils.jl:404-406)
+    st->epsilon = fmaxf(st->epsilon - decay, eps_end); // utils.jl:480
+    st->updates += 1;
+}
+
+}  // namespace snk
+
+using namespace snk;
+
+struct snk_trainer_s {
+    snk_env env = nullptr;
+    snk_dqn dqn = nullptr;
+    snk_replay rb = nullptr;
+    snk_trainer_cfg_t cfg{};
+    TrainStats *stats = nullptr;
+    uint8_t *act = nullptr;
+    int64_t *idx = nullptr;
+    double *loss_log = nullptr;
+    int64_t log_cap = 0;
+    int32_t B = 64;
+    hipGraph_t graph[2] = {nullptr, nullptr};
+    hipGraphExec_t exec[2] = {nullptr, nullptr};
+    hipStream_t graph_stream = nullptr;
+};
+
+// One iteration's launch sequence (capturable: no host sync, no allocation)
+static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
+    const EnvDev &E = env_dev(h->env);
+    const ReplayDev &R = replay_dev(h->rb);
+    snk_dqn_s *q = h->dqn;
+    HeadArgs ha;
+    ha.act = h->act;
+    ha.seed = h->cfg.seed;
+    ha.tptr = &E.ctl->t;
+    ha.eps_dev = &h->stats->epsilon;
+    qnet_forward(q->L, q->theta_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s);
+    env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s);
+    env_launch_advance(E, &R, s);
+    episode_stats_kernel<<<1, 1024, 0, s>>>(E.out_done, E.out_ep_reward, E.out_score, E.n, h->stats);
+    launch_check("episode_stats_kernel");
+    if (!learn) return;
+    for (int u = 0; u < h->cfg.updates_per_iter; ++u) {
+        replay_launch_sample(R, h->B, h->cfg.seed ^ 0x5A4D504C45ULL, 0, &h->stats->updates, h->idx, nullptr, s);
+        HeadArgs m;
+        m.idx = h->idx;
+        m.rew = R.reward;
+        m.done = R.done;
+        m.mask = R.mask;
+        m.act_idx = R.act;
+        dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s);
+        rmsprop_launch(q->L.P, q->theta_q, q->acc, q->grad, q->lr, q->rho, q->eps, s);
+        dqn_sync_target_launch(q, &h->stats->updates, h->cfg.target_update_rate, s);
+        post_update_kernel<<<1, 64, 0, s>>>(h->stats, q->loss_dev, h->loss_log, h->log_cap, h->cfg.decay,
+                                            h->cfg.epsilon_end);
+        launch_check("post_update_kernel");
+    }
+}
+
+extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, snk_replay rb,
+                                  const snk_trainer_cfg_t *cfg) {
+    return guard([&] {
+        SNK_CHECK(out && env && dqn && rb && cfg, SNK_ERR_INVALID, "NULL argument");
+        const EnvDev &E = env_dev(env);
+        const ReplayDev &R = replay_dev(rb);
+        SNK_CHECK(E.autoreset, SNK_ERR_STATE, "the batched trainer needs auto-reset envs");
+        SNK_CHECK(E.bs == dqn->L.bs && E.C == dqn->L.C && R.bs == E.bs && R.C == E.C, SNK_ERR_INVALID,
+                  "env / model / replay geometry mismatch");
+        SNK_CHECK(cfg->updates_per_iter >= 0 && cfg->target_update_rate > 0, SNK_ERR_INVALID, "bad trainer config");
+        auto *h = new snk_trainer_s();
+        h->env = env;
+        h->dqn = dqn;
+        h->rb = rb;
+        h->cfg = *cfg;
+        h->B = replay_batch(rb);
+        h->log_cap = cfg->loss_log_capacity > 0 ? cfg->loss_log_capacity : 1;
+        hipStream_t s = stream();
+        h->stats = dalloc<TrainStats>(1);
+        h->act = dalloc<uint8_t>(E.n);
+        h->idx = dalloc<int64_t>(h->B);
+        h->loss_log = dalloc<double>(h->log_cap);
+        TrainStats st{};
+        st.epsilon = cfg->epsilon;
+        st.reward_max = -INFINITY;
+        SNK_HIP(hipMemcpyAsync(h->stats, &st, sizeof st, hipMemcpyHostToDevice, s));
+        SNK_HIP(hipMemsetAsync(h->loss_log, 0, h->log_cap * sizeof(double), s));
+        SNK_HIP(hipMemsetAsync(h->act, 0, E.n, s));
+        SNK_HIP(hipMemsetAsync(h->idx, 0, h->B * sizeof(int64_t), s));
+        // every workspace the iteration touches is allocated now (graph capture)
+        qwork_ensure(dqn->act, dqn->L, E.n, false);
+        qwork_ensure(dqn->tgt, dqn->L, h->B, false);
+        qwork_ensure(dqn->trn, dqn->L, h->B, true);
+        const int64_t need = qnet_backward_slab_floats(dqn->L, h->B);
+        if (need > dqn->slab_cap) {
+            dfree(dqn->slab);
+            dqn->slab = dalloc<float>(need);
+            dqn->slab_cap = need;
+        }
+        SNK_HIP(hipStreamSynchronize(s));
+        *out = h;
+    });
+}
+
+extern "C" int snk_trainer_destroy(snk_trainer h) {
+    return guard([&] {
+        if (!h) return;
+        (void)hipStreamSynchronize(stream());
+        for (int i = 0; i < 2; ++i) {
+            if (h->exec[i]) (void)hipGraphExecDestroy(h->exec[i]);
+            if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
+        }
+        for (void *p : {(void *)h->stats, (void *)h->act, (void *)h->idx, (void *)h->loss_log}) dfree(p);
+        delete h;
+    });
+}
+
+extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int32_t use_graph) {
+    return guard([&] {
+        SNK_CHECK(h && iters >= 0, SNK_ERR_INVALID, "bad trainer_run arguments");
+        hipStream_t s = stream();
+        if (learn && h->cfg.updates_per_iter > 0) {
+            int64_t len = 0;
+            if (snk_replay_length(h->rb, &len) != SNK_OK) throw Error{SNK_ERR_HIP};
+            SNK_CHECK(len >= h->B, SNK_ERR_STATE, "replay holds %lld < batch_size %d transitions (fill it first)",
+                      (long long)len, h->B);
+        }
+        const int g = learn ? 1 : 0;
+        if (use_graph && !h->exec[g]) {
+            SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            try {
+                trainer_iteration(h, learn != 0, s);
+            } catch (...) {
+                hipGraph_t dummy;
+                (void)hipStreamEndCapture(s, &dummy);
+                throw;
+            }
+            SNK_HIP(hipStreamEndCapture(s, &h->graph[g]));
+            SNK_HIP(hipGraphInstantiate(&h->exec[g], h->graph[g], nullptr, nullptr, 0));
+        }
+        for (int64_t i = 0; i < iters; ++i) {
+            if (use_graph)
+                SNK_HIP(hipGraphLaunch(h->exec[g], s));
+            else
+                trainer_iteration(h, learn != 0, s);
+        }
+    });
+}
+
+extern "C" int snk_trainer_stats(snk_trainer h, snk_trainer_stats_t *out) {
+    return guard([&] {
+        SNK_CHECK(h && out, SNK_ERR_INVALID, "NULL argument");
+        TrainStats st;
+        hipStream_t s = stream();
+        SNK_HIP(hipMemcpyAsync(&st, h->stats, sizeof st, hipMemcpyDeviceToHost, s));
+        SNK_HIP(hipStreamSynchronize(s));
+        out->episodes = st.episodes;
+        out->score_sum = st.score_sum;
+        out->updates = st.updates;
+        out->env_steps = st.env_steps;
+        out->reward_sum = st.reward_sum;
+        out->last_loss = st.last_loss;
+        out->reward_max = st.reward_max;
+        out->score_max = st.score_max;
+        out->epsilon = st.epsilon;
+    });
+}
+
+extern "C" int snk_trainer_losses(snk_trainer h, double *host, int64_t n) {
+    return guard([&] {
+        SNK_CHECK(h && host && n >= 0 && n <= h->log_cap, SNK_ERR_INVALID, "bad losses arguments");
+        SNK_HIP(hipMemcpyAsync(host, h->loss_log, n * sizeof(double), hipMemcpyDeviceToHost, stream()));
+        SNK_HIP(hipStreamSynchronize(stream()));
+    });
+}
+
+extern "C" int snk_trainer_act_ptr(snk_trainer h, uint8_t **act_dev) {
+    return guard([&] {
+        SNK_CHECK(h && act_dev, SNK_ERR_INVALID, "NULL argument");
+        *act_dev = h->act;
+    });
+}

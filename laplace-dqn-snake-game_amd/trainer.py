@@ -1,0 +1,136 @@
+"""Trainer, train!, fill_buffer!, epsilon_greedy and play_episode
+(structs.jl:192-216, utils.jl:153-259, 389-494) on the GPU.
+
+The batched trainer keeps the reference's per-update schedule — epsilon
+decays by `decay` per update, update_target_net! when nb % rate == 0
+(nb = 0 included), n_batches + 1 updates in all — but feeds the replay from
+`n_envs` games stepped in lockstep (`updates_per_iter` updates per lockstep
+step) instead of one full episode per update. With n_envs = 1 and
+`schedule="episode"`, train_ plays one whole episode per update exactly as
+utils.jl:434-482 does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import DeviceArray, call, vp
+from .env import SnakeGame, step_indices_dev
+from .qnet import DQNModel
+from .replay import ReplayBuffer, stack_exp
+
+
+def epsilon_greedy(game: SnakeGame, model: DQNModel, epsilon: float, *, seed: int = 0,
+                   act: DeviceArray | None = None) -> np.ndarray:
+    """utils.jl:153-172 for every env: action indices into available_actions."""
+    act = act if act is not None else DeviceArray(game.n_envs, np.uint8)
+    call("snk_dqn_act", model.handle, game.handle, float(epsilon), int(seed), act.ptr)
+    return act.numpy()
+
+
+class Trainer:
+    """structs.jl:205 `Trainer(; n_batches=1000, target_update_rate=1000,
+    epsilon=1.0, epsilon_end=0.05, decay=1e-6, save=true, game, model)`."""
+
+    def __init__(self, *, n_batches: int = 1000, target_update_rate: int = 1000, epsilon: float = 1.0,
+                 epsilon_end: float = 0.05, decay: float = 1e-6, save: bool = False, game: SnakeGame | None = None,
+                 model: DQNModel | None = None, n_envs: int = 1, board_size: int = 10, n_frames: int = 2,
+                 capacity: int = 50000, batch_size: int = 64, updates_per_iter: int = 1, gamma: float = 0.97,
+                 seed: int = 1234, loss_log_capacity: int = 1 << 20):
+        self.game = game if game is not None else SnakeGame(board_size, n_frames, n_envs=n_envs, autoreset=True)
+        if not self.game.autoreset:
+            raise ValueError("the batched trainer needs auto-reset games")
+        bs, nf = self.game.board_size, self.game.n_frames
+        self.model = model if model is not None else DQNModel(bs, 3, n_frames=nf, seed=seed)
+        self.buffer = ReplayBuffer(capacity, board_size=bs, n_frames=nf, batch_size=batch_size)
+        self.n_batches, self.target_update_rate = int(n_batches), int(target_update_rate)
+        self.epsilon, self.epsilon_end, self.decay = float(epsilon), float(epsilon_end), float(decay)
+        self.save, self.gamma, self.seed = bool(save), float(gamma), int(seed)
+        self.updates_per_iter = int(updates_per_iter)
+        self.loss_log_capacity = int(loss_log_capacity)
+        cfg = _lib.TrainerCfg(self.epsilon, self.epsilon_end, self.decay, self.updates_per_iter,
+                              self.target_update_rate, self.gamma, self.seed, self.loss_log_capacity)
+        h = vp()
+        call("snk_trainer_create", C.byref(h), self.game.handle, self.model.handle, self.buffer.handle,
+             C.byref(cfg))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib._lib is not None:
+            _lib._lib.snk_trainer_destroy(self._h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def run(self, iters: int, learn: bool = True, graph: bool = True) -> None:
+        call("snk_trainer_run", self._h, int(iters), int(learn), int(graph))
+
+    def stats(self) -> dict:
+        st = _lib.TrainerStats()
+        call("snk_trainer_stats", self._h, C.byref(st))
+        return {k: getattr(st, k) for k, _ in st._fields_}
+
+    @property
+    def losses(self) -> np.ndarray:
+        """tr.losses (utils.jl:404-406), newest last (up to the log capacity)."""
+        n = min(self.stats()["updates"], self.loss_log_capacity)
+        out = np.zeros(self.loss_log_capacity, np.float64)
+        call("snk_trainer_losses", self._h, _lib.ptr(out), self.loss_log_capacity)
+        u = self.stats()["updates"]
+        if u <= self.loss_log_capacity:
+            return out[:n]
+        k = u % self.loss_log_capacity
+        return np.concatenate([out[k:], out[:k]])
+
+
+def fill_buffer_(tr: Trainer, graph: bool = True) -> None:
+    """utils.jl:389-402: play (with tr.epsilon) until more than `capacity`
+    experiences have been stored."""
+    need = tr.buffer.capacity + 1 - tr.buffer.count
+    if need > 0:
+        tr.run(math.ceil(need / tr.game.n_envs), learn=False, graph=graph)
+
+
+def train_(tr: Trainer, trainer_name: str | None = None, graph: bool = True) -> dict:
+    """utils.jl:420-494: fill the buffer, then n_batches + 1 DQN updates."""
+    fill_buffer_(tr, graph=graph)
+    if tr.updates_per_iter > 0:
+        total = tr.n_batches + 1 - tr.stats()["updates"]
+        if total > 0:
+            tr.run(math.ceil(total / tr.updates_per_iter), learn=True, graph=graph)
+    return tr.stats()
+
+
+def play_episode(model: DQNModel, epsilon: float, *, actions_list=None, board_size: int | None = None,
+                 n_frames: int | None = None, seed: int = 0, max_steps: int = 100000):
+    """utils.jl:198-259: one SnakeGame() played to the end (epsilon-greedy, or
+    the fixed `actions_list` of action indices). Returns (experiences,
+    episode_reward, boards) where boards is the board history b_0..b_L."""
+    bs = board_size or model.board_size
+    nf = n_frames or model.n_frames
+    game = SnakeGame(bs, nf, n_envs=1, autoreset=True)
+    rb = ReplayBuffer(max_steps + 1, board_size=bs, n_frames=nf, batch_size=1)
+    act = DeviceArray(1, np.uint8)
+    L = 0
+    while L < max_steps:
+        if actions_list is not None:
+            if L >= len(actions_list):
+                break
+            act.upload(np.array([actions_list[L]], np.uint8))
+        else:
+            call("snk_dqn_act", model.handle, game.handle, float(epsilon), int(seed), act.ptr)
+        step_indices_dev(game, act.ptr, replay=rb)
+        L += 1
+        if game.last("done")["done"][0]:
+            break
+    exp = stack_exp(rb, np.arange(L, dtype=np.int64))
+    ep_reward = np.float32(0)
+    for r in exp["rewards"]:
+        ep_reward = np.float32(ep_reward + r)
+    boards = [exp["states"][0][-1].astype(np.int8)] + [s[-1].astype(np.int8) for s in exp["next_states"]]
+    return exp, float(ep_reward), np.stack(boards)

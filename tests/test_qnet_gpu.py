@@ -1,0 +1,160 @@
+"""GPU parity of the Q-net forward / DQN update against the oracle.
+
+Tolerances (fp32 device arithmetic vs the fp64 oracle; north_star asks 1e-5
+relative for fp32 Q-values):
+  Q-values      |q - q_ref| <= 1e-5 * max(1, |q_ref|)
+  loss          relative 1e-5
+  gradients     ||g - g_ref|| <= 1e-5 * ||g_ref||  and per element
+                |g - g_ref| <= 1e-5 * max|g_ref| + 1e-4 * |g_ref|
+RMSProp given an identical gradient is bit-exact (same Float32 op order).
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _qclose(q, qref):
+    return np.all(np.abs(q - qref) <= 1e-5 * np.maximum(1.0, np.abs(qref)))
+
+
+def test_params_roundtrip_flux_order(snk, golden):
+    m = snk.DQNModel(10, 3, n_frames=1)
+    p = golden["vanilla_params"]
+    assert m.P == p.size
+    m.set_params(p)
+    assert np.array_equal(m.get_params(), p)
+    m.set_params(p, snk.SNK_NET_TARGET)
+    assert np.array_equal(m.get_params(snk.SNK_NET_TARGET), p)
+
+
+def test_vanilla_bson_greedy_kat_on_device(snk, golden):
+    """BSON vanilla weights: 129/129 greedy actions of the vanilla GIF, and
+    Q-values within 1e-5 of the fp64 oracle."""
+    m = snk.DQNModel(10, 3, n_frames=1)
+    m.set_params(golden["vanilla_params"])
+    fx = golden["vanilla1"]
+    x = fx["boards_cells"][:129].astype(np.float32)[:, None, :]
+    q = m(x)
+    assert (q.argmax(1) == fx["act_idx"]).all()
+    assert _qclose(q, golden["vanilla_q"]), np.abs(q - golden["vanilla_q"]).max()
+
+
+@pytest.mark.parametrize("bs,C,B", [(12, 2, 300), (10, 2, 77), (20, 2, 40), (12, 1, 64)])
+def test_forward_random_vs_oracle(snk, bs, C, B):
+    rng = np.random.default_rng(bs * 10 + C)
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=7)
+    p = m.get_params()
+    assert p.size == snk.nparams(bs, C) == oracle.qnet_nparams(bs, C)
+    x = rng.integers(-1, 3, size=(B, C, bs * bs)).astype(np.float32)
+    q = m(x)
+    qref = oracle.qnet_forward(bs, C, p, x)
+    assert _qclose(q, qref), np.abs(q - qref).max()
+
+
+def test_forward_env_and_act(snk):
+    bs, C, n = 12, 2, 513
+    g = snk.SnakeGame(bs, C, n_envs=n, autoreset=True)
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=3)
+    act = snk.DeviceArray(n, np.uint8)
+    for t in range(5):
+        snk.synth_actions_dev(g, 11, act)
+        snk.step_indices_dev(g, act.ptr)
+    q_env = m.q_env(g)
+    q_ref = m(snk.assemble_state_(g))
+    assert np.array_equal(q_env, q_ref)
+    a0 = snk.epsilon_greedy(g, m, 0.0)
+    assert np.array_equal(a0, q_env.argmax(1))
+    a1 = snk.epsilon_greedy(g, m, 1.0, seed=5)
+    counts = np.bincount(a1, minlength=3)
+    assert counts.min() > n / 3 * 0.7
+
+
+def _random_replay(snk, bs, C, n=96, T=30, seed=3):
+    g = snk.SnakeGame(bs, C, n_envs=n, autoreset=True)
+    rb = snk.ReplayBuffer(n * T, board_size=bs, n_frames=C, batch_size=64)
+    act = snk.DeviceArray(n, np.uint8)
+    for t in range(T):
+        snk.synth_actions_dev(g, seed, act)
+        snk.step_indices_dev(g, act.ptr, replay=rb)
+    return g, rb
+
+
+@pytest.mark.parametrize("bs,C", [(12, 2), (10, 1)])
+def test_loss_and_grad_vs_oracle(snk, bs, C):
+    g, rb = _random_replay(snk, bs, C)
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=21)
+    rng = np.random.default_rng(0)
+    # a target net different from the online net
+    tp = m.get_params() + rng.standard_normal(m.P).astype(np.float32) * 0.01
+    m.set_params(tp, snk.SNK_NET_TARGET)
+    idx, B = snk.sample(rb, seed=4)
+    ids = idx.numpy()[:B]
+    loss = m.loss_grad(rb, idx, B)
+    grad = m.grad
+    b = snk.stack_exp(rb, ids)
+    lref, gref, _ = oracle.dqn_loss_grad(bs, C, m.get_params(), tp, b["states"], b["actions"] - 1, b["rewards"],
+                                         b["next_states"], b["dones"].astype(np.uint8),
+                                         b["suicidal_mask"].astype(np.uint8))
+    assert abs(loss - lref) <= 1e-5 * abs(lref)
+    assert np.linalg.norm(grad - gref) <= 1e-5 * np.linalg.norm(gref)
+    assert np.all(np.abs(grad - gref) <= 1e-5 * np.abs(gref).max() + 1e-4 * np.abs(gref))
+    # the stack_exp-tensor path gives the identical result
+    loss2 = m.loss_grad_batch(b)
+    assert loss2 == loss and np.array_equal(m.grad, grad)
+
+
+def test_rmsprop_bitexact(snk):
+    m = snk.DQNModel(12, 3, n_frames=2, seed=5)
+    rng = np.random.default_rng(1)
+    P = m.P
+    g = (rng.standard_normal(P) * 10.0 ** rng.uniform(-9, 0, P)).astype(np.float32)
+    acc = (np.abs(rng.standard_normal(P)) * 1e-3).astype(np.float32)
+    acc[::7] = 0
+    th = m.get_params()
+    m.set_params(g, snk.SNK_NET_GRAD)
+    m.set_params(acc, snk.SNK_NET_OPT_STATE)
+    for _ in range(3):
+        m.apply_grad()
+        th, acc = oracle.rmsprop(th, acc, g)
+    assert np.array_equal(m.get_params(), th)
+    assert np.array_equal(m.get_params(snk.SNK_NET_OPT_STATE), acc)
+
+
+def test_update_and_target_sync(snk):
+    g, rb = _random_replay(snk, 12, 2)
+    m = snk.DQNModel(12, 3, n_frames=2, seed=8)
+    th0 = m.get_params()
+    idx, B = snk.sample(rb, seed=9)
+    loss = m.loss_grad(rb, idx, B)
+    grad = m.grad
+    m.apply_grad()
+    th1, _ = oracle.rmsprop(th0, np.zeros_like(th0), grad)
+    assert np.array_equal(m.get_params(), th1)
+    assert np.array_equal(m.get_params(snk.SNK_NET_TARGET), th0)
+    snk.update_target_net_(m)
+    assert np.array_equal(m.get_params(snk.SNK_NET_TARGET), th1)
+    assert np.isfinite(loss)
+
+
+def test_trainer_schedule_and_graph_determinism(snk):
+    """train!: fill the buffer, n_batches+1 updates, epsilon decay per update
+    (Float32, utils.jl:480), target sync at nb % rate == 0; the captured
+    hipGraph replay is bit-identical to eager launches."""
+    outs = []
+    for graph in (False, True):
+        tr = snk.Trainer(n_batches=40, target_update_rate=16, n_envs=128, board_size=12, n_frames=2,
+                         capacity=1000, decay=1e-3, seed=77)
+        st = snk.train_(tr, graph=graph)
+        outs.append((tr.model.get_params(), tr.model.get_params(snk.SNK_NET_TARGET), tr.losses, st))
+    (p0, t0, l0, s0), (p1, t1, l1, s1) = outs
+    assert np.array_equal(p0, p1) and np.array_equal(t0, t1) and np.array_equal(l0, l1)
+    assert s0["updates"] == 41 and s1 == s0
+    eps = np.float32(1.0)
+    for _ in range(41):
+        eps = max(np.float32(eps - np.float32(1e-3)), np.float32(0.05))
+    assert np.float32(s0["epsilon"]) == eps
+    assert len(l0) == 41 and np.all(np.isfinite(l0))
+    assert s0["env_steps"] >= 1001 and s0["episodes"] > 0
