@@ -372,7 +372,9 @@ __global__ void rmsprop_kernel(int64_t P, float *__restrict__ theta, float *__re
         const float g = grad[i];
         const float qd = rho * acc[i] + omr * (g * g);
         acc[i] = qd;
-        theta[i] = theta[i] - (g * eta) / (__fsqrt_rn(qd) + eps);
+        // correctly rounded sqrt and divide (HIP default; __fsqrt_rn would be
+        // the native approximation) so the update matches Optimisers' Float32
+        theta[i] = theta[i] - (g * eta) / (__builtin_sqrtf(qd) + eps);
     }
 }
 
