@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""bench.py — throughput of the batched Snake-DQN hot path on MI355X.
+
+Metric (BASELINE.json): env-steps/sec @4096 envs (+ D(50k) build sec).
+Workload (BASELINE.json configs[1]): 4096 parallel 12x12 envs, 2-frame
+3-action DQN, fp32, per GPU (weak scaling). One timed "step" is one lockstep
+iteration of the whole hot path, replayed from one captured hipGraph:
+  epsilon_greedy Q forward over all 4096 envs -> step!/virtual_step/auto-reset
+  -> store! into the 50k replay -> one DQN update (sample 64, t_net TD target,
+  Huber, backward, RMSProp, target-sync check) [-> RCCL gradient all-reduce
+  for N > 1].
+value = env-steps of all ranks / max-over-ranks wall time. Synthetic data:
+env dynamics are the real game from SnakeGame(); the net is glorot-initialised
+(no checkpoint of the 2-frame 12x12 net exists).
+
+python bench.py [--gpus N] [--steps K] [--warmup W]
+For N > 1 launch one process per GPU with torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--n-envs", type=int, default=4096)
+    p.add_argument("--board-size", type=int, default=12)
+    p.add_argument("--n-frames", type=int, default=2)
+    p.add_argument("--updates-per-iter", type=int, default=1)
+    p.add_argument("--epsilon", type=float, default=0.05)
+    p.add_argument("--capacity", type=int, default=50000)
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="skip per-kernel timing / D build")
+    return p.parse_args()
+
+
+def cpu_baseline(args) -> dict:
+    """The CPU oracle (oracle/liboracle.so, plain C, 1 thread) timed on this
+    host on a bounded sample of the same workload, extrapolated to one full
+    iteration: Q forward of 4096 states (timed on 128, scaled), 4096 env steps
+    (timed on all 4096 for 3 steps), one 64-sample DQN update (timed once)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    bs, C, n = args.board_size, args.n_frames, args.n_envs
+    rng = np.random.default_rng(0)
+    P = oracle.qnet_nparams(bs, C)
+    params = (rng.standard_normal(P) * 0.05).astype(np.float32)
+    nf = 128
+    x = rng.integers(-1, 3, size=(nf, C, bs * bs)).astype(np.float64)
+    t0 = time.perf_counter()
+    oracle.qnet_forward(bs, C, params, x)
+    t_fwd = (time.perf_counter() - t0) / nf * n
+    ob = oracle.OracleBatch(n, bs, C)
+    t0 = time.perf_counter()
+    for t in range(3):
+        ob.step(oracle.synth_actions(7, n, t), want_frames=True)
+    t_step = (time.perf_counter() - t0) / 3
+    B = 64
+    s = rng.integers(-1, 3, size=(B, C, bs * bs))
+    sn = rng.integers(-1, 3, size=(B, C, bs * bs))
+    t0 = time.perf_counter()
+    _, g, _ = oracle.dqn_loss_grad(bs, C, params, params, s, rng.integers(0, 3, B), np.zeros(B, np.float32), sn,
+                                   np.zeros(B, np.uint8), np.zeros((B, 3), np.uint8))
+    oracle.rmsprop(params, np.zeros_like(params), g.astype(np.float32))
+    t_upd = (time.perf_counter() - t0) * args.updates_per_iter
+    it = t_fwd + t_step + t_upd
+    return {"value": n / it, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle C restatement, 1 thread: Q forward on {nf} of {n} states (scaled x{n // nf}), "
+                       f"3 lockstep steps of {n} envs, one B=64 loss+grad+RMSProp; per-iteration "
+                       f"fwd {t_fwd:.2f}s + step {t_step:.3f}s + update {t_upd:.2f}s")}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")   # host-side barrier / max-reduce; device traffic is RCCL in-library
+
+    import numpy as np
+    import snake_amd as snk
+    from snake_amd import _lib
+    lib = snk.load()
+    _lib.call("snk_set_device", local)
+
+    n, bs, C = args.n_envs, args.board_size, args.n_frames
+    tr = snk.Trainer(n_envs=n, board_size=bs, n_frames=C, capacity=args.capacity, batch_size=64,
+                     epsilon=args.epsilon, epsilon_end=args.epsilon, decay=0.0,
+                     updates_per_iter=args.updates_per_iter, seed=1234 + rank)
+    comm = None
+    if world > 1:
+        comm = snk.dist_attach(tr, dist, rank, world)
+    graph = not args.no_graph
+    snk.fill_buffer_(tr, graph=graph)                    # fill_buffer!: untimed
+    tr.run(args.warmup, learn=True, graph=graph)
+
+    def barrier():
+        _lib.call("snk_synchronize")
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    tr.run(args.steps, learn=True, graph=graph)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = tr.stats()
+    faults = tr.game.check_faults()
+
+    out = {
+        "metric": "env-steps/sec/GPU @4096 envs + D(50k) build sec, 1/2/4/8 MI355X",
+        "value": world * n * args.steps / elapsed,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (real Snake dynamics from SnakeGame(); glorot-initialised Q-net)",
+        "config": {"workload": f"{n} lockstep {bs}x{bs} envs/GPU, {C}-frame 3-action DQN: "
+                               f"eps-greedy Q forward + step!/virtual_step + store! + "
+                               f"{args.updates_per_iter} B=64 update(s) per step",
+                   "n_envs_per_gpu": n, "board_size": bs, "n_frames": C, "replay_capacity": args.capacity,
+                   "batch_size": 64, "epsilon": args.epsilon, "parallelism": f"dp{world}" if world > 1 else "none",
+                   "hipgraph": graph},
+        "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
+                        "food_faults": faults},
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and not args.no_extras:
+        # dominant kernel: conv3 of the act forward (implicit GEMM on f32 MFMA)
+        ms = np.zeros(5, np.float64)
+        _lib.call("snk_dqn_time_act_layers", tr.model.handle, tr.game.handle, 20, _lib.ptr(ms))
+        wo = bs - 5
+        flop_conv3 = 2.0 * n * wo * wo * (36 * 32) * 64
+        flop_total = 2.0 * n * (bs * bs * 16 * 9 * C + bs * bs * 32 * 144 + wo * wo * 64 * 1152 + wo * wo * 64 * 64 + 64 * 3)
+        tf = flop_conv3 / (ms[2] * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": "conv3 implicit GEMM (act forward, 32x32x2 f32 MFMA)",
+                           "achieved": tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_TFLOPS,
+                           "traffic": None, "avg_launch_ms": ms[2],
+                           "flop_per_launch": flop_conv3}
+        out["act_forward_ms"] = {"conv1": ms[0], "conv2": ms[1], "conv3": ms[2], "dense1": ms[3], "head": ms[4],
+                                 "total": float(ms.sum()),
+                                 "tflops_total": flop_total / (ms.sum() * 1e-3) / 1e12}
+        # the fused env step + store kernel (HBM roofline)
+        act = snk.DeviceArray(n, np.uint8)
+        snk.synth_actions_dev(tr.game, 99, act)
+        sms = _lib.f64(0)
+        import ctypes
+        _lib.call("snk_env_time_step", tr.game.handle, tr.buffer.handle, act.ptr, 50, ctypes.byref(sms))
+        step_bytes = (C + 4) * bs * bs + 57
+        gbs = n * step_bytes / (sms.value * 1e-3) / 1e9
+        out["step_kernel"] = {"avg_launch_ms": sms.value, "bytes_per_env_step": step_bytes,
+                              "achieved_GBs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS,
+                              "env_steps_per_s": n / (sms.value * 1e-3)}
+        out["d_build_sec"] = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -153,6 +153,12 @@ int snk_dqn_forward(snk_dqn m, int32_t which, const float *x_dev, int64_t B, flo
 int snk_dqn_forward_env(snk_dqn m, int32_t which, snk_env env, float *q_dev);
 /* epsilon_greedy (utils.jl:153-172) for every env: act_dev [n] action index */
 int snk_dqn_act(snk_dqn m, snk_env env, float epsilon, uint64_t seed, uint8_t *act_dev);
+/* measurement: average ms per launch of each stage of the epsilon_greedy
+ * forward over env's batch, ms_out[5] = conv1, conv2, conv3, dense1, head
+ * (HIP events on the library stream) */
+int snk_dqn_time_act_layers(snk_dqn m, snk_env env, int32_t reps, double *ms_out);
+/* measurement: average ms of the fused step(+store) kernel over reps real steps */
+int snk_env_time_step(snk_env env, snk_replay rb_or_null, const uint8_t *act_dev, int32_t reps, double *ms_out);
 /* Q of the last forward_env/act call, host [n][3] */
 int snk_dqn_last_q(snk_dqn m, float *q_host, int64_t n);
 /* utils.jl:448-464: TD target on t_net (Float64, suicidal mask -> -100),
@@ -200,6 +206,20 @@ int snk_trainer_stats(snk_trainer t, snk_trainer_stats_t *out);
 /* tr.losses: loss of update u at host[u % loss_log_capacity] */
 int snk_trainer_losses(snk_trainer t, double *host, int64_t n);
 int snk_trainer_act_ptr(snk_trainer t, uint8_t **act_dev);
+
+/* ---------------------------------------------------------------- multi-GPU
+ * Data-parallel replicas (new: the reference is single-process). One process
+ * per GPU; RCCL over xGMI. The 128-byte unique id is created on rank 0 and
+ * shipped to the other ranks by the host (torch.distributed store/gloo). */
+typedef struct snk_comm_s *snk_comm;
+int snk_comm_unique_id(uint8_t *id128_host);
+int snk_comm_create(snk_comm *out, int32_t nranks, int32_t rank, const uint8_t *id128_host);
+int snk_comm_destroy(snk_comm c);
+int snk_comm_allreduce_mean(snk_comm c, float *buf_dev, int64_t n);
+int snk_comm_broadcast(snk_comm c, float *buf_dev, int64_t n, int32_t root);
+/* the trainer all-reduces (mean) the gradient of every update across the
+ * communicator; broadcasts rank 0's q_net first */
+int snk_trainer_set_comm(snk_trainer t, snk_comm c);
 
 #ifdef __cplusplus
 }

@@ -95,6 +95,8 @@ _PROTOS = {
     "snk_dqn_forward_env": [vp, i32, vp, vp],
     "snk_dqn_act": [vp, vp, f32, u64, vp],
     "snk_dqn_last_q": [vp, vp, i64],
+    "snk_dqn_time_act_layers": [vp, vp, i32, vp],
+    "snk_env_time_step": [vp, vp, vp, i32, P(f64)],
     "snk_dqn_loss_grad": [vp, vp, vp, i64, f64, P(f64)],
     "snk_dqn_loss_grad_batch": [vp, vp, vp, vp, vp, vp, vp, i64, f64, P(f64)],
     "snk_dqn_apply_grad": [vp],
@@ -105,6 +107,12 @@ _PROTOS = {
     "snk_trainer_stats": [vp, vp],
     "snk_trainer_losses": [vp, vp, i64],
     "snk_trainer_act_ptr": [vp, P(vp)],
+    "snk_trainer_set_comm": [vp, vp],
+    "snk_comm_unique_id": [vp],
+    "snk_comm_create": [P(vp), i32, i32, vp],
+    "snk_comm_destroy": [vp],
+    "snk_comm_allreduce_mean": [vp, vp, i64],
+    "snk_comm_broadcast": [vp, vp, i64, i32],
 }
 
 SNK_NET_Q = 0

@@ -264,6 +264,41 @@ extern "C" int snk_dqn_act(snk_dqn h, snk_env env, float epsilon, uint64_t seed,
     });
 }
 
+extern "C" int snk_dqn_time_act_layers(snk_dqn h, snk_env env, int32_t reps, double *ms_out) {
+    return guard([&] {
+        SNK_CHECK(h && env && ms_out && reps > 0, SNK_ERR_INVALID, "bad time_act_layers arguments");
+        const EnvDev &E = env_dev(env);
+        SNK_CHECK(E.bs == h->L.bs && E.C == h->L.C, SNK_ERR_INVALID, "env/model geometry mismatch");
+        hipStream_t s = stream();
+        qwork_ensure(h->act, h->L, E.n, false);
+        if (h->meta_cap < E.n) {
+            SNK_HIP(hipStreamSynchronize(s));
+            dfree(h->meta);
+            h->meta = dalloc<uint8_t>(2 * E.n);
+            h->meta_cap = E.n;
+        }
+        HeadArgs ha;
+        ha.act = h->meta;
+        ha.epsilon = 0.05f;
+        ha.tptr = &E.ctl->t;
+        qnet_forward(h->L, h->theta_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s);
+        hipEvent_t a, b;
+        SNK_HIP(hipEventCreate(&a));
+        SNK_HIP(hipEventCreate(&b));
+        for (int layer = 0; layer < 5; ++layer) {
+            SNK_HIP(hipEventRecord(a, s));
+            for (int r = 0; r < reps; ++r) qnet_forward(h->L, h->theta_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, layer);
+            SNK_HIP(hipEventRecord(b, s));
+            SNK_HIP(hipEventSynchronize(b));
+            float ms = 0.0f;
+            SNK_HIP(hipEventElapsedTime(&ms, a, b));
+            ms_out[layer] = (double)ms / reps;
+        }
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+    });
+}
+
 extern "C" int snk_dqn_last_q(snk_dqn h, float *q_host, int64_t n) {
     return guard([&] {
         SNK_CHECK(h && q_host && n >= 0 && n <= h->act.cap, SNK_ERR_INVALID, "bad last_q arguments");

@@ -437,9 +437,9 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
 
 // ---------------------------------------------------------------- forward
 void qnet_forward(const QLayout &L, const float *th, const BoardSrc &src, int64_t S, QWork &w, HeadMode mode,
-                  const HeadArgs &ha, hipStream_t s) {
+                  const HeadArgs &ha, hipStream_t s, int only) {
     const int bs = L.bs, nc = L.ncell;
-    {
+    if (only < 0 || only == 0) {
         const int64_t total = S * nc;
         const int grid = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
         if (L.C == 1)
@@ -448,12 +448,12 @@ void qnet_forward(const QLayout &L, const float *th, const BoardSrc &src, int64_
             conv1_fwd_kernel<2><<<grid, 256, 0, s>>>(src, th + L.off_w1, th + L.off_b1, w.a1, S, bs);
         launch_check("conv1_fwd_kernel");
     }
-    {   // conv2: M = S*bs^2, K = 9*16, N = 32
+    if (only < 0 || only == 1) {   // conv2: M = S*bs^2, K = 9*16, N = 32
         AConvFwd<16, 3, 1> al{w.a1, bs, bs, FastDiv(nc), FastDiv(bs)};
         gemm<1>(al, BRowMajor{th + L.off_w2, 144, 32}, EpBiasRelu{w.a2, th + L.off_b2, (int)(S * nc), 32, 1},
                 S * nc, 32, 144, 1, 144, s);
     }
-    {   // conv3: M = S*Wo^2, K = 36*32, N = 64
+    if (only < 0 || only == 2) {   // conv3: M = S*Wo^2, K = 36*32, N = 64
         const int no = L.Wo * L.Wo;
         AConvFwd<32, 6, 0> al{w.a2, bs, L.Wo, FastDiv(no), FastDiv(L.Wo)};
         gemm<2>(al, BRowMajor{th + L.off_w3, 1152, 64}, EpBiasRelu{w.a3, th + L.off_b3, (int)(S * no), 64, 1},
@@ -462,8 +462,10 @@ void qnet_forward(const QLayout &L, const float *th, const BoardSrc &src, int64_
     int kc;
     const int ks = d1_split(L, S, kc);
     // Dense1 (split-K partial sums; bias + relu in the head)
-    gemm<2>(ARowMajor{w.a3, L.K1, L.K1}, BRowMajor{th + L.off_d1w, L.K1, 64}, EpSlab{w.slab, (int)S, 64}, S, 64,
-            L.K1, ks, kc, s);
+    if (only < 0 || only == 3)
+        gemm<2>(ARowMajor{w.a3, L.K1, L.K1}, BRowMajor{th + L.off_d1w, L.K1, 64}, EpSlab{w.slab, (int)S, 64}, S, 64,
+                L.K1, ks, kc, s);
+    if (only >= 0 && only != 4) return;
     const int grid = ceil_div(S, 4);
     switch (mode) {
         case HEAD_Q: head_kernel<HEAD_Q><<<grid, 256, 0, s>>>(w.slab, ks, S, th, L, w.h1, w.q, ha); break;

@@ -85,8 +85,10 @@ struct HeadArgs {
 };
 
 // forward: q[S][3] into w.q (and w.h1); mode-specific epilogue
+// only = -1: the whole chain; 0..4: just conv1 / conv2 / conv3 / dense1 / head
+// (inputs from a previous full forward; used for per-layer timing)
 void qnet_forward(const QLayout &L, const float *theta, const BoardSrc &src, int64_t S, QWork &w,
-                  HeadMode mode, const HeadArgs &ha, hipStream_t s);
+                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1);
 // backward of the loss whose dq sits in w.dq (after HEAD_LOSS): grad (packed) overwritten
 void qnet_backward(const QLayout &L, const float *theta, const BoardSrc &src, int64_t S, QWork &w,
                    float *grad, float *slab, int64_t slab_cap, hipStream_t s);

@@ -177,6 +177,32 @@ extern "C" int snk_env_step_store(snk_env env, const uint8_t *act_dev, int32_t a
     });
 }
 
+extern "C" int snk_env_time_step(snk_env env, snk_replay rb, const uint8_t *act_dev, int32_t reps, double *ms_out) {
+    return guard([&] {
+        SNK_CHECK(env && act_dev && ms_out && reps > 0, SNK_ERR_INVALID, "bad time_step arguments");
+        const EnvDev &E = env_dev(env);
+        SNK_CHECK(!rb || E.autoreset, SNK_ERR_STATE, "fused store needs auto-reset envs");
+        hipStream_t s = stream();
+        hipEvent_t a, b;
+        SNK_HIP(hipEventCreate(&a));
+        SNK_HIP(hipEventCreate(&b));
+        double total = 0.0;
+        for (int r = 0; r < reps; ++r) {
+            SNK_HIP(hipEventRecord(a, s));
+            env_launch_step(E, act_dev, SNK_ACT_INDEX, rb ? &rb->d : nullptr, s);
+            SNK_HIP(hipEventRecord(b, s));
+            env_launch_advance(E, rb ? &rb->d : nullptr, s);
+            SNK_HIP(hipEventSynchronize(b));
+            float ms = 0.0f;
+            SNK_HIP(hipEventElapsedTime(&ms, a, b));
+            total += ms;
+        }
+        *ms_out = total / reps;
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+    });
+}
+
 extern "C" int snk_replay_store(snk_replay h, int64_t B, const int8_t *frames, const uint8_t *act,
                                 const float *rew, const uint8_t *done, const uint8_t *mask,
                                 const uint8_t *dirs) {

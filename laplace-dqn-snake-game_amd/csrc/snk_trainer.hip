@@ -87,11 +87,16 @@ __global__ void post_update_kernel(TrainStats *st, const double *loss, double *l
     st->updates += 1;
 }
 
+void comm_allreduce_mean(snk_comm h, float *buf, int64_t n, hipStream_t s);
+void comm_broadcast(snk_comm h, float *buf, int64_t n, int root, hipStream_t s);
+int comm_size(snk_comm h);
+
 }  // namespace snk
 
 using namespace snk;
 
 struct snk_trainer_s {
+    snk_comm comm = nullptr;
     snk_env env = nullptr;
     snk_dqn dqn = nullptr;
     snk_replay rb = nullptr;
@@ -132,6 +137,7 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
         m.mask = R.mask;
         m.act_idx = R.act;
         dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s);
+        if (h->comm) comm_allreduce_mean(h->comm, q->grad, q->L.P, s);   // data-parallel replicas
         rmsprop_launch(q->L.P, q->theta_q, q->acc, q->grad, q->lr, q->rho, q->eps, s);
         dqn_sync_target_launch(q, &h->stats->updates, h->cfg.target_update_rate, s);
         post_update_kernel<<<1, 64, 0, s>>>(h->stats, q->loss_dev, h->loss_log, h->log_cap, h->cfg.decay,
@@ -225,6 +231,26 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
                 SNK_HIP(hipGraphLaunch(h->exec[g], s));
             else
                 trainer_iteration(h, learn != 0, s);
+        }
+    });
+}
+
+extern "C" int snk_trainer_set_comm(snk_trainer h, snk_comm comm) {
+    return guard([&] {
+        SNK_CHECK(h && comm, SNK_ERR_INVALID, "NULL argument");
+        hipStream_t s = stream();
+        snk_dqn_s *q = h->dqn;
+        // replicas start from rank 0's q_net; t_net = q_net; fresh RMSProp state
+        comm_broadcast(comm, q->theta_q, q->L.P, 0, s);
+        dqn_sync_target_launch(q, nullptr, 1, s);
+        SNK_HIP(hipMemsetAsync(q->acc, 0, q->L.P * sizeof(float), s));
+        SNK_HIP(hipStreamSynchronize(s));
+        h->comm = comm;
+        for (int i = 0; i < 2; ++i) {   // captured graphs predate the collective
+            if (h->exec[i]) (void)hipGraphExecDestroy(h->exec[i]);
+            if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
+            h->exec[i] = nullptr;
+            h->graph[i] = nullptr;
         }
     });
 }
