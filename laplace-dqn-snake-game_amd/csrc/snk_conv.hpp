@@ -1,0 +1,180 @@
+// snk_conv.hpp — LDS-staged implicit-GEMM convolution on v_mfma_f32_32x32x2_f32.
+//
+// out[m][n] = sum_{kk, c} A[m][(kk, c)] * Wk[kk][c][n]
+//   m  = (sample, output position)           -> MFMA rows (32 per wave)
+//   kk = kernel offset (du, dv), c = channel -> reduction, CK channels per kk
+//   n  = output channel                      -> MFMA columns (CN = 32 or 64)
+// MODE_FWD    A = x[s][p + (du,dv) - PAD][c]      (true conv, packed weights)
+// MODE_DX     A = dz[s][p - (du,dv) + PAD][c]     (data gradient: c = conv COUT,
+//             n = conv CIN, weights used untransposed)
+// MODE_DENSE  A = x[s][kk][c] (Dense1: kk enumerates the Wo^2 positions)
+//
+// Workgroup = 4 waves = 128 rows x CN columns. Per kernel offset kk the
+// workgroup stages that offset's CK x CN weight block into LDS as [n][c]
+// (c contiguous, row padded by 4 floats: conflict-free ds_read_b128), double
+// buffered with one barrier per offset; each lane reads its A operand as
+// float4 along c straight from global/L2 (every im2col row is a contiguous
+// channel run) one offset ahead. A lane's float4 covers 4 consecutive MFMA
+// k-steps: lane half h holds k = 8*kb + 4h + j at step j of channel block kb,
+// and the B fragment is read with the same (kb, h, j) mapping.
+// grid = (ceil(M/128), kk splits); with splits the epilogue writes partial
+// slabs that a reduce kernel finishes.
+#pragma once
+#include "snk_gemm.hpp"
+
+namespace snk {
+
+enum ConvMode { MODE_FWD = 0, MODE_DX = 1, MODE_DENSE = 2 };
+enum ConvEpi { EPI_BIAS_RELU = 0, EPI_SLAB = 1, EPI_RELU_MASK = 2 };
+
+struct ConvArgs {
+    const float *x;      // A source [S][HIN*HIN][CK]
+    const float *w;      // packed conv weights [KS*KS][CIN][COUT] of the layer
+    const float *bias;   // EPI_BIAS_RELU
+    const float *act;    // EPI_RELU_MASK: mask source, same shape as out
+    float *out;          // [M][CN] or slab [split][M][CN]
+    int M, HIN, HOUT, nkk, kk_per_split;
+    uint32_t d2m, d2s, d1m, d1s;   // FastDiv(HOUT*HOUT), FastDiv(HOUT) magic/shift
+};
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
+
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+    constexpr int NT = CN / 32;
+    constexpr int KB = CK / 8;
+    constexpr int LDB = CK + 4;
+    constexpr int NV = (CK * CN / 4 + 255) / 256;  // float4 staging loads per thread
+    __shared__ __attribute__((aligned(16))) float Bs[2][CN * LDB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int m = blockIdx.x * 128 + wave * 32 + r;
+    const bool ok = m < a.M;
+    const int mm = ok ? m : 0;
+    int s, i = 0, j = 0;
+    if (MODE == MODE_DENSE) {
+        s = mm;
+    } else {
+        s = (int)fdiv((uint32_t)mm, a.d2m, a.d2s);
+        const int p = mm - s * a.HOUT * a.HOUT;
+        j = (int)fdiv((uint32_t)p, a.d1m, a.d1s);
+        i = p - j * a.HOUT;
+    }
+    const float *xs = a.x + (int64_t)s * a.HIN * a.HIN * CK + 4 * h;
+    const int kk0 = blockIdx.y * a.kk_per_split;
+    const int kk1 = min(a.nkk, kk0 + a.kk_per_split);
+
+    f32x16 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[nt][g] = 0.0f;
+
+    float4 bv[NV];
+    auto stage_load = [&](int kk) {
+        const float4 *src = reinterpret_cast<const float4 *>(a.w + (int64_t)kk * CK * CN);
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int e4 = tid + q * 256;
+            bv[q] = e4 < CK * CN / 4 ? src[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto stage_store = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int e4 = tid + q * 256;
+            if (e4 >= CK * CN / 4) continue;
+            const int e = e4 * 4;
+            if (MODE == MODE_DX) {
+                // weight block [ci = n][co = c]: c contiguous already
+                const int n = e / CK, c = e - n * CK;
+                *reinterpret_cast<float4 *>(&Bs[buf][n * LDB + c]) = bv[q];
+            } else {
+                // weight block [c][n]: transpose to [n][c]
+                const int c = e / CN, n = e - c * CN;
+                Bs[buf][(n + 0) * LDB + c] = bv[q].x;
+                Bs[buf][(n + 1) * LDB + c] = bv[q].y;
+                Bs[buf][(n + 2) * LDB + c] = bv[q].z;
+                Bs[buf][(n + 3) * LDB + c] = bv[q].w;
+            }
+        }
+    };
+    auto load_a = [&](int kk, float4 (&av)[KB]) {
+        const float *p;
+        bool valid = ok;
+        if (MODE == MODE_DENSE) {
+            p = xs + kk * CK;
+        } else {
+            const int dv = kk / KS, du = kk - dv * KS;
+            const int xi = MODE == MODE_FWD ? i + du - PAD : i - du + PAD;
+            const int xj = MODE == MODE_FWD ? j + dv - PAD : j - dv + PAD;
+            valid = valid && xi >= 0 && xi < a.HIN && xj >= 0 && xj < a.HIN;
+            p = xs + (xi + xj * a.HIN) * CK;
+        }
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+            av[kb] = valid ? *reinterpret_cast<const float4 *>(p + kb * 8) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+
+    float4 a_cur[KB], a_nxt[KB];
+    if (kk0 < kk1) {
+        stage_load(kk0);
+        stage_store(0);
+        load_a(kk0, a_cur);
+    }
+    __syncthreads();
+    for (int kk = kk0; kk < kk1; ++kk) {
+        const int buf = (kk - kk0) & 1;
+        const bool more = kk + 1 < kk1;
+        if (more) {
+            stage_load(kk + 1);
+            load_a(kk + 1, a_nxt);
+        }
+        const float *bb = &Bs[buf][r * LDB + 4 * h];
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+            float4 b4[NT];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) b4[nt] = *reinterpret_cast<const float4 *>(bb + nt * 32 * LDB + kb * 8);
+            const float av4[4] = {a_cur[kb].x, a_cur[kb].y, a_cur[kb].z, a_cur[kb].w};
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const float bq[4] = {b4[nt].x, b4[nt].y, b4[nt].z, b4[nt].w};
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av4[jj], bq[jj], acc[nt], 0, 0, 0);
+            }
+        }
+        if (more) stage_store(buf ^ 1);
+        __syncthreads();
+        if (more) {
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) a_cur[kb] = a_nxt[kb];
+        }
+    }
+
+    // epilogue: acc register g of lane l is C[(g&3) + 8*(g>>2) + 4*(l>>5)][l&31]
+    const int mrow0 = blockIdx.x * 128 + wave * 32;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int col = nt * 32 + r;
+        const float b = EPI == EPI_BIAS_RELU ? a.bias[col] : 0.0f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int row = mrow0 + acc_row(g, lane);
+            if (row >= a.M) continue;
+            const int64_t o = (int64_t)row * CN + col;
+            if (EPI == EPI_BIAS_RELU) {
+                const float v = acc[nt][g] + b;
+                a.out[o] = v > 0.0f ? v : 0.0f;
+            } else if (EPI == EPI_SLAB) {
+                a.out[(int64_t)blockIdx.y * a.M * CN + o] = acc[nt][g];
+            } else {
+                a.out[o] = a.act[o] > 0.0f ? acc[nt][g] : 0.0f;
+            }
+        }
+    }
+}
+
+}  // namespace snk

@@ -227,6 +227,61 @@ static void gemm(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int
     launch_check("gemm_kernel");
 }
 
+// ---------------------------------------------------------------- LDS-staged conv
+static int conv_splits(int64_t M, int nkk) {
+    const int64_t wgs = ceil_div(M, 128);
+    if (wgs >= 512) return 1;
+    return (int)std::min<int64_t>(nkk, ceil_div(512, wgs));
+}
+
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
+static void conv_launch(ConvArgs a, int splits, hipStream_t s) {
+    a.kk_per_split = ceil_div(a.nkk, splits);
+    splits = ceil_div(a.nkk, a.kk_per_split);
+    const FastDiv d2((uint32_t)std::max(1, a.HOUT * a.HOUT)), d1((uint32_t)std::max(1, a.HOUT));
+    a.d2m = d2.m; a.d2s = d2.s; a.d1m = d1.m; a.d1s = d1.s;
+    dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)splits);
+    conv_mfma_kernel<CK, CN, KS, PAD, MODE, EPI><<<grid, 256, 0, s>>>(a);
+    launch_check("conv_mfma_kernel");
+}
+
+// finish a kk-split conv: out = relu(sum_z slab[z] + bias)  or  (act > 0) * sum_z slab[z]
+__global__ void conv_reduce_kernel(const float *__restrict__ slab, int splits, int64_t MN, int N,
+                                   const float *__restrict__ bias, const float *__restrict__ act,
+                                   float *__restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += (int64_t)gridDim.x * blockDim.x) {
+        float v = 0.0f;
+        for (int z = 0; z < splits; ++z) v += slab[(int64_t)z * MN + i];
+        if (bias) {
+            v += bias[i % N];
+            out[i] = v > 0.0f ? v : 0.0f;
+        } else {
+            out[i] = act[i] > 0.0f ? v : 0.0f;
+        }
+    }
+}
+
+// out = conv (bias + relu), kk-split through the conv slab when the grid is small
+template <int CK, int CN, int KS, int PAD>
+static void conv_fwd(const float *x, const float *w, const float *bias, float *out, int64_t M, int HIN, int HOUT,
+                     QWork &wk, hipStream_t s) {
+    ConvArgs a{};
+    a.x = x; a.w = w; a.bias = bias; a.M = (int)M; a.HIN = HIN; a.HOUT = HOUT; a.nkk = KS * KS;
+    const int sp = conv_splits(M, a.nkk);
+    if (sp == 1) {
+        a.out = out;
+        conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_BIAS_RELU>(a, 1, s);
+        return;
+    }
+    a.out = wk.cslab;
+    SNK_CHECK((int64_t)sp * M * CN <= wk.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
+    conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_SLAB>(a, sp, s);
+    const int used = ceil_div(a.nkk, ceil_div(a.nkk, sp));
+    conv_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(M * CN, 256), 4096), 256, 0, s>>>(
+        wk.cslab, used, M * CN, CN, bias, nullptr, out);
+    launch_check("conv_reduce_kernel");
+}
+
 // ---------------------------------------------------------------- conv1 (VALU)
 template <int C>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(BoardSrc src, const float *__restrict__ w,
@@ -393,30 +448,47 @@ __global__ void loss_mean_kernel(const double *__restrict__ loss, int64_t B, dou
 
 // ---------------------------------------------------------------- workspace
 void qwork_free(QWork &w) {
-    for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a3, (void *)w.slab, (void *)w.h1, (void *)w.q,
+    for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a3, (void *)w.slab, (void *)w.cslab, (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.target,
                     (void *)w.loss})
         dfree(p);
     w = QWork{};
 }
 
-static int d1_split(const QLayout &L, int64_t S, int &kchunk) {
-    int ks;
-    choose_split(ceil_div(S, 32), L.K1, ks, kchunk);
-    return ks;
+// Dense1 split over its Wo^2 positions: returns the number of partial slabs
+static int d1_split(const QLayout &L, int64_t S, int &kk_per) {
+    const int nkk = L.Wo * L.Wo;
+    kk_per = ceil_div(nkk, conv_splits(S, nkk));
+    return ceil_div(nkk, kk_per);
+}
+
+static int64_t conv_slab_floats(const QLayout &L, int64_t S, bool train) {
+    int64_t need = 0;
+    auto add = [&](int64_t M, int nkk, int N) {
+        const int sp = conv_splits(M, nkk);
+        if (sp > 1) need = std::max(need, (int64_t)sp * M * N);
+    };
+    add(S * L.ncell, 9, 32);
+    add(S * L.Wo * L.Wo, 36, 64);
+    if (train) add(S * L.ncell, 36, 32);
+    return need;
 }
 
 void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     int kc;
     const int64_t need_slab = (int64_t)d1_split(L, S, kc) * S * 64;
-    if (S <= w.cap && need_slab <= w.slab_floats && (!train || w.has_train)) return;
+    const int64_t need_cslab = conv_slab_floats(L, S, train || w.has_train);
+    if (S <= w.cap && need_slab <= w.slab_floats && need_cslab <= w.cslab_floats && (!train || w.has_train)) return;
     (void)hipStreamSynchronize(stream());
     const int64_t cap = std::max(S, w.cap);
     const int64_t slab = std::max({need_slab, w.slab_floats, (int64_t)d1_split(L, cap, kc) * cap * 64});
     const bool tr = train || w.has_train;
+    const int64_t cslab = std::max({need_cslab, w.cslab_floats, conv_slab_floats(L, cap, tr)});
     qwork_free(w);
     w.cap = cap;
     w.slab_floats = slab;
+    w.cslab_floats = cslab;
+    w.cslab = dalloc<float>((size_t)std::max<int64_t>(cslab, 1));
     w.a1 = dalloc<float>((size_t)cap * L.ncell * 16);
     w.a2 = dalloc<float>((size_t)cap * L.ncell * 32);
     w.a3 = dalloc<float>((size_t)cap * L.K1);
@@ -448,23 +520,19 @@ void qnet_forward(const QLayout &L, const float *th, const BoardSrc &src, int64_
             conv1_fwd_kernel<2><<<grid, 256, 0, s>>>(src, th + L.off_w1, th + L.off_b1, w.a1, S, bs);
         launch_check("conv1_fwd_kernel");
     }
-    if (only < 0 || only == 1) {   // conv2: M = S*bs^2, K = 9*16, N = 32
-        AConvFwd<16, 3, 1> al{w.a1, bs, bs, FastDiv(nc), FastDiv(bs)};
-        gemm<1>(al, BRowMajor{th + L.off_w2, 144, 32}, EpBiasRelu{w.a2, th + L.off_b2, (int)(S * nc), 32, 1},
-                S * nc, 32, 144, 1, 144, s);
-    }
-    if (only < 0 || only == 2) {   // conv3: M = S*Wo^2, K = 36*32, N = 64
-        const int no = L.Wo * L.Wo;
-        AConvFwd<32, 6, 0> al{w.a2, bs, L.Wo, FastDiv(no), FastDiv(L.Wo)};
-        gemm<2>(al, BRowMajor{th + L.off_w3, 1152, 64}, EpBiasRelu{w.a3, th + L.off_b3, (int)(S * no), 64, 1},
-                S * no, 64, 1152, 1, 1152, s);
-    }
+    if (only < 0 || only == 1)   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
+        conv_fwd<16, 32, 3, 1>(w.a1, th + L.off_w2, th + L.off_b2, w.a2, S * nc, bs, bs, w, s);
+    if (only < 0 || only == 2)   // conv3: M = S*Wo^2, K = 36 offsets x 32, N = 64
+        conv_fwd<32, 64, 6, 0>(w.a2, th + L.off_w3, th + L.off_b3, w.a3, S * L.Wo * L.Wo, bs, L.Wo, w, s);
     int kc;
     const int ks = d1_split(L, S, kc);
-    // Dense1 (split-K partial sums; bias + relu in the head)
-    if (only < 0 || only == 3)
-        gemm<2>(ARowMajor{w.a3, L.K1, L.K1}, BRowMajor{th + L.off_d1w, L.K1, 64}, EpSlab{w.slab, (int)S, 64}, S, 64,
-                L.K1, ks, kc, s);
+    // Dense1 (split over the Wo^2 positions into partial slabs; bias + relu in the head)
+    if (only < 0 || only == 3) {
+        ConvArgs a{};
+        a.x = w.a3; a.w = th + L.off_d1w; a.out = w.slab; a.M = (int)S; a.HIN = L.Wo; a.HOUT = 1;
+        a.nkk = L.Wo * L.Wo;
+        conv_launch<64, 64, 0, 0, MODE_DENSE, EPI_SLAB>(a, ks, s);
+    }
     if (only >= 0 && only != 4) return;
     const int grid = ceil_div(S, 4);
     switch (mode) {
@@ -521,8 +589,23 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
     gemm<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64},
             EpSlab{slab, 1153, 64}, 1153, 64, S * no, p.ks_c3, p.kc_c3, s);
     reduce_into(slab, p.ks_c3, 1153 * 64, grad + L.off_w3, s);
-    gemm<1>(AConvDx<64, 6, 0>{w.dz3, bs, L.Wo, FastDiv(nc), FastDiv(bs)}, BConvT<32, 64>{th + L.off_w3, 2304},
-            EpReluMask{w.dz2, w.a2, (int)(S * nc), 32}, S * nc, 32, 2304, 1, 2304, s);
+    {
+        ConvArgs a{};
+        a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs; a.nkk = 36;
+        const int sp = conv_splits(S * nc, 36);
+        if (sp == 1) {
+            a.out = w.dz2;
+            conv_launch<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK>(a, 1, s);
+        } else {
+            a.out = w.cslab;
+            SNK_CHECK((int64_t)sp * S * nc * 32 <= w.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
+            conv_launch<64, 32, 6, 0, MODE_DX, EPI_SLAB>(a, sp, s);
+            const int used = ceil_div(36, ceil_div(36, sp));
+            conv_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(S * nc * 32, 256), 4096), 256, 0, s>>>(
+                w.cslab, used, S * nc * 32, 32, nullptr, w.a2, w.dz2);
+            launch_check("conv_reduce_kernel");
+        }
+    }
     // conv2
     gemm<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32},
             EpSlab{slab, 145, 32}, 145, 32, S * nc, p.ks_c2, p.kc_c2, s);

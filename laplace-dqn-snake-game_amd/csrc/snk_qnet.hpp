@@ -14,6 +14,7 @@
 // W[p*64 + c][o] matching the device activation layout [s][p][c].
 // Activations: [sample][position p = i + j*H (column-major)][channel].
 #pragma once
+#include "snk_conv.hpp"
 #include "snk_gemm.hpp"
 #include "snk_internal.hpp"
 
@@ -51,8 +52,9 @@ struct BoardSrc {
 
 // Device workspace for one batch geometry
 struct QWork {
-    int64_t cap = 0, slab_floats = 0;
+    int64_t cap = 0, slab_floats = 0, cslab_floats = 0;
     float *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *slab = nullptr, *h1 = nullptr, *q = nullptr;
+    float *cslab = nullptr;   // partial sums of kk-split convolutions
     // training only
     float *dq = nullptr, *dz1 = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dzc1 = nullptr;
     double *target = nullptr, *loss = nullptr;
