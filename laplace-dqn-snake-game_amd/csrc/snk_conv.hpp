@@ -11,7 +11,8 @@
 //
 // Workgroup = 4 waves = 128 rows x CN columns. Per kernel offset kk the
 // workgroup stages that offset's CK x CN weight block into LDS as [n][c]
-// (c contiguous, row padded by 4 floats: conflict-free ds_read_b128), double
+// (c contiguous, row padded by 4 floats: conflict-free ds_read_b128; filled by
+// 16-byte copies from a weight image already laid out [kk][n][c]), double
 // buffered with one barrier per offset; each lane reads its A operand as
 // float4 along c straight from global/L2 (every im2col row is a contiguous
 // channel run) one offset ahead. A lane's float4 covers 4 consecutive MFMA
@@ -29,7 +30,7 @@ enum ConvEpi { EPI_BIAS_RELU = 0, EPI_SLAB = 1, EPI_RELU_MASK = 2 };
 
 struct ConvArgs {
     const float *x;      // A source [S][HIN*HIN][CK]
-    const float *w;      // packed conv weights [KS*KS][CIN][COUT] of the layer
+    const float *w;      // weight image [nkk][CN][CK]
     const float *bias;   // EPI_BIAS_RELU
     const float *act;    // EPI_RELU_MASK: mask source, same shape as out
     float *out;          // [M][CN] or slab [split][M][CN]
@@ -85,19 +86,12 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
         for (int q = 0; q < NV; ++q) {
             const int e4 = tid + q * 256;
             if (e4 >= CK * CN / 4) continue;
+            // weight block [n][c] with c contiguous: DX reads the packed layout
+            // [kk][ci = n][co = c]; FWD / DENSE read the transposed copy
+            // [kk][co = n][ci = c] (snk_qnet: transpose_fwd_weights)
             const int e = e4 * 4;
-            if (MODE == MODE_DX) {
-                // weight block [ci = n][co = c]: c contiguous already
-                const int n = e / CK, c = e - n * CK;
-                *reinterpret_cast<float4 *>(&Bs[buf][n * LDB + c]) = bv[q];
-            } else {
-                // weight block [c][n]: transpose to [n][c]
-                const int c = e / CN, n = e - c * CN;
-                Bs[buf][(n + 0) * LDB + c] = bv[q].x;
-                Bs[buf][(n + 1) * LDB + c] = bv[q].y;
-                Bs[buf][(n + 2) * LDB + c] = bv[q].z;
-                Bs[buf][(n + 3) * LDB + c] = bv[q].w;
-            }
+            const int n = e / CK, c = e - n * CK;
+            *reinterpret_cast<float4 *>(&Bs[buf][n * LDB + c]) = bv[q];
         }
     };
     auto load_a = [&](int kk, float4 (&av)[KB]) {

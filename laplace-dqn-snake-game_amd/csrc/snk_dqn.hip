@@ -44,6 +44,15 @@ void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, 
     copy_if_due_kernel<<<(unsigned)std::min<int64_t>(ceil_div(h->L.P, 256), 2048), 256, 0, s>>>(
         h->theta_q, h->theta_t, h->L.P, counter, rate);
     launch_check("copy_if_due_kernel");
+    copy_if_due_kernel<<<(unsigned)std::min<int64_t>(ceil_div(h->L.T, 256), 2048), 256, 0, s>>>(
+        h->wt_q, h->wt_t, h->L.T, counter, rate);
+    launch_check("copy_if_due_kernel");
+}
+
+void dqn_q_changed(snk_dqn_s *h, hipStream_t s) { transpose_fwd_launch(h->L, h->theta_q, h->wt_q, s); }
+
+static const float *which_wt(snk_dqn_s *h, int32_t which) {
+    return which == SNK_NET_TARGET ? h->wt_t : h->wt_q;
 }
 
 BoardSrc src_env(const EnvDev &E) {
@@ -91,11 +100,11 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
     ta.gamma = gamma;
     ta.target = h->trn.target;
     ta.B = B;
-    qnet_forward(h->L, h->theta_t, sn_src, B, h->tgt, HEAD_TARGET, ta, s);
+    qnet_forward(h->L, h->theta_t, h->wt_t, sn_src, B, h->tgt, HEAD_TARGET, ta, s);
     HeadArgs la = ta;
     la.loss = h->trn.loss;
     la.dq = h->trn.dq;
-    qnet_forward(h->L, h->theta_q, s_src, B, h->trn, HEAD_LOSS, la, s);
+    qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s);
     qnet_backward(h->L, h->theta_q, s_src, B, h->trn, h->grad, h->slab, h->slab_cap, s);
     loss_mean_launch(h->trn.loss, B, h->loss_dev, s);
 }
@@ -147,7 +156,10 @@ extern "C" int snk_dqn_create(snk_dqn *out, int32_t bs, int32_t C, float lr, flo
         hipStream_t s = stream();
         SNK_HIP(hipMemcpyAsync(h->perm, perm.data(), P * 4, hipMemcpyHostToDevice, s));
         SNK_HIP(hipMemcpyAsync(h->tmp, flux.data(), P * 4, hipMemcpyHostToDevice, s));
+        h->wt_q = dalloc<float>(h->L.T);
+        h->wt_t = dalloc<float>(h->L.T);
         dqn_permute(h, h->tmp, h->theta_q, true, s);
+        dqn_q_changed(h, s);
         dqn_sync_target_launch(h, nullptr, 1, s);   // t_net = deepcopy(q_net) (structs.jl:177)
         SNK_HIP(hipMemsetAsync(h->acc, 0, P * 4, s));
         SNK_HIP(hipMemsetAsync(h->grad, 0, P * 4, s));
@@ -165,7 +177,8 @@ extern "C" int snk_dqn_destroy(snk_dqn h) {
         qwork_free(h->tgt);
         qwork_free(h->trn);
         for (void *p : {(void *)h->theta_q, (void *)h->theta_t, (void *)h->acc, (void *)h->grad, (void *)h->tmp,
-                        (void *)h->perm, (void *)h->slab, (void *)h->loss_dev, (void *)h->meta})
+                        (void *)h->perm, (void *)h->slab, (void *)h->loss_dev, (void *)h->meta, (void *)h->wt_q,
+                        (void *)h->wt_t})
             dfree(p);
         delete h;
     });
@@ -196,6 +209,8 @@ extern "C" int snk_dqn_set_params(snk_dqn h, int32_t which, const float *flux_ho
         hipStream_t s = stream();
         SNK_HIP(hipMemcpyAsync(h->tmp, flux_host, h->L.P * 4, hipMemcpyHostToDevice, s));
         dqn_permute(h, h->tmp, dst, true, s);
+        if (which == SNK_NET_Q) dqn_q_changed(h, s);
+        if (which == SNK_NET_TARGET) transpose_fwd_launch(h->L, h->theta_t, h->wt_t, s);
         SNK_HIP(hipStreamSynchronize(s));
     });
 }
@@ -231,7 +246,7 @@ extern "C" int snk_dqn_forward(snk_dqn h, int32_t which, const float *x_dev, int
         SNK_CHECK(which == SNK_NET_Q || which == SNK_NET_TARGET, SNK_ERR_INVALID, "forward needs q or target net");
         hipStream_t s = stream();
         qwork_ensure(h->act, h->L, B, false);
-        qnet_forward(h->L, which_buf(h, which), src_float(h->L, x_dev), B, h->act, HEAD_Q, HeadArgs{}, s);
+        qnet_forward(h->L, which_buf(h, which), which_wt(h, which),src_float(h->L, x_dev), B, h->act, HEAD_Q, HeadArgs{}, s);
         SNK_HIP(hipMemcpyAsync(q_dev, h->act.q, B * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
     });
 }
@@ -243,7 +258,7 @@ extern "C" int snk_dqn_forward_env(snk_dqn h, int32_t which, snk_env env, float 
         SNK_CHECK(E.bs == h->L.bs && E.C == h->L.C, SNK_ERR_INVALID, "env/model geometry mismatch");
         hipStream_t s = stream();
         qwork_ensure(h->act, h->L, E.n, false);
-        qnet_forward(h->L, which_buf(h, which), src_env(E), E.n, h->act, HEAD_Q, HeadArgs{}, s);
+        qnet_forward(h->L, which_buf(h, which), which_wt(h, which),src_env(E), E.n, h->act, HEAD_Q, HeadArgs{}, s);
         SNK_HIP(hipMemcpyAsync(q_dev, h->act.q, E.n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
     });
 }
@@ -260,7 +275,7 @@ extern "C" int snk_dqn_act(snk_dqn h, snk_env env, float epsilon, uint64_t seed,
         ha.epsilon = epsilon;
         ha.seed = seed;
         ha.tptr = &E.ctl->t;
-        qnet_forward(h->L, h->theta_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s);
+        qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s);
     });
 }
 
@@ -281,13 +296,13 @@ extern "C" int snk_dqn_time_act_layers(snk_dqn h, snk_env env, int32_t reps, dou
         ha.act = h->meta;
         ha.epsilon = 0.05f;
         ha.tptr = &E.ctl->t;
-        qnet_forward(h->L, h->theta_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s);
+        qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s);
         hipEvent_t a, b;
         SNK_HIP(hipEventCreate(&a));
         SNK_HIP(hipEventCreate(&b));
         for (int layer = 0; layer < 5; ++layer) {
             SNK_HIP(hipEventRecord(a, s));
-            for (int r = 0; r < reps; ++r) qnet_forward(h->L, h->theta_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, layer);
+            for (int r = 0; r < reps; ++r) qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, layer);
             SNK_HIP(hipEventRecord(b, s));
             SNK_HIP(hipEventSynchronize(b));
             float ms = 0.0f;
@@ -359,6 +374,7 @@ extern "C" int snk_dqn_apply_grad(snk_dqn h) {
     return guard([&] {
         SNK_CHECK(h, SNK_ERR_INVALID, "NULL argument");
         rmsprop_launch(h->L.P, h->theta_q, h->acc, h->grad, h->lr, h->rho, h->eps, stream());
+        dqn_q_changed(h, stream());
     });
 }
 

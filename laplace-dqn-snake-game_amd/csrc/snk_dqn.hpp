@@ -6,6 +6,7 @@ struct snk_dqn_s {
     snk::QLayout L{};
     float lr = 5e-4f, rho = 0.9f, eps = 1e-8f;
     float *theta_q = nullptr, *theta_t = nullptr, *acc = nullptr, *grad = nullptr, *tmp = nullptr;
+    float *wt_q = nullptr, *wt_t = nullptr;   // forward weight images of q_net / t_net
     int32_t *perm = nullptr;        // packed index -> Flux.destructure index
     snk::QWork act, tgt, trn;       // workspaces: acting (n_envs), target net, training batch
     float *slab = nullptr;
@@ -28,4 +29,6 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
                    double gamma, hipStream_t s);
 void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, hipStream_t s);
 void dqn_permute(snk_dqn_s *h, const float *src, float *dst, bool to_packed, hipStream_t s);
+// q_net parameters changed: rebuild its forward weight image
+void dqn_q_changed(snk_dqn_s *h, hipStream_t s);
 }  // namespace snk

@@ -1,9 +1,8 @@
 // snk_gemm.hpp — generic fp32 MFMA implicit-GEMM engine for the Q-net.
 //
 // C[M][N] = sum_k A[M][K] * B[K][N] on v_mfma_f32_32x32x2_f32 (exact f32,
-// gfx950 has no xf32). A wave owns a 32-row tile and NT 32-column tiles; a
-// 256-thread workgroup stacks 4 waves along M. grid = (M tiles / 4, N groups,
-// K splits). Operands come from LOADER functors so one engine serves the
+// gfx950 has no xf32). A workgroup owns a 32-row x NT*32-column tile.
+// grid = (M tiles, N groups, K splits). Operands come from LOADER functors so one engine serves the
 // forward convolutions (implicit im2col), the data-gradient "transposed"
 // convolutions and the weight-gradient reductions of the backward pass.
 //
@@ -19,30 +18,79 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int acc_row(int g, int lane) { return (g & 3) + 8 * (g >> 2) + 4 * (lane >> 5); }
 
-template <int NT, class AL, class BL, class EP>
-__global__ __launch_bounds__(256) void gemm_kernel(AL al, BL bl, EP ep, int M, int K, int kchunk) {
+// KW waves per workgroup share ONE 32 x (NT*32) output tile and split its
+// K range among themselves; their accumulators are summed through LDS by the
+// whole workgroup (no global partials). grid.z adds K splits across workgroups that
+// write partial slabs (EpSlab) when even that is too little parallelism.
+// The k loop moves 8 k (4 MFMA steps) per iteration with the next
+// iteration's operands loaded ahead (software pipeline).
+template <int NT, int KW, class AL, class BL, class EP>
+__global__ __launch_bounds__(64 * KW) void gemm_kernel(AL al, BL bl, EP ep, int M, int K, int kchunk) {
+    __shared__ float red[KW > 1 ? KW * NT * 16 * 64 : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int m0 = (blockIdx.x * 4 + wave) * 32;
-    if (m0 >= M) return;
+    const int m0 = blockIdx.x * 32;
     const int r = lane & 31, h = lane >> 5;
     const int n0 = blockIdx.y * (NT * 32);
     const int kb = blockIdx.z * kchunk;
     const int ke = min(K, kb + kchunk);
+    const int sub = (((ke - kb) + KW - 1) / KW + 7) & ~7;
+    const int wb = kb + wave * sub;
+    const int we = min(ke, wb + sub);
     f32x16 acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int g = 0; g < 16; ++g) acc[nt][g] = 0.0f;
     const auto ctx = al.row(m0 + r, M);
-#pragma unroll 4
-    for (int k = kb; k < ke; k += 2) {
-        const float a = al.load(ctx, k + h, ke);
+    float a_c[4], b_c[4][NT], a_n[4], b_n[4][NT];
+    auto load = [&](int k, float (&av)[4], float (&bv)[4][NT]) {
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-            const float b = bl.load(k + h, n0 + nt * 32 + r, ke);
-            acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[nt], 0, 0, 0);
+        for (int i = 0; i < 4; ++i) {
+            const int kk = k + 2 * i + h;
+            const bool v = kk < we;
+            av[i] = v ? al.load(ctx, kk, we) : 0.0f;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) bv[i][nt] = v ? bl.load(kk, n0 + nt * 32 + r, we) : 0.0f;
+        }
+    };
+    if (wb < we) load(wb, a_c, b_c);
+    for (int k = wb; k < we; k += 8) {
+        const bool more = k + 8 < we;
+        if (more) load(k + 8, a_n, b_n);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_c[i], b_c[i][nt], acc[nt], 0, 0, 0);
+        if (more) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a_c[i] = a_n[i];
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) b_c[i][nt] = b_n[i][nt];
+            }
         }
     }
+    if (KW > 1) {
+        // every wave parks its tile in LDS; the workgroup then sums the KW
+        // copies element by element (fixed wave order: deterministic)
+        float *dst = red + wave * NT * 16 * 64;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) dst[(nt * 16 + g) * 64 + lane] = acc[nt][g];
+        __syncthreads();
+        if (m0 >= M) return;
+        for (int e = threadIdx.x; e < NT * 16 * 64; e += 64 * KW) {
+            float v = red[e];
+#pragma unroll
+            for (int w = 1; w < KW; ++w) v += red[w * NT * 16 * 64 + e];
+            const int nt = e >> 10, g = (e >> 6) & 15, ln = e & 63;
+            ep.store1(v, m0 + acc_row(g, ln), n0 + nt * 32 + (ln & 31), (int)blockIdx.z);
+        }
+        return;
+    }
+    if (m0 >= M) return;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) ep.store(acc[nt], m0, n0 + nt * 32, lane, (int)blockIdx.z);
 }
@@ -52,6 +100,12 @@ struct EpBiasRelu {  // y[row][col] = relu?(acc + bias[col])
     float *y;
     const float *bias;
     int M, N, relu;
+    __device__ void store1(float v, int row, int col, int) const {
+        if (row >= M || col >= N) return;
+        v += bias ? bias[col] : 0.0f;
+        if (relu) v = v > 0.0f ? v : 0.0f;
+        y[(int64_t)row * N + col] = v;
+    }
     __device__ void store(const f32x16 &acc, int m0, int c0, int lane, int) const {
         const int col = c0 + (lane & 31);
         if (col >= N) return;
@@ -70,6 +124,9 @@ struct EpBiasRelu {  // y[row][col] = relu?(acc + bias[col])
 struct EpSlab {  // partial sums of K-split z: slab[z][row][col]
     float *slab;
     int M, N;
+    __device__ void store1(float v, int row, int col, int z) const {
+        if (row < M && col < N) slab[(int64_t)z * M * N + (int64_t)row * N + col] = v;
+    }
     __device__ void store(const f32x16 &acc, int m0, int c0, int lane, int z) const {
         const int col = c0 + (lane & 31);
         if (col >= N) return;
@@ -85,6 +142,11 @@ struct EpReluMask {  // y = (act > 0) ? acc : 0   (backward through relu)
     float *y;
     const float *act;
     int M, N;
+    __device__ void store1(float v, int row, int col, int) const {
+        if (row >= M || col >= N) return;
+        const int64_t o = (int64_t)row * N + col;
+        y[o] = act[o] > 0.0f ? v : 0.0f;
+    }
     __device__ void store(const f32x16 &acc, int m0, int c0, int lane, int) const {
         const int col = c0 + (lane & 31);
         if (col >= N) return;

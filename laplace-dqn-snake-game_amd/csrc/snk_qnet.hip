@@ -35,7 +35,35 @@ QLayout make_layout(int bs, int C) {
     L.off_d2w = o; o += 3 * 64;
     L.off_d2b = o; o += 3;
     L.P = o;
+    L.off_t2 = 0;
+    L.off_t3 = 9 * 32 * 16;
+    L.off_td = L.off_t3 + 36 * 64 * 32;
+    L.T = L.off_td + (int64_t)L.Wo * L.Wo * 64 * 64;
     return L;
+}
+
+// block [nkk][CK][CN] of theta -> [nkk][CN][CK] of the image (c contiguous per output)
+__global__ void transpose_fwd_kernel(const float *__restrict__ th, float *__restrict__ wt, QLayout L) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < L.T; t += (int64_t)gridDim.x * blockDim.x) {
+        int64_t base, u;
+        int CK, CN;
+        if (t < L.off_t3) {
+            u = t; base = L.off_w2; CK = 16; CN = 32;
+        } else if (t < L.off_td) {
+            u = t - L.off_t3; base = L.off_w3; CK = 32; CN = 64;
+        } else {
+            u = t - L.off_td; base = L.off_d1w; CK = 64; CN = 64;
+        }
+        const int64_t kk = u / (CK * CN);
+        const int r = (int)(u - kk * CK * CN);
+        const int n = r / CK, c = r - n * CK;
+        wt[t] = th[base + (kk * CK + c) * CN + n];
+    }
+}
+
+void transpose_fwd_launch(const QLayout &L, const float *theta, float *wt, hipStream_t s) {
+    transpose_fwd_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.T, 256), 2048), 256, 0, s>>>(theta, wt, L);
+    launch_check("transpose_fwd_kernel");
 }
 
 void packed_to_flux_index(const QLayout &L, int32_t *perm) {
@@ -208,22 +236,37 @@ struct ADenseDw {  // row m = input feature (m == KW: bias ones), k = sample r: 
 };
 
 // ---------------------------------------------------------------- launch helpers
-static void choose_split(int64_t waves, int64_t K, int &ks, int &kchunk) {
-    const int64_t target = 2048;
-    int64_t want = std::max<int64_t>(1, target / std::max<int64_t>(1, waves));
-    const int64_t maxks = std::max<int64_t>(1, K / 64);
-    int64_t k = std::min(want, maxks);
-    int64_t chunk = (K + k - 1) / k;
-    chunk = (chunk + 1) & ~int64_t(1);
-    ks = (int)((K + chunk - 1) / chunk);
-    kchunk = (int)chunk;
+
+// kw waves per output tile (intra-workgroup split-K, LDS reduce) and z
+// workgroup splits (partial slabs) chosen to put ~1 wave on every SIMD while
+// keeping >= 64 k per wave.
+struct GemmPlan {
+    int kw, z, kchunk;
+};
+static GemmPlan plan_gemm(int64_t M, int N, int NT, int64_t K, bool allow_z) {
+    const int64_t tiles = ceil_div(M, 32) * ceil_div(N, NT * 32);
+    // these GEMMs (the B = 64 backward) are latency-bound: many short waves
+    const int64_t target = 4096;
+    int kw = 1;
+    while (kw < 8 && tiles * kw * 2 <= target && K / (kw * 2) >= 32) kw *= 2;
+    int z = 1;
+    if (allow_z)
+        while (z < 64 && tiles * kw * z * 2 <= target && K / ((int64_t)kw * z * 2) >= 32) z *= 2;
+    int64_t chunk = ceil_div(K, z);
+    chunk = (chunk + 7) & ~int64_t(7);
+    return GemmPlan{kw, (int)ceil_div(K, chunk), (int)chunk};
 }
 
 template <int NT, class AL, class BL, class EP>
-static void gemm(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int64_t K, int ks, int kchunk,
+static void gemm(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int64_t K, const GemmPlan &p,
                  hipStream_t s) {
-    dim3 grid((unsigned)ceil_div(M, 128), (unsigned)ceil_div(N, NT * 32), (unsigned)ks);
-    gemm_kernel<NT><<<grid, 256, 0, s>>>(al, bl, ep, (int)M, (int)K, kchunk);
+    dim3 grid((unsigned)ceil_div(M, 32), (unsigned)ceil_div(N, NT * 32), (unsigned)p.z);
+    switch (p.kw) {
+        case 1: gemm_kernel<NT, 1><<<grid, 64, 0, s>>>(al, bl, ep, (int)M, (int)K, p.kchunk); break;
+        case 2: gemm_kernel<NT, 2><<<grid, 128, 0, s>>>(al, bl, ep, (int)M, (int)K, p.kchunk); break;
+        case 4: gemm_kernel<NT, 4><<<grid, 256, 0, s>>>(al, bl, ep, (int)M, (int)K, p.kchunk); break;
+        default: gemm_kernel<NT, 8><<<grid, 512, 0, s>>>(al, bl, ep, (int)M, (int)K, p.kchunk); break;
+    }
     launch_check("gemm_kernel");
 }
 
@@ -231,7 +274,7 @@ static void gemm(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int
 static int conv_splits(int64_t M, int nkk) {
     const int64_t wgs = ceil_div(M, 128);
     if (wgs >= 512) return 1;
-    return (int)std::min<int64_t>(nkk, ceil_div(512, wgs));
+    return (int)std::min<int64_t>(std::min(nkk, 16), ceil_div(512, wgs));
 }
 
 template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
@@ -300,6 +343,9 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(BoardSrc src, const floa
         float acc[16];
 #pragma unroll
         for (int co = 0; co < 16; ++co) acc[co] = sw[9 * C * 16 + co];
+        const int8_t *pl[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) pl[c] = src.plane(s, c);
 #pragma unroll
         for (int kk = 0; kk < 9; ++kk) {
             const int du = kk % 3, dv = kk / 3;
@@ -307,7 +353,8 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(BoardSrc src, const floa
             if (xi < 0 || xi >= bs || xj < 0 || xj >= bs) continue;
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const float v = src.load(s, c, xi + xj * bs);
+                const int cell = xi + xj * bs;
+                const float v = pl[c] ? (float)pl[c][cell] : src.fbase[(s * C + c) * ncell + cell];
 #pragma unroll
                 for (int co = 0; co < 16; ++co) acc[co] = __builtin_fmaf(v, sw[(kk * C + c) * 16 + co], acc[co]);
             }
@@ -395,21 +442,27 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float *__restrict__
     dz1[s * 64 + lane] = h1[s * 64 + lane] > 0.0f ? g : 0.0f;
 }
 
-// Dense2 weight/bias gradient: 195 outputs, reduction over S
-__global__ void d2_grad_kernel(const float *__restrict__ dq, const float *__restrict__ h1, int64_t S, QLayout L,
-                               float *__restrict__ grad) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 195) return;
+// Dense2 weight/bias gradient: 195 outputs reduced over S, the batch staged
+// through LDS 64 samples at a time (coalesced loads, no dependent global reads)
+__global__ __launch_bounds__(256) void d2_grad_kernel(const float *__restrict__ dq, const float *__restrict__ h1,
+                                                      int64_t S, QLayout L, float *__restrict__ grad) {
+    __shared__ float sdq[64 * 3], sh[64 * 64];
+    const int t = threadIdx.x;
+    const int a = t < 192 ? t / 64 : t - 192, o = t < 192 ? t - a * 64 : 0;
     float acc = 0.0f;
-    if (t < 192) {
-        const int a = t / 64, o = t - a * 64;
-        for (int64_t s = 0; s < S; ++s) acc = __builtin_fmaf(dq[s * 3 + a], h1[s * 64 + o], acc);
-        grad[L.off_d2w + t] = acc;
-    } else {
-        const int a = t - 192;
-        for (int64_t s = 0; s < S; ++s) acc += dq[s * 3 + a];
-        grad[L.off_d2b + a] = acc;
+    for (int64_t s0 = 0; s0 < S; s0 += 64) {
+        const int n = (int)min((int64_t)64, S - s0);
+        __syncthreads();
+        for (int i = t; i < n * 64; i += 256) sh[i] = h1[s0 * 64 + i];
+        if (t < n * 3) sdq[t] = dq[s0 * 3 + t];
+        __syncthreads();
+        if (t < 192)
+            for (int k = 0; k < n; ++k) acc = __builtin_fmaf(sdq[k * 3 + a], sh[k * 64 + o], acc);
+        else if (t < 195)
+            for (int k = 0; k < n; ++k) acc += sdq[k * 3 + a];
     }
+    if (t < 192) grad[L.off_d2w + t] = acc;
+    else if (t < 195) grad[L.off_d2b + a] = acc;
 }
 
 __global__ void slab_reduce_kernel(const float *__restrict__ slab, int ks, int64_t MN, float *__restrict__ out) {
@@ -508,7 +561,8 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
 }
 
 // ---------------------------------------------------------------- forward
-void qnet_forward(const QLayout &L, const float *th, const BoardSrc &src, int64_t S, QWork &w, HeadMode mode,
+void qnet_forward(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
+                  HeadMode mode,
                   const HeadArgs &ha, hipStream_t s, int only) {
     const int bs = L.bs, nc = L.ncell;
     if (only < 0 || only == 0) {
@@ -521,15 +575,15 @@ void qnet_forward(const QLayout &L, const float *th, const BoardSrc &src, int64_
         launch_check("conv1_fwd_kernel");
     }
     if (only < 0 || only == 1)   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
-        conv_fwd<16, 32, 3, 1>(w.a1, th + L.off_w2, th + L.off_b2, w.a2, S * nc, bs, bs, w, s);
+        conv_fwd<16, 32, 3, 1>(w.a1, wt + L.off_t2, th + L.off_b2, w.a2, S * nc, bs, bs, w, s);
     if (only < 0 || only == 2)   // conv3: M = S*Wo^2, K = 36 offsets x 32, N = 64
-        conv_fwd<32, 64, 6, 0>(w.a2, th + L.off_w3, th + L.off_b3, w.a3, S * L.Wo * L.Wo, bs, L.Wo, w, s);
+        conv_fwd<32, 64, 6, 0>(w.a2, wt + L.off_t3, th + L.off_b3, w.a3, S * L.Wo * L.Wo, bs, L.Wo, w, s);
     int kc;
     const int ks = d1_split(L, S, kc);
     // Dense1 (split over the Wo^2 positions into partial slabs; bias + relu in the head)
     if (only < 0 || only == 3) {
         ConvArgs a{};
-        a.x = w.a3; a.w = th + L.off_d1w; a.out = w.slab; a.M = (int)S; a.HIN = L.Wo; a.HOUT = 1;
+        a.x = w.a3; a.w = wt + L.off_td; a.out = w.slab; a.M = (int)S; a.HIN = L.Wo; a.HOUT = 1;
         a.nkk = L.Wo * L.Wo;
         conv_launch<64, 64, 0, 0, MODE_DENSE, EPI_SLAB>(a, ks, s);
     }
@@ -545,29 +599,47 @@ void qnet_forward(const QLayout &L, const float *th, const BoardSrc &src, int64_
 }
 
 // ---------------------------------------------------------------- backward
+// weight-gradient GEMMs: M = weight rows (+1 bias row of ones), N = out channels,
+// K = rows (sample, position) of the layer output
 struct BwdPlan {
-    int ks_d1, kc_d1, ks_c3, kc_c3, ks_c2, kc_c2, ks_c1, kc_c1;
+    GemmPlan d1, c3, c2, c1, d1x, c2x;
 };
 static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
     BwdPlan p;
-    choose_split(ceil_div(L.K1 + 1, 32), S, p.ks_d1, p.kc_d1);
-    choose_split(ceil_div(1153, 32) * 1, S * L.Wo * L.Wo, p.ks_c3, p.kc_c3);
-    choose_split(ceil_div(145, 32), S * L.ncell, p.ks_c2, p.kc_c2);
-    choose_split(ceil_div(9 * L.C + 1, 32), S * L.ncell, p.ks_c1, p.kc_c1);
+    p.d1 = plan_gemm(L.K1 + 1, 64, 2, S, true);
+    p.c3 = plan_gemm(1153, 64, 2, S * L.Wo * L.Wo, true);
+    p.c2 = plan_gemm(145, 32, 1, S * L.ncell, true);
+    p.c1 = plan_gemm(9 * L.C + 1, 16, 1, S * L.ncell, true);
+    p.d1x = plan_gemm(S, L.K1, 2, 64, false);
+    p.c2x = plan_gemm(S * L.ncell, 16, 1, 288, false);
     return p;
 }
+static int64_t zslab(const GemmPlan &g, int64_t MN) { return g.z > 1 ? (int64_t)g.z * MN : 0; }
 int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S) {
     const BwdPlan p = bwd_plan(L, S);
-    int64_t m = (int64_t)p.ks_d1 * (L.K1 + 1) * 64;
-    m = std::max(m, (int64_t)p.ks_c3 * 1153 * 64);
-    m = std::max(m, (int64_t)p.ks_c2 * 145 * 32);
-    m = std::max(m, (int64_t)p.ks_c1 * (9 * L.C + 1) * 16);
-    return m;
+    int64_t m = zslab(p.d1, (int64_t)(L.K1 + 1) * 64);
+    m = std::max(m, zslab(p.c3, 1153 * 64));
+    m = std::max(m, zslab(p.c2, 145 * 32));
+    m = std::max(m, zslab(p.c1, (int64_t)(9 * L.C + 1) * 16));
+    return std::max<int64_t>(m, 1);
 }
 
 static void reduce_into(const float *slab, int ks, int64_t MN, float *out, hipStream_t s) {
     slab_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(MN, 256), 2048), 256, 0, s>>>(slab, ks, MN, out);
     launch_check("slab_reduce_kernel");
+}
+
+// weight gradient straight into grad[off..] when one workgroup column covers K,
+// else through z partial slabs and a reduce
+template <int NT, class AL, class BL>
+static void wgrad(const AL &al, const BL &bl, int64_t M, int N, int64_t K, const GemmPlan &p, float *dst,
+                  float *slab, hipStream_t s) {
+    if (p.z == 1) {
+        gemm<NT>(al, bl, EpSlab{dst, (int)M, N}, M, N, K, p, s);
+    } else {
+        gemm<NT>(al, bl, EpSlab{slab, (int)M, N}, M, N, K, p, s);
+        reduce_into(slab, p.z, M * N, dst, s);
+    }
 }
 
 void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64_t S, QWork &w, float *grad,
@@ -580,15 +652,12 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
     d2_grad_kernel<<<1, 256, 0, s>>>(w.dq, w.h1, S, L, grad);
     launch_check("d2_grad_kernel");
     // Dense1: dW (+ bias row) and dX (relu mask on a3)
-    gemm<2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, EpSlab{slab, L.K1 + 1, 64}, L.K1 + 1, 64, S, p.ks_d1,
-            p.kc_d1, s);
-    reduce_into(slab, p.ks_d1, (int64_t)(L.K1 + 1) * 64, grad + L.off_d1w, s);
+    wgrad<2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, L.K1 + 1, 64, S, p.d1, grad + L.off_d1w, slab, s);
     gemm<2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + L.off_d1w, 64, L.K1, 64}, EpReluMask{w.dz3, w.a3, (int)S, L.K1},
-            S, L.K1, 64, 1, 64, s);
-    // conv3: dW over rows (s, pout); dX onto the 12x12x32 input (relu mask on a2)
-    gemm<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64},
-            EpSlab{slab, 1153, 64}, 1153, 64, S * no, p.ks_c3, p.kc_c3, s);
-    reduce_into(slab, p.ks_c3, 1153 * 64, grad + L.off_w3, s);
+            S, L.K1, 64, p.d1x, s);
+    // conv3: dW over rows (s, pout); dX onto the bs x bs x 32 input (relu mask on a2)
+    wgrad<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64}, 1153,
+             64, S * no, p.c3, grad + L.off_w3, slab, s);
     {
         ConvArgs a{};
         a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs; a.nkk = 36;
@@ -607,15 +676,13 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         }
     }
     // conv2
-    gemm<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32},
-            EpSlab{slab, 145, 32}, 145, 32, S * nc, p.ks_c2, p.kc_c2, s);
-    reduce_into(slab, p.ks_c2, 145 * 32, grad + L.off_w2, s);
+    wgrad<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32}, 145, 32,
+             S * nc, p.c2, grad + L.off_w2, slab, s);
     gemm<1>(AConvDx<32, 3, 1>{w.dz2, bs, bs, FastDiv(nc), FastDiv(bs)}, BConvT<16, 32>{th + L.off_w2, 288},
-            EpReluMask{w.dzc1, w.a1, (int)(S * nc), 16}, S * nc, 16, 288, 1, 288, s);
+            EpReluMask{w.dzc1, w.a1, (int)(S * nc), 16}, S * nc, 16, 288, p.c2x, s);
     // conv1 (weights only)
-    gemm<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
-            EpSlab{slab, 9 * L.C + 1, 16}, 9 * L.C + 1, 16, S * nc, p.ks_c1, p.kc_c1, s);
-    reduce_into(slab, p.ks_c1, (int64_t)(9 * L.C + 1) * 16, grad + L.off_w1, s);
+    wgrad<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16}, 9 * L.C + 1, 16,
+             S * nc, p.c1, grad + L.off_w1, slab, s);
 }
 
 void rmsprop_launch(int64_t P, float *theta, float *acc, const float *grad, float eta, float rho, float eps,

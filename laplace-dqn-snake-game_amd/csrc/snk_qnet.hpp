@@ -23,10 +23,14 @@ namespace snk {
 struct QLayout {
     int bs, C, ncell, Wo, K1;   // K1 = Wo*Wo*64 (Dense1 fan-in)
     int64_t off_w1, off_b1, off_w2, off_b2, off_w3, off_b3, off_d1w, off_d1b, off_d2w, off_d2b, P;
+    // forward weight image [kk][out][in] of conv2, conv3, Dense1 (size T)
+    int64_t off_t2, off_t3, off_td, T;
 };
 QLayout make_layout(int bs, int C);
 // flux index of every packed index (host)
 void packed_to_flux_index(const QLayout &L, int32_t *perm);
+// theta -> forward weight image (after every change of theta)
+void transpose_fwd_launch(const QLayout &L, const float *theta, float *wt, hipStream_t s);
 
 // Source of the Q-net input planes: env frame ring, replay slots, or a
 // float tensor in Julia (bs,bs,C,B) memory.
@@ -47,6 +51,13 @@ struct BoardSrc {
             p = base + (s * 3 + slot) * (int64_t)pitch;
         }
         return (float)p[cell];
+    }
+    // int8 plane of (sample, channel); nullptr in float mode
+    __device__ __forceinline__ const int8_t *plane(int64_t s, int c) const {
+        if (fbase) return nullptr;
+        if (idx) return base + idx[s] * (int64_t)replay_nf * pitch + (int64_t)(c + chan0) * pitch;
+        const int slot = (int)((*tptr + 3 - (C - 1 - c)) % 3);
+        return base + (s * 3 + slot) * (int64_t)pitch;
     }
 };
 
@@ -89,7 +100,7 @@ struct HeadArgs {
 // forward: q[S][3] into w.q (and w.h1); mode-specific epilogue
 // only = -1: the whole chain; 0..4: just conv1 / conv2 / conv3 / dense1 / head
 // (inputs from a previous full forward; used for per-layer timing)
-void qnet_forward(const QLayout &L, const float *theta, const BoardSrc &src, int64_t S, QWork &w,
+void qnet_forward(const QLayout &L, const float *theta, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
                   HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1);
 // backward of the loss whose dq sits in w.dq (after HEAD_LOSS): grad (packed) overwritten
 void qnet_backward(const QLayout &L, const float *theta, const BoardSrc &src, int64_t S, QWork &w,

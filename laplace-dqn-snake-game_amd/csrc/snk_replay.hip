@@ -43,37 +43,43 @@ __global__ void replay_gather_kernel(ReplayDev R, const int64_t *__restrict__ id
     }
 }
 
-// Floyd's algorithm: a uniformly random B-subset of [0, len). One wave; lane 0
-// draws sequentially against an open-addressing set in LDS.
-__global__ void replay_sample_kernel(const int64_t *__restrict__ count, int64_t cap, int32_t batch,
-                                     uint64_t seed, uint64_t draw, const int64_t *__restrict__ draw_dev,
-                                     int64_t *__restrict__ out, int32_t *__restrict__ b_out) {
-    if (draw_dev) draw = (uint64_t)*draw_dev;
-    constexpr int HS = 8192;
+// Floyd's algorithm: a uniformly random B-subset of [0, len). Step n draws
+// t_n uniform in [0, len-B+n] and keeps t_n unless already chosen, else
+// len-B+n. The B candidates are drawn in parallel (one thread each); one
+// thread then runs the short serial pass against an open-addressing set in LDS.
+__global__ __launch_bounds__(256) void replay_sample_kernel(const int64_t *__restrict__ count, int64_t cap,
+                                                            int32_t batch, uint64_t seed, uint64_t draw,
+                                                            const int64_t *__restrict__ draw_dev,
+                                                            int64_t *__restrict__ out, int32_t *__restrict__ b_out) {
+    constexpr int HS = 8192;   // >= 2 * max batch (4096)
     __shared__ int64_t set[HS];
+    __shared__ int64_t cand[4096];
+    if (draw_dev) draw = (uint64_t)*draw_dev;
     const int64_t len = min(*count, cap);
     const int B = (int)min((int64_t)batch, len);
-    const int hs = B * 2 <= 64 ? 128 : (B * 2 <= HS ? HS : HS);
+    int hs = 128;
+    while (hs < 2 * B) hs <<= 1;
     for (int i = threadIdx.x; i < hs; i += blockDim.x) set[i] = -1;
+    for (int n = threadIdx.x; n < B; n += blockDim.x) {
+        const uint64_t jp1 = (uint64_t)(len - B + n + 1);
+        cand[n] = (int64_t)__umul64hi(rng_hash(seed, draw, (uint64_t)n), jp1);   // [0, len-B+n]
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         if (b_out) *b_out = B;
-        int n = 0;
-        for (int64_t j = len - B; j < len; ++j) {
-            const uint64_t h = rng_hash(seed, draw, (uint64_t)n);
-            const int64_t t = (int64_t)(((unsigned __int128)h * (uint64_t)(j + 1)) >> 64);  // [0, j]
-            // membership of t
-            int p = (int)(splitmix64((uint64_t)t) & (hs - 1));
+        for (int n = 0; n < B; ++n) {
+            const int64_t t = cand[n];
+            int p = (int)(splitmix64((uint64_t)t) & (uint64_t)(hs - 1));
             bool found = false;
-            while (set[p] >= 0) {
-                if (set[p] == t) { found = true; break; }
-                p = (p + 1) & (hs - 1);
+            for (int64_t v; (v = set[p]) >= 0; p = (p + 1) & (hs - 1))
+                if (v == t) { found = true; break; }
+            const int64_t v = found ? len - B + n : t;
+            if (found) {
+                p = (int)(splitmix64((uint64_t)v) & (uint64_t)(hs - 1));
+                while (set[p] >= 0) p = (p + 1) & (hs - 1);
             }
-            const int64_t v = found ? j : t;
-            p = (int)(splitmix64((uint64_t)v) & (hs - 1));
-            while (set[p] >= 0) p = (p + 1) & (hs - 1);
             set[p] = v;
-            out[n++] = v;
+            out[n] = v;
         }
     }
 }
@@ -270,7 +276,7 @@ extern "C" int snk_replay_empty(snk_replay h) {
 namespace snk {
 void replay_launch_sample(const ReplayDev &d, int32_t batch, uint64_t seed, uint64_t draw,
                           const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s) {
-    replay_sample_kernel<<<1, 64, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev);
+    replay_sample_kernel<<<1, 256, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev);
     launch_check("replay_sample_kernel");
 }
 }  // namespace snk

@@ -122,7 +122,7 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
     ha.seed = h->cfg.seed;
     ha.tptr = &E.ctl->t;
     ha.eps_dev = &h->stats->epsilon;
-    qnet_forward(q->L, q->theta_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s);
+    qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s);
     env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s);
     env_launch_advance(E, &R, s);
     episode_stats_kernel<<<1, 1024, 0, s>>>(E.out_done, E.out_ep_reward, E.out_score, E.n, h->stats);
@@ -139,6 +139,7 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
         dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s);
         if (h->comm) comm_allreduce_mean(h->comm, q->grad, q->L.P, s);   // data-parallel replicas
         rmsprop_launch(q->L.P, q->theta_q, q->acc, q->grad, q->lr, q->rho, q->eps, s);
+        dqn_q_changed(q, s);
         dqn_sync_target_launch(q, &h->stats->updates, h->cfg.target_update_rate, s);
         post_update_kernel<<<1, 64, 0, s>>>(h->stats, q->loss_dev, h->loss_log, h->log_cap, h->cfg.decay,
                                             h->cfg.epsilon_end);
@@ -242,6 +243,7 @@ extern "C" int snk_trainer_set_comm(snk_trainer h, snk_comm comm) {
         snk_dqn_s *q = h->dqn;
         // replicas start from rank 0's q_net; t_net = q_net; fresh RMSProp state
         comm_broadcast(comm, q->theta_q, q->L.P, 0, s);
+        dqn_q_changed(q, s);
         dqn_sync_target_launch(q, nullptr, 1, s);
         SNK_HIP(hipMemsetAsync(q->acc, 0, q->L.P * sizeof(float), s));
         SNK_HIP(hipStreamSynchronize(s));
