@@ -25,6 +25,8 @@
 
 namespace snk {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 enum ConvMode { MODE_FWD = 0, MODE_DX = 1, MODE_DENSE = 2 };
 enum ConvEpi { EPI_BIAS_RELU = 0, EPI_SLAB = 1, EPI_RELU_MASK = 2 };
 
@@ -46,7 +48,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     constexpr int KB = CK / 8;
     constexpr int LDB = CK + 4;
     constexpr int NV = (CK * CN / 4 + 255) / 256;  // float4 staging loads per thread
-    __shared__ __attribute__((aligned(16))) float Bs[2][CN * LDB];
+    __shared__ __attribute__((aligned(16))) float Bs[2][CN * LDB + 4];   // + pad slot for idle stagers
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -72,80 +74,93 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
         for (int g = 0; g < 16; ++g) acc[nt][g] = 0.0f;
 
-    float4 bv[NV];
-    auto stage_load = [&](int kk) {
-        const float4 *src = reinterpret_cast<const float4 *>(a.w + (int64_t)kk * CK * CN);
+    // Every global load below is unconditional: out-of-range lanes read a safe
+    // in-bounds address and their value is zeroed arithmetically. A branch
+    // around a load makes hipcc wait vmcnt(0) for the in-flight prefetch.
+    constexpr int NE4 = CK * CN / 4;   // float4s per weight block
+    const f32x4 *wsrc = reinterpret_cast<const f32x4 *>(a.w);
+    int s_src[NV], s_dst[NV];          // staging: source float4 and LDS float offset
 #pragma unroll
-        for (int q = 0; q < NV; ++q) {
-            const int e4 = tid + q * 256;
-            bv[q] = e4 < CK * CN / 4 ? src[e4] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    auto stage_store = [&](int buf) {
+    for (int q = 0; q < NV; ++q) {
+        const int e4 = tid + q * 256;
+        const bool in = (NE4 % 256 == 0) || e4 < NE4;
+        const int e = (in ? e4 : 0) * 4;
+        const int n = e / CK, c = e - n * CK;
+        s_src[q] = in ? e4 : 0;
+        s_dst[q] = in ? n * LDB + c : CN * LDB;   // idle lanes write the pad slot
+    }
+
+    f32x4 bst[NV], a_cur[KB], a_nxt[KB];
+    // ---- prologue: weights of kk0 -> LDS, A of kk0 -> registers
+    {
 #pragma unroll
-        for (int q = 0; q < NV; ++q) {
-            const int e4 = tid + q * 256;
-            if (e4 >= CK * CN / 4) continue;
-            // weight block [n][c] with c contiguous: DX reads the packed layout
-            // [kk][ci = n][co = c]; FWD / DENSE read the transposed copy
-            // [kk][co = n][ci = c] (snk_qnet: transpose_fwd_weights)
-            const int e = e4 * 4;
-            const int n = e / CK, c = e - n * CK;
-            *reinterpret_cast<float4 *>(&Bs[buf][n * LDB + c]) = bv[q];
-        }
-    };
-    auto load_a = [&](int kk, float4 (&av)[KB]) {
-        const float *p;
-        bool valid = ok;
+        for (int q = 0; q < NV; ++q) bst[q] = wsrc[(int64_t)kk0 * NE4 + s_src[q]];
+        const float *p = xs;
+        float msk = ok ? 1.0f : 0.0f;
         if (MODE == MODE_DENSE) {
-            p = xs + kk * CK;
+            p = xs + kk0 * CK;
         } else {
-            const int dv = kk / KS, du = kk - dv * KS;
+            const int dv = kk0 / KS, du = kk0 - dv * KS;
             const int xi = MODE == MODE_FWD ? i + du - PAD : i - du + PAD;
             const int xj = MODE == MODE_FWD ? j + dv - PAD : j - dv + PAD;
-            valid = valid && xi >= 0 && xi < a.HIN && xj >= 0 && xj < a.HIN;
-            p = xs + (xi + xj * a.HIN) * CK;
+            const bool v = ok && xi >= 0 && xi < a.HIN && xj >= 0 && xj < a.HIN;
+            p = v ? xs + (xi + xj * a.HIN) * CK : xs;
+            msk = v ? 1.0f : 0.0f;
         }
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-            av[kb] = valid ? *reinterpret_cast<const float4 *>(p + kb * 8) : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-
-    float4 a_cur[KB], a_nxt[KB];
-    if (kk0 < kk1) {
-        stage_load(kk0);
-        stage_store(0);
-        load_a(kk0, a_cur);
+        for (int kb = 0; kb < KB; ++kb) {
+            a_cur[kb] = *reinterpret_cast<const f32x4 *>(p + kb * 8) * msk;
+        }
+#pragma unroll
+        for (int q = 0; q < NV; ++q) *reinterpret_cast<f32x4 *>(&Bs[0][s_dst[q]]) = bst[q];
     }
     __syncthreads();
     for (int kk = kk0; kk < kk1; ++kk) {
         const int buf = (kk - kk0) & 1;
-        const bool more = kk + 1 < kk1;
-        if (more) {
-            stage_load(kk + 1);
-            load_a(kk + 1, a_nxt);
+        const bool more = kk + 1 < kk1;   // wave-uniform
+        const int kn = more ? kk + 1 : kk;
+        // ---- prefetch kk+1 (weights to registers, A to registers)
+#pragma unroll
+        for (int q = 0; q < NV; ++q) bst[q] = wsrc[(int64_t)kn * NE4 + s_src[q]];
+        float msk_n = ok ? 1.0f : 0.0f;
+        {
+            const float *p = xs;
+            if (MODE == MODE_DENSE) {
+                p = xs + kn * CK;
+            } else {
+                const int dv = kn / KS, du = kn - dv * KS;
+                const int xi = MODE == MODE_FWD ? i + du - PAD : i - du + PAD;
+                const int xj = MODE == MODE_FWD ? j + dv - PAD : j - dv + PAD;
+                const bool v = ok && xi >= 0 && xi < a.HIN && xj >= 0 && xj < a.HIN;
+                p = v ? xs + (xi + xj * a.HIN) * CK : xs;
+                msk_n = v ? 1.0f : 0.0f;
+            }
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) a_nxt[kb] = *reinterpret_cast<const f32x4 *>(p + kb * 8);
         }
+        // keep the prefetch issued here, ahead of the MFMAs that hide its latency
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- MFMA on kk
         const float *bb = &Bs[buf][r * LDB + 4 * h];
 #pragma unroll
         for (int kb = 0; kb < KB; ++kb) {
-            float4 b4[NT];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) b4[nt] = *reinterpret_cast<const float4 *>(bb + nt * 32 * LDB + kb * 8);
-            const float av4[4] = {a_cur[kb].x, a_cur[kb].y, a_cur[kb].z, a_cur[kb].w};
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-                const float bq[4] = {b4[nt].x, b4[nt].y, b4[nt].z, b4[nt].w};
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj)
-                    acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av4[jj], bq[jj], acc[nt], 0, 0, 0);
+                const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bb + nt * 32 * LDB + kb * 8);
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[kb][0], b4[0], acc[nt], 0, 0, 0);
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[kb][1], b4[1], acc[nt], 0, 0, 0);
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[kb][2], b4[2], acc[nt], 0, 0, 0);
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[kb][3], b4[3], acc[nt], 0, 0, 0);
             }
         }
-        if (more) stage_store(buf ^ 1);
-        __syncthreads();
-        if (more) {
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- weights of kk+1 -> the other LDS buffer (last read one barrier ago)
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) a_cur[kb] = a_nxt[kb];
-        }
+        for (int q = 0; q < NV; ++q) *reinterpret_cast<f32x4 *>(&Bs[buf ^ 1][s_dst[q]]) = bst[q];
+        __syncthreads();
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+            a_cur[kb] = a_nxt[kb] * msk_n;
     }
 
     // epilogue: acc register g of lane l is C[(g&3) + 8*(g>>2) + 4*(l>>5)][l&31]
