@@ -221,6 +221,47 @@ int snk_comm_broadcast(snk_comm c, float *buf_dev, int64_t n, int32_t root);
  * communicator; broadcasts rank 0's q_net first */
 int snk_trainer_set_comm(snk_trainer t, snk_comm c);
 
+/* ---------------------------------------------------------------- Laplace D
+ * compute_D.jl:33-142: the deviation matrix D (P x K, Float64, Julia
+ * column-major: column pos = one Float64.(destructure(q_net)) snapshot,
+ * contiguous), its Welford mean/var (compute_D.jl:9-31, duplicated at
+ * la_utils.jl:14-36) and the Gram G = D'D (K x K) whose eigenvalues / (K-1)
+ * are the spectrum plot_traj.jl:10-16 takes from svd(D). */
+typedef struct snk_laplace_s *snk_laplace;
+#define SNK_LAP_D 0      /* double [K][P] (= Julia P x K column-major) */
+#define SNK_LAP_MEAN 1   /* double [P] */
+#define SNK_LAP_VAR 2    /* double [P]  m2 / max(K-1, 1) */
+#define SNK_LAP_GRAM 3   /* double [K][K] */
+#define SNK_LAP_D32 4    /* float [K][ld32] fp32 copy of the centred D (MFMA operand) */
+int snk_laplace_create(snk_laplace *out, int64_t n_params, int32_t K);
+int snk_laplace_destroy(snk_laplace h);
+/* compute_D.jl:67-71  deviation_matrix[:, pos] = Float64.(theta) (pos 0-based) */
+int snk_laplace_snapshot(snk_laplace h, snk_dqn m, int32_t pos);
+/* load / read one column (host doubles, P of them) */
+int snk_laplace_set_column(snk_laplace h, int32_t pos, const double *col_host);
+int snk_laplace_get(snk_laplace h, int32_t which, void *host, int64_t bytes);
+int snk_laplace_buffer_ptr(snk_laplace h, int32_t which, void **dev_out, int64_t *ld_out);
+/* compute_D.jl:74-81: fit! every column in order (Welford, Float64), then
+ * deviation_matrix .-= mean; also refreshes the fp32 copy */
+int snk_laplace_fit_center(snk_laplace h);
+/* G = D'D (K x K): fp32 MFMA over the centred D, fp64 accumulation across
+ * 1024-long k blocks and across the K-splits; ms_out (optional) = kernel ms */
+int snk_laplace_gram(snk_laplace h, float *ms_out);
+
+/* Per-sample Jacobians of the Q-net over replay slots (north_star "D = J'J";
+ * the reference has no Jacobian): row s is
+ * dQ(state of slot s)[a_s] / dtheta with a_s the stored action index, i.e.
+ * the direction of the per-sample gradient of the Huber TD loss
+ * (utils.jl:453-464). J_dev: float [n][n_params] in Flux.destructure order.
+ * slots_dev: int64 [n] replay slots, NULL = slots 0..n-1. */
+int snk_jacobian(snk_dqn m, snk_replay rb, const int64_t *slots_dev, int64_t n, float *J_dev);
+/* G = J J' (n x n, float, full symmetric) over replay slots 0..n-1 without
+ * materialising the Dense sections of J (rank-1 per sample:
+ * G = Gc + (A3 A3' + 1) o (Z Z') + [a_i = a_j] o (H H' + 1), Gc the conv
+ * sections' Gram on MFMA). ms_out (optional, 4 floats): forward + data
+ * gradients, per-sample conv Jacobians, conv Gram, dense terms + mirror. */
+int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_dev, float *ms_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -113,12 +113,27 @@ _PROTOS = {
     "snk_comm_destroy": [vp],
     "snk_comm_allreduce_mean": [vp, vp, i64],
     "snk_comm_broadcast": [vp, vp, i64, i32],
+    "snk_laplace_create": [P(vp), i64, i32],
+    "snk_laplace_destroy": [vp],
+    "snk_laplace_snapshot": [vp, vp, i32],
+    "snk_laplace_set_column": [vp, i32, vp],
+    "snk_laplace_get": [vp, i32, vp, i64],
+    "snk_laplace_buffer_ptr": [vp, i32, P(vp), P(i64)],
+    "snk_laplace_fit_center": [vp],
+    "snk_laplace_gram": [vp, P(f32)],
+    "snk_jacobian": [vp, vp, vp, i64, vp],
+    "snk_jacobian_gram": [vp, vp, i64, vp, P(f32)],
 }
 
 SNK_NET_Q = 0
 SNK_NET_TARGET = 1
 SNK_NET_OPT_STATE = 2
 SNK_NET_GRAD = 3
+SNK_LAP_D = 0
+SNK_LAP_MEAN = 1
+SNK_LAP_VAR = 2
+SNK_LAP_GRAM = 3
+SNK_LAP_D32 = 4
 
 
 class TrainerCfg(C.Structure):

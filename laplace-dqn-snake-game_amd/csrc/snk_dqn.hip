@@ -176,7 +176,9 @@ extern "C" int snk_dqn_destroy(snk_dqn h) {
         qwork_free(h->act);
         qwork_free(h->tgt);
         qwork_free(h->trn);
-        for (void *p : {(void *)h->theta_q, (void *)h->theta_t, (void *)h->acc, (void *)h->grad, (void *)h->tmp,
+        qwork_free(h->jw);
+        for (void *p : {(void *)h->jbuf, (void *)h->jidx, (void *)h->jact, (void *)h->theta_q, (void *)h->theta_t,
+                        (void *)h->acc, (void *)h->grad, (void *)h->tmp,
                         (void *)h->perm, (void *)h->slab, (void *)h->loss_dev, (void *)h->meta, (void *)h->wt_q,
                         (void *)h->wt_t})
             dfree(p);

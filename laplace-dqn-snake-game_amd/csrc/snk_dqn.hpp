@@ -14,6 +14,12 @@ struct snk_dqn_s {
     double *loss_dev = nullptr;
     uint8_t *meta = nullptr;
     int64_t meta_cap = 0;
+    // per-sample Jacobian / Gram workspace (snk_laplace.hip)
+    snk::QWork jw;
+    float *jbuf = nullptr;
+    int64_t jbuf_floats = 0, jn_cap = 0;
+    int64_t *jidx = nullptr;
+    uint8_t *jact = nullptr;
 };
 
 namespace snk {

@@ -642,22 +642,15 @@ static void wgrad(const AL &al, const BL &bl, int64_t M, int N, int64_t K, const
     }
 }
 
-void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64_t S, QWork &w, float *grad,
-                   float *slab, int64_t slab_cap, hipStream_t s) {
-    const BwdPlan p = bwd_plan(L, S);
-    SNK_CHECK(slab_cap >= qnet_backward_slab_floats(L, S), SNK_ERR_INTERNAL, "backward slab too small");
-    const int bs = L.bs, nc = L.ncell, no = L.Wo * L.Wo;
+// data-gradient chain shared by the loss backward and the per-sample Jacobian:
+// dz1 (from dq) -> dz3 -> dz2 -> dzc1, each relu-masked by its activation
+static void backward_data_chain(const QLayout &L, const float *th, int64_t S, QWork &w, const BwdPlan &p,
+                                hipStream_t s) {
+    const int bs = L.bs, nc = L.ncell;
     head_bwd_kernel<<<ceil_div(S, 4), 256, 0, s>>>(w.dq, w.h1, th, L, S, w.dz1);
     launch_check("head_bwd_kernel");
-    d2_grad_kernel<<<1, 256, 0, s>>>(w.dq, w.h1, S, L, grad);
-    launch_check("d2_grad_kernel");
-    // Dense1: dW (+ bias row) and dX (relu mask on a3)
-    wgrad<2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, L.K1 + 1, 64, S, p.d1, grad + L.off_d1w, slab, s);
     gemm<2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + L.off_d1w, 64, L.K1, 64}, EpReluMask{w.dz3, w.a3, (int)S, L.K1},
             S, L.K1, 64, p.d1x, s);
-    // conv3: dW over rows (s, pout); dX onto the bs x bs x 32 input (relu mask on a2)
-    wgrad<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64}, 1153,
-             64, S * no, p.c3, grad + L.off_w3, slab, s);
     {
         ConvArgs a{};
         a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs; a.nkk = 36;
@@ -675,14 +668,115 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             launch_check("conv_reduce_kernel");
         }
     }
-    // conv2
-    wgrad<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32}, 145, 32,
-             S * nc, p.c2, grad + L.off_w2, slab, s);
     gemm<1>(AConvDx<32, 3, 1>{w.dz2, bs, bs, FastDiv(nc), FastDiv(bs)}, BConvT<16, 32>{th + L.off_w2, 288},
             EpReluMask{w.dzc1, w.a1, (int)(S * nc), 16}, S * nc, 16, 288, p.c2x, s);
-    // conv1 (weights only)
+}
+
+void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64_t S, QWork &w, float *grad,
+                   float *slab, int64_t slab_cap, hipStream_t s) {
+    const BwdPlan p = bwd_plan(L, S);
+    SNK_CHECK(slab_cap >= qnet_backward_slab_floats(L, S), SNK_ERR_INTERNAL, "backward slab too small");
+    const int bs = L.bs, nc = L.ncell, no = L.Wo * L.Wo;
+    backward_data_chain(L, th, S, w, p, s);
+    d2_grad_kernel<<<1, 256, 0, s>>>(w.dq, w.h1, S, L, grad);
+    launch_check("d2_grad_kernel");
+    wgrad<2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, L.K1 + 1, 64, S, p.d1, grad + L.off_d1w, slab, s);
+    wgrad<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64}, 1153,
+             64, S * no, p.c3, grad + L.off_w3, slab, s);
+    wgrad<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32}, 145, 32,
+             S * nc, p.c2, grad + L.off_w2, slab, s);
     wgrad<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16}, 9 * L.C + 1, 16,
              S * nc, p.c1, grad + L.off_w1, slab, s);
+}
+
+// ---------------------------------------------------------------- per-sample Jacobian
+// dq = one-hot of the stored action (the direction of dQ(s)[a]/dtheta); act_out[s] = that action
+__global__ void jac_onehot_kernel(const uint8_t *__restrict__ act, const int64_t *__restrict__ idx, int64_t S,
+                                  float *__restrict__ dq, uint8_t *__restrict__ act_out) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const int a = act[idx ? idx[s] : s] % 3;   // as the loss head (utils.jl:453-455)
+    dq[s * 3 + 0] = a == 0 ? 1.0f : 0.0f;
+    dq[s * 3 + 1] = a == 1 ? 1.0f : 0.0f;
+    dq[s * 3 + 2] = a == 2 ? 1.0f : 0.0f;
+    if (act_out) act_out[s] = (uint8_t)a;
+}
+
+// Dense1 / Dense2 sections of a Jacobian row: rank-1 outer products
+__global__ void jac_dense_kernel(const float *__restrict__ a3, const float *__restrict__ dz1,
+                                 const float *__restrict__ h1, const uint8_t *__restrict__ act, int64_t S, QLayout L,
+                                 float *__restrict__ J, int64_t ldJ) {
+    const int64_t nd = L.P - L.off_d1w;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < S * nd; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = t / nd, e = t - s * nd;
+        const int64_t pk = L.off_d1w + e;
+        float v;
+        if (pk < L.off_d1b) {
+            const int64_t f = e >> 6;
+            v = a3[s * L.K1 + f] * dz1[s * 64 + (e & 63)];
+        } else if (pk < L.off_d2w) {
+            v = dz1[s * 64 + (pk - L.off_d1b)];
+        } else if (pk < L.off_d2b) {
+            const int k = (int)(pk - L.off_d2w);
+            v = (k >> 6) == act[s] ? h1[s * 64 + (k & 63)] : 0.0f;
+        } else {
+            v = (int)(pk - L.off_d2b) == act[s] ? 1.0f : 0.0f;
+        }
+        J[s * ldJ + pk] = v;
+    }
+}
+
+struct EpJac {  // per-sample weight gradient z -> J[z][off + row*N + col]
+    float *J;
+    int64_t ld;
+    int M, N;
+    __device__ void store1(float v, int row, int col, int z) const {
+        if (row < M && col < N) J[(int64_t)z * ld + (int64_t)row * N + col] = v;
+    }
+    __device__ void store(const f32x16 &acc, int m0, int c0, int lane, int z) const {
+        const int col = c0 + (lane & 31);
+        if (col >= N) return;
+        float *o = J + (int64_t)z * ld;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int row = m0 + acc_row(g, lane);
+            if (row < M) o[(int64_t)row * N + col] = acc[g];
+        }
+    }
+};
+
+void qnet_jacobian(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, const uint8_t *act,
+                   const int64_t *idx, int64_t S, QWork &w, uint8_t *act_out, float *J, int64_t ldJ, bool dense,
+                   hipStream_t s, hipEvent_t ev_chain) {
+    const int bs = L.bs, nc = L.ncell, no = L.Wo * L.Wo;
+    qnet_forward(L, th, wt, src, S, w, HEAD_Q, HeadArgs{}, s);
+    jac_onehot_kernel<<<(unsigned)ceil_div(S, 256), 256, 0, s>>>(act, idx, S, w.dq, act_out);
+    launch_check("jac_onehot_kernel");
+    backward_data_chain(L, th, S, w, bwd_plan(L, S), s);
+    if (ev_chain) SNK_HIP(hipEventRecord(ev_chain, s));
+    // per-sample conv weight/bias gradients: one GEMM "split" per sample
+    // (grid.z = sample, k = that sample's output positions)
+    const int64_t CH = 32768;
+    for (int64_t s0 = 0; s0 < S; s0 += CH) {
+        const int64_t cs = std::min(CH, S - s0);
+        float *Jr = J + s0 * ldJ;
+        gemm<2>(AConvDw<32, 6, 0>{w.a2 + s0 * nc * 32, bs, L.Wo, cs * no, FastDiv(no), FastDiv(L.Wo)},
+                BRows{w.dz3 + s0 * no * 64, cs * no, 64}, EpJac{Jr + L.off_w3, ldJ, 1153, 64}, 1153, 64, cs * no,
+                GemmPlan{1, (int)cs, no}, s);
+        gemm<1>(AConvDw<16, 3, 1>{w.a1 + s0 * nc * 16, bs, bs, cs * nc, FastDiv(nc), FastDiv(bs)},
+                BRows{w.dz2 + s0 * nc * 32, cs * nc, 32}, EpJac{Jr + L.off_w2, ldJ, 145, 32}, 145, 32, cs * nc,
+                GemmPlan{1, (int)cs, nc}, s);
+        BoardSrc sh = src;
+        if (sh.idx) sh.idx += s0;
+        if (sh.fbase) sh.fbase += s0 * L.C * nc;
+        gemm<1>(ABoardDw{sh, bs, L.C, cs * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1 + s0 * nc * 16, cs * nc, 16},
+                EpJac{Jr + L.off_w1, ldJ, 9 * L.C + 1, 16}, 9 * L.C + 1, 16, cs * nc, GemmPlan{1, (int)cs, nc}, s);
+    }
+    if (dense) {
+        SNK_CHECK(act_out != nullptr, SNK_ERR_INTERNAL, "dense Jacobian needs the action array");
+        jac_dense_kernel<<<4096, 256, 0, s>>>(w.a3, w.dz1, w.h1, act_out, S, L, J, ldJ);
+        launch_check("jac_dense_kernel");
+    }
 }
 
 void rmsprop_launch(int64_t P, float *theta, float *acc, const float *grad, float eta, float rho, float eps,

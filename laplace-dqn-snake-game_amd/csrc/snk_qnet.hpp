@@ -106,6 +106,13 @@ void qnet_forward(const QLayout &L, const float *theta, const float *wt, const B
 void qnet_backward(const QLayout &L, const float *theta, const BoardSrc &src, int64_t S, QWork &w,
                    float *grad, float *slab, int64_t slab_cap, hipStream_t s);
 int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S);
+// per-sample Jacobian rows J[s] = dQ(x_s)[a_s]/dtheta (packed order, row
+// stride ldJ), a_s = act[idx[s]] % 3 (written to act_out). The conv sections
+// [0, off_d1w) always; the Dense sections only with dense = true. ev_chain
+// (optional) is recorded after the forward + data-gradient chain.
+void qnet_jacobian(const QLayout &L, const float *theta, const float *wt, const BoardSrc &src, const uint8_t *act,
+                   const int64_t *idx, int64_t S, QWork &w, uint8_t *act_out, float *J, int64_t ldJ, bool dense,
+                   hipStream_t s, hipEvent_t ev_chain = nullptr);
 void rmsprop_launch(int64_t P, float *theta, float *acc, const float *grad, float eta, float rho, float eps,
                     hipStream_t s);
 void loss_mean_launch(const double *loss, int64_t B, double *out, hipStream_t s);

@@ -1,0 +1,151 @@
+"""Laplace D build (compute_D.jl, la_utils.jl:14-36, plot_traj.jl:10-16) and
+the per-sample-Jacobian Gram of the north star, on the GPU.
+
+`LaplaceD` owns the reference's `deviation_matrix` (P x K Float64; stored
+column by column, i.e. Julia's own memory order) together with the Welford
+`MeanStd` state. `compute_D(tr)` drives a `Trainer` through the reference's
+schedule: burn-in, one snapshot every `thin` updates, Welford + centring
+once K columns are in.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import DeviceArray, call, vp
+from .qnet import DQNModel
+from .replay import ReplayBuffer
+
+
+class LaplaceD:
+    """`deviation_matrix = zeros(Float64, (param_count, K))` + `MeanStd(param_count)`
+    (compute_D.jl:50-55)."""
+
+    def __init__(self, n_params: int, K: int = 1000):
+        self.P, self.K = int(n_params), int(K)
+        h = vp()
+        call("snk_laplace_create", C.byref(h), self.P, self.K)
+        self._h = h
+        self.fitted = False
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib._lib is not None:
+            _lib._lib.snk_laplace_destroy(self._h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def snapshot(self, model: DQNModel, pos: int) -> None:
+        """compute_D.jl:69-70 `deviation_matrix[:, position] = Float64.(theta)` (pos 0-based)."""
+        call("snk_laplace_snapshot", self._h, model.handle, int(pos))
+
+    def set_column(self, pos: int, col) -> None:
+        col = np.ascontiguousarray(col, np.float64)
+        assert col.size == self.P, (col.size, self.P)
+        call("snk_laplace_set_column", self._h, int(pos), _lib.ptr(col))
+
+    def fit_center(self) -> None:
+        """compute_D.jl:74-81: `for c in eachcol(D) fit!(o, c) end; D .-= mean(o)`."""
+        call("snk_laplace_fit_center", self._h)
+        self.fitted = True
+
+    def _get(self, which: int, shape, dtype) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        call("snk_laplace_get", self._h, which, _lib.ptr(out), out.nbytes)
+        return out
+
+    def D(self) -> np.ndarray:
+        """[K, P]: row k is column k of the reference's P x K matrix."""
+        return self._get(_lib.SNK_LAP_D, (self.K, self.P), np.float64)
+
+    def mean(self) -> np.ndarray:
+        """compute_D.jl:29 `mean(o::MeanStd)`."""
+        return self._get(_lib.SNK_LAP_MEAN, self.P, np.float64)
+
+    def var(self) -> np.ndarray:
+        """compute_D.jl:30 `var(o) = m2 ./ max(n - 1, 1)`."""
+        return self._get(_lib.SNK_LAP_VAR, self.P, np.float64)
+
+    def std(self) -> np.ndarray:
+        """compute_D.jl:31 (sqrt of the device var)."""
+        return np.sqrt(self.var())
+
+    def gram(self) -> tuple[np.ndarray, float]:
+        """G = D'D (K x K, fp64 result of fp32 MFMA with fp64 accumulation) and the Gram kernel's ms."""
+        ms = C.c_float(0.0)
+        call("snk_laplace_gram", self._h, C.byref(ms))
+        return self._get(_lib.SNK_LAP_GRAM, (self.K, self.K), np.float64), ms.value
+
+    def spectrum(self, G: np.ndarray | None = None, floor: float = 1e-7) -> np.ndarray:
+        """plot_traj.jl:10-19: lambda = S.^2/(K-1) of svd(D), the eigenvalues of
+        D'D/(K-1), keeping those > 1e-7 (host analysis of the device Gram,
+        as plot_traj.jl is analysis of the saved D)."""
+        if G is None:
+            G, _ = self.gram()
+        lam = np.linalg.eigvalsh(G) / (self.K - 1)
+        return np.sort(lam[lam > floor])[::-1]
+
+
+def compute_D(tr, K: int = 1000, thin: int = 10, burn_in: int = 50_000, graph: bool = True,
+              reset_optimizer: bool = True) -> LaplaceD:
+    """compute_D.jl:33-86 on a Trainer: fill_buffer!, a fresh RMSProp state
+    (`Flux.setup`, :47), then the training loop; at update nb (1-based) with
+    nb >= burn_in and nb % thin == 0 the current q_net goes into the next
+    column, *before* that update runs; after the K-th column: Welford +
+    centring, return (the BSON save of :84 is the caller's business)."""
+    from .trainer import fill_buffer_
+
+    if tr.updates_per_iter != 1:
+        raise ValueError("compute_D snapshots between single updates: use updates_per_iter = 1")
+    model = tr.model
+    lap = LaplaceD(model.P, K)
+    fill_buffer_(tr, graph=graph)
+    if reset_optimizer:
+        model.set_params(np.zeros(model.P, np.float32), _lib.SNK_NET_OPT_STATE)
+    first = burn_in if burn_in % thin == 0 else burn_in + (thin - burn_in % thin)
+    tr.run(first - 1, learn=True, graph=graph)          # updates nb = 1 .. first-1
+    for pos in range(K):
+        lap.snapshot(model, pos)                          # before update nb = first + pos*thin
+        if pos + 1 < K:
+            tr.run(thin, learn=True, graph=graph)
+    lap.fit_center()
+    return lap
+
+
+def jacobian(model: DQNModel, buf: ReplayBuffer, n: int | None = None, slots=None) -> np.ndarray:
+    """Per-sample Jacobians J[s] = dQ(state_s)[a_s]/dtheta (Flux.destructure
+    order) for replay slots `slots` (default 0..n-1): [n, P] float32."""
+    if slots is not None:
+        slots = np.ascontiguousarray(slots, np.int64)
+        n = slots.size
+        dslots = DeviceArray.from_host(slots)
+    else:
+        dslots = None
+    n = int(n if n is not None else len(buf))
+    J = DeviceArray((n, model.P), np.float32)
+    call("snk_jacobian", model.handle, buf.handle, dslots.ptr if dslots is not None else None, n, J.ptr)
+    return J.numpy()
+
+
+def jacobian_gram(model: DQNModel, buf: ReplayBuffer, n: int | None = None, *, out: DeviceArray | None = None,
+                  host: bool = True):
+    """G = J J' over replay slots 0..n-1 (default: the whole buffer).
+    Returns (G, ms) with G a host [n, n] float32 array (or the DeviceArray
+    when host=False) and ms the 4 phase times (forward + data gradients,
+    per-sample conv Jacobians, conv Gram, dense terms + mirror)."""
+    n = int(n if n is not None else len(buf))
+    G = out if out is not None else DeviceArray((n, n), np.float32)
+    ms = (C.c_float * 4)()
+    call("snk_jacobian_gram", model.handle, buf.handle, n, G.ptr, ms)
+    t = [float(v) for v in ms]
+    return (G.numpy() if host else G), t
+
+
+def d_build_seconds(ms) -> float:
+    """Wall time of one Jacobian-Gram D build from its phase times."""
+    return sum(ms) / 1e3 if ms else math.nan
