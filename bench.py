@@ -44,7 +44,10 @@ def parse():
     p.add_argument("--capacity", type=int, default=50000)
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-extras", action="store_true", help="skip per-kernel timing / D build")
+    p.add_argument("--no-extras", action="store_true", help="skip per-kernel timing")
+    p.add_argument("--no-dbuild", action="store_true", help="skip the Laplace D builds")
+    p.add_argument("--d-samples", type=int, default=0, help="Jacobian Gram rows (0 = the whole replay buffer)")
+    p.add_argument("--d-snapshots", type=int, default=1000, help="K of the snapshot D (compute_D.jl:51)")
     return p.parse_args()
 
 
@@ -83,6 +86,62 @@ def cpu_baseline(args) -> dict:
             "sample": (f"oracle C restatement, 1 thread: Q forward on {nf} of {n} states (scaled x{n // nf}), "
                        f"3 lockstep steps of {n} envs, one B=64 loss+grad+RMSProp; per-iteration "
                        f"fwd {t_fwd:.2f}s + step {t_step:.3f}s + update {t_upd:.2f}s")}
+
+
+def d_build(args, snk, tr) -> dict:
+    """The two Laplace D builds, after the timed region, on rank 0.
+
+    d_build_sec: G = J J' over the replay buffer's 50k per-sample Jacobians
+    (north_star / configs[4]); phases timed with HIP events on the library
+    stream. snapshot_gram: compute_D.jl's own D (K q_net snapshots, one per
+    trainer iteration here), Welford + centring + D'D."""
+    import time
+
+    import numpy as np
+    from snake_amd import _lib
+
+    n = args.d_samples or len(tr.buffer)
+    Kc = 9 * args.n_frames * 16 + 16 + 4640 + 73792            # conv columns of a Jacobian row
+    G = snk.DeviceArray((n, n), np.float32)
+    snk.jacobian_gram(tr.model, tr.buffer, n, out=G, host=False)   # workspace allocation + first launch
+    _lib.call("snk_synchronize")
+    t0 = time.perf_counter()
+    _, ms = snk.jacobian_gram(tr.model, tr.buffer, n, out=G, host=False)
+    wall = time.perf_counter() - t0
+    flop_gram = float(n) * (n + 1) * Kc                          # lower triangle incl. diagonal, 2 flop / MAC
+    tf = flop_gram / (ms[2] * 1e-3) / 1e12
+    P = tr.model.P
+    res = {"d_build_sec": wall,
+           "d_build": {"kind": "per-sample Jacobian Gram G = J J' (n x n, fp32 MFMA, fp64 accumulation)",
+                       "n_samples": n, "n_params": P, "conv_columns": Kc,
+                       "phase_ms": {"forward_and_data_grads": ms[0], "per_sample_conv_jacobians": ms[1],
+                                    "conv_gram": ms[2], "dense_terms_and_mirror": ms[3]},
+                       "naive_flop": 2.0 * n * n * P, "executed_gram_flop": flop_gram,
+                       "roofline": {"bound": "mfma", "kernel": "syrk_kernel (conv-column Gram)", "achieved": tf,
+                                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_TFLOPS,
+                                    "avg_launch_ms": ms[2], "flop_per_launch": flop_gram, "traffic": None}}}
+    del G
+    K = args.d_snapshots
+    if K > 1:
+        lap = snk.LaplaceD(P, K)
+        for pos in range(K):
+            lap.snapshot(tr.model, pos)
+            tr.run(1, learn=True, graph=not args.no_graph)
+        _lib.call("snk_synchronize")
+        t0 = time.perf_counter()
+        lap.fit_center()
+        _lib.call("snk_synchronize")
+        t_fit = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        _, gms = lap.gram()
+        t_gram = time.perf_counter() - t0
+        fl = float(K) * (K + 1) * ((P + 3) // 4 * 4)
+        res["snapshot_gram"] = {"kind": "compute_D.jl D (P x K Float64 snapshots) -> Welford, centre, G = D'D",
+                                "K": K, "n_params": P, "welford_center_ms": 1e3 * t_fit,
+                                "welford_center_GBs": 28.0 * K * P / t_fit / 1e9,
+                                "gram_kernel_ms": gms, "gram_total_ms": 1e3 * t_gram,
+                                "gram_tflops": fl / (gms * 1e-3) / 1e12}
+    return res
 
 
 def main():
@@ -181,7 +240,8 @@ def main():
         out["step_kernel"] = {"avg_launch_ms": sms.value, "bytes_per_env_step": step_bytes,
                               "achieved_GBs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS,
                               "env_steps_per_s": n / (sms.value * 1e-3)}
-        out["d_build_sec"] = None
+    if rank == 0 and not args.no_dbuild:
+        out.update(d_build(args, snk, tr))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
