@@ -86,7 +86,7 @@ BoardSrc src_float(const QLayout &L, const float *x) {
 // One DQN loss + gradient on B transitions of a replay (or explicit batch):
 // target forward on s', online forward on s with the Huber head, backward.
 void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, const HeadArgs &meta, int64_t B,
-                   double gamma, hipStream_t s) {
+                   double gamma, hipStream_t s, const LossOpts &o) {
     qwork_ensure(h->tgt, h->L, B, false);
     qwork_ensure(h->trn, h->L, B, true);
     const int64_t need = qnet_backward_slab_floats(h->L, B);
@@ -96,17 +96,47 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
         h->slab = dalloc<float>(need);
         h->slab_cap = need;
     }
+    Fork serial;
+    serial.main = s;
+    Fork &F = o.fork ? *o.fork : serial;
     HeadArgs ta = meta;
     ta.gamma = gamma;
     ta.target = h->trn.target;
     ta.B = B;
-    qnet_forward(h->L, h->theta_t, h->wt_t, sn_src, B, h->tgt, HEAD_TARGET, ta, s);
+    // t_net(s') (optionally on a side stream beside q_net(s)); the loss head needs both
+    hipStream_t q0 = F.fork(0, FK_TARGET);
+    qnet_forward(h->L, h->theta_t, h->wt_t, sn_src, B, h->tgt, HEAD_TARGET, ta, q0);
     HeadArgs la = ta;
     la.loss = h->trn.loss;
     la.dq = h->trn.dq;
-    qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s);
-    qnet_backward(h->L, h->theta_q, s_src, B, h->trn, h->grad, h->slab, h->slab_cap, s);
-    loss_mean_launch(h->trn.loss, B, h->loss_dev, s);
+    la.dz1 = h->trn.dz1;
+    for (int layer = 0; layer < 4; ++layer)
+        qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, layer);
+    F.join(0, FK_TARGET);
+    qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, 4);
+    hipStream_t q1 = o.loss_mean ? F.fork(1, FK_LOSS) : s;
+    if (o.loss_mean) loss_mean_launch(h->trn.loss, B, h->loss_dev, q1);
+    BwdOpts bo;
+    bo.fork = o.fork;
+    bo.defer = o.defer;
+    bo.dz1_ready = true;
+    qnet_backward(h->L, h->theta_q, s_src, B, h->trn, h->grad, h->slab, h->slab_cap, s, bo);
+    if (o.loss_mean) F.join(1, FK_LOSS);
+}
+
+UpdateTarget dqn_update_target(snk_dqn_s *h, const int64_t *counter, int64_t rate) {
+    UpdateTarget u;
+    u.theta = h->theta_q;
+    u.acc = h->acc;
+    u.wt = h->wt_q;
+    u.theta_t = h->theta_t;
+    u.wt_t = h->wt_t;
+    u.counter = counter;
+    u.rate = rate;
+    u.lr = h->lr;
+    u.rho = h->rho;
+    u.eps = h->eps;
+    return u;
 }
 
 }  // namespace snk
@@ -375,8 +405,8 @@ extern "C" int snk_dqn_loss_grad_batch(snk_dqn h, const float *states, const int
 extern "C" int snk_dqn_apply_grad(snk_dqn h) {
     return guard([&] {
         SNK_CHECK(h, SNK_ERR_INVALID, "NULL argument");
-        rmsprop_launch(h->L.P, h->theta_q, h->acc, h->grad, h->lr, h->rho, h->eps, stream());
-        dqn_q_changed(h, stream());
+        const UpdateTarget u = dqn_update_target(h, nullptr, 1);   // RMSProp + forward image, one pass
+        grad_update_launch(h->L, nullptr, h->grad, &u, stream());
     });
 }
 

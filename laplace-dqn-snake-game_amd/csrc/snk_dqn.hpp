@@ -27,12 +27,20 @@ const EnvDev &env_dev(snk_env h);
 const ReplayDev &replay_dev(snk_replay h);
 int32_t replay_batch(snk_replay h);
 void replay_launch_sample(const ReplayDev &d, int32_t batch, uint64_t seed, uint64_t draw,
-                          const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s);
+                          const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s,
+                          int64_t pending = 0);
 BoardSrc src_env(const EnvDev &E);
 BoardSrc src_replay(const ReplayDev &R, const int64_t *idx, int chan0);
 BoardSrc src_float(const QLayout &L, const float *x);
+struct LossOpts {
+    Fork *fork = nullptr;            // target forward / weight gradients / loss mean on side streams
+    GradSlabs *defer = nullptr;      // leave K-split slabs and Dense2 to grad_update_launch
+    bool loss_mean = true;           // reduce the per-sample losses into h->loss_dev here
+};
 void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, const HeadArgs &meta, int64_t B,
-                   double gamma, hipStream_t s);
+                   double gamma, hipStream_t s, const LossOpts &o = LossOpts{});
+// RMSProp + forward image (+ target copy when *counter % rate == 0) of an already finished gradient
+UpdateTarget dqn_update_target(snk_dqn_s *h, const int64_t *counter, int64_t rate);
 void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, hipStream_t s);
 void dqn_permute(snk_dqn_s *h, const float *src, float *dst, bool to_packed, hipStream_t s);
 // q_net parameters changed: rebuild its forward weight image

@@ -388,6 +388,15 @@ __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ sla
     float q[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) q[a] = theta[L.off_d2b + a] + wave_sum(theta[L.off_d2w + a * 64 + lane] * h);
+    if (MODE == HEAD_LOSS && ha.dz1) {
+        // head_bwd fused: dz1 = (h1 > 0) * sum_a dq[a] W2[a][o] with dq one-hot at the taken action
+        const int64_t m = ha.idx ? ha.idx[s] : s;
+        const int a = ha.act_idx[m] % 3;
+        const double e = (double)q[a] - ha.target[s];
+        const double ae = fabs(e);
+        const float g = (float)((ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / (double)ha.B);
+        ha.dz1[s * 64 + lane] = h > 0.0f ? g * theta[L.off_d2w + a * 64 + lane] : 0.0f;
+    }
     if (lane != 0) return;
     qo[s * 3 + 0] = q[0];
     qo[s * 3 + 1] = q[1];
@@ -615,31 +624,25 @@ static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
     return p;
 }
 static int64_t zslab(const GemmPlan &g, int64_t MN) { return g.z > 1 ? (int64_t)g.z * MN : 0; }
-int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S) {
+// the four weight-gradient GEMMs may run concurrently: each owns a slab region
+struct SlabRegions {
+    int64_t d1, c3, c2, c1, total;
+};
+static SlabRegions slab_regions(const QLayout &L, int64_t S) {
     const BwdPlan p = bwd_plan(L, S);
-    int64_t m = zslab(p.d1, (int64_t)(L.K1 + 1) * 64);
-    m = std::max(m, zslab(p.c3, 1153 * 64));
-    m = std::max(m, zslab(p.c2, 145 * 32));
-    m = std::max(m, zslab(p.c1, (int64_t)(9 * L.C + 1) * 16));
-    return std::max<int64_t>(m, 1);
+    SlabRegions r;
+    r.d1 = 0;
+    r.c3 = r.d1 + zslab(p.d1, (int64_t)(L.K1 + 1) * 64);
+    r.c2 = r.c3 + zslab(p.c3, 1153 * 64);
+    r.c1 = r.c2 + zslab(p.c2, 145 * 32);
+    r.total = std::max<int64_t>(r.c1 + zslab(p.c1, (int64_t)(9 * L.C + 1) * 16), 1);
+    return r;
 }
+int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S) { return slab_regions(L, S).total; }
 
 static void reduce_into(const float *slab, int ks, int64_t MN, float *out, hipStream_t s) {
     slab_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(MN, 256), 2048), 256, 0, s>>>(slab, ks, MN, out);
     launch_check("slab_reduce_kernel");
-}
-
-// weight gradient straight into grad[off..] when one workgroup column covers K,
-// else through z partial slabs and a reduce
-template <int NT, class AL, class BL>
-static void wgrad(const AL &al, const BL &bl, int64_t M, int N, int64_t K, const GemmPlan &p, float *dst,
-                  float *slab, hipStream_t s) {
-    if (p.z == 1) {
-        gemm<NT>(al, bl, EpSlab{dst, (int)M, N}, M, N, K, p, s);
-    } else {
-        gemm<NT>(al, bl, EpSlab{slab, (int)M, N}, M, N, K, p, s);
-        reduce_into(slab, p.z, M * N, dst, s);
-    }
 }
 
 // data-gradient chain shared by the loss backward and the per-sample Jacobian:
@@ -673,20 +676,188 @@ static void backward_data_chain(const QLayout &L, const float *th, int64_t S, QW
 }
 
 void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64_t S, QWork &w, float *grad,
-                   float *slab, int64_t slab_cap, hipStream_t s) {
+                   float *slab, int64_t slab_cap, hipStream_t s, const BwdOpts &o) {
     const BwdPlan p = bwd_plan(L, S);
-    SNK_CHECK(slab_cap >= qnet_backward_slab_floats(L, S), SNK_ERR_INTERNAL, "backward slab too small");
+    const SlabRegions sr = slab_regions(L, S);
+    SNK_CHECK(slab_cap >= sr.total, SNK_ERR_INTERNAL, "backward slab too small");
     const int bs = L.bs, nc = L.ncell, no = L.Wo * L.Wo;
-    backward_data_chain(L, th, S, w, p, s);
-    d2_grad_kernel<<<1, 256, 0, s>>>(w.dq, w.h1, S, L, grad);
-    launch_check("d2_grad_kernel");
-    wgrad<2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, L.K1 + 1, 64, S, p.d1, grad + L.off_d1w, slab, s);
-    wgrad<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64}, 1153,
-             64, S * no, p.c3, grad + L.off_w3, slab, s);
-    wgrad<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32}, 145, 32,
-             S * nc, p.c2, grad + L.off_w2, slab, s);
-    wgrad<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16}, 9 * L.C + 1, 16,
-             S * nc, p.c1, grad + L.off_w1, slab, s);
+    Fork serial;
+    serial.main = s;
+    Fork &F = o.fork ? *o.fork : serial;
+    GradSlabs *D = o.defer;
+    if (D) {
+        *D = GradSlabs{};
+        D->dq = w.dq;
+        D->h1 = w.h1;
+        D->S = S;
+    }
+    // a weight gradient: straight into grad, through slabs + reduce, or left
+    // as slabs for grad_update_launch (section k of D)
+    auto wg = [&](int k, auto launch, const GemmPlan &g, int64_t off, int64_t n, float *sl, hipStream_t q) {
+        if (g.z == 1) {
+            launch(grad + off, q);
+        } else {
+            launch(sl, q);
+            if (D) {
+                D->slab[k] = sl; D->z[k] = g.z; D->off[k] = off; D->n[k] = n;
+            } else {
+                reduce_into(sl, g.z, n, grad + off, q);
+            }
+        }
+    };
+    // critical path: dz1 -> dz3 -> dz2 -> dzc1 -> conv1 weights; each weight
+    // gradient forks off as soon as its dz exists
+    if (!o.dz1_ready) {
+        head_bwd_kernel<<<ceil_div(S, 4), 256, 0, s>>>(w.dq, w.h1, th, L, S, w.dz1);
+        launch_check("head_bwd_kernel");
+    }
+    {
+        hipStream_t q = F.fork(0, FK_WGRAD);
+        if (!D) {
+            d2_grad_kernel<<<1, 256, 0, q>>>(w.dq, w.h1, S, L, grad);
+            launch_check("d2_grad_kernel");
+        }
+        const int64_t M = L.K1 + 1;
+        wg(0, [&](float *dst, hipStream_t qq) {
+            gemm<2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, EpSlab{dst, (int)M, 64}, M, 64, S, p.d1, qq);
+        }, p.d1, L.off_d1w, M * 64, slab + sr.d1, q);
+    }
+    gemm<2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + L.off_d1w, 64, L.K1, 64}, EpReluMask{w.dz3, w.a3, (int)S, L.K1},
+            S, L.K1, 64, p.d1x, s);
+    {
+        hipStream_t q = F.fork(1, FK_WGRAD);
+        wg(1, [&](float *dst, hipStream_t qq) {
+            gemm<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64},
+                    EpSlab{dst, 1153, 64}, 1153, 64, S * no, p.c3, qq);
+        }, p.c3, L.off_w3, 1153 * 64, slab + sr.c3, q);
+    }
+    {
+        ConvArgs a{};
+        a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs; a.nkk = 36;
+        const int sp = conv_splits(S * nc, 36);
+        if (sp == 1) {
+            a.out = w.dz2;
+            conv_launch<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK>(a, 1, s);
+        } else {
+            a.out = w.cslab;
+            SNK_CHECK((int64_t)sp * S * nc * 32 <= w.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
+            conv_launch<64, 32, 6, 0, MODE_DX, EPI_SLAB>(a, sp, s);
+            const int used = ceil_div(36, ceil_div(36, sp));
+            conv_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(S * nc * 32, 256), 4096), 256, 0, s>>>(
+                w.cslab, used, S * nc * 32, 32, nullptr, w.a2, w.dz2);
+            launch_check("conv_reduce_kernel");
+        }
+    }
+    {
+        hipStream_t q = F.fork(2, FK_WGRAD);
+        wg(2, [&](float *dst, hipStream_t qq) {
+            gemm<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32},
+                    EpSlab{dst, 145, 32}, 145, 32, S * nc, p.c2, qq);
+        }, p.c2, L.off_w2, 145 * 32, slab + sr.c2, q);
+    }
+    gemm<1>(AConvDx<32, 3, 1>{w.dz2, bs, bs, FastDiv(nc), FastDiv(bs)}, BConvT<16, 32>{th + L.off_w2, 288},
+            EpReluMask{w.dzc1, w.a1, (int)(S * nc), 16}, S * nc, 16, 288, p.c2x, s);
+    {
+        const int64_t M = 9 * L.C + 1;
+        wg(3, [&](float *dst, hipStream_t qq) {
+            gemm<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
+                    EpSlab{dst, (int)M, 16}, M, 16, S * nc, p.c1, qq);
+        }, p.c1, L.off_w1, M * 16, slab + sr.c1, s);
+    }
+    F.join(0, FK_WGRAD);
+    F.join(1, FK_WGRAD);
+    F.join(2, FK_WGRAD);
+}
+
+// ---------------------------------------------------------------- fused update
+struct UpdArgs {
+    QLayout L;
+    GradSlabs g;
+    float *grad;
+    UpdateTarget u;
+    int finish, apply;
+};
+
+// index of packed parameter i in the forward weight image, or -1
+__device__ __forceinline__ int64_t image_index(const QLayout &L, int64_t i) {
+    int64_t u, base;
+    int CK, CN;
+    if (i >= L.off_w2 && i < L.off_b2) {
+        u = i - L.off_w2; base = L.off_t2; CK = 16; CN = 32;
+    } else if (i >= L.off_w3 && i < L.off_b3) {
+        u = i - L.off_w3; base = L.off_t3; CK = 32; CN = 64;
+    } else if (i >= L.off_d1w && i < L.off_d1b) {
+        u = i - L.off_d1w; base = L.off_td; CK = 64; CN = 64;
+    } else {
+        return -1;
+    }
+    const int64_t kk = u / (CK * CN);
+    const int r = (int)(u - kk * CK * CN);
+    const int c = r / CN, n = r - c * CN;
+    return base + kk * CK * CN + (int64_t)n * CK + c;
+}
+
+__global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
+    const QLayout &L = a.L;
+    const bool due = a.apply && a.u.counter && (*a.u.counter % a.u.rate) == 0;   // utils.jl:469-472
+    const float omr = 1.0f - a.u.rho;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L.P; i += (int64_t)gridDim.x * blockDim.x) {
+        float g;
+        if (a.finish) {
+            g = a.grad[i];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int64_t j = i - a.g.off[k];
+                if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
+                    float v = 0.0f;   // slab_reduce order
+                    for (int z = 0; z < a.g.z[k]; ++z) v += a.g.slab[k][(int64_t)z * a.g.n[k] + j];
+                    g = v;
+                }
+            }
+            if (i >= L.off_d2w) {   // d2_grad order
+                const int t = (int)(i - L.off_d2w);
+                float acc = 0.0f;
+                if (t < 192) {
+                    const int ac = t >> 6, o = t & 63;
+                    for (int64_t s = 0; s < a.g.S; ++s) acc = __builtin_fmaf(a.g.dq[s * 3 + ac], a.g.h1[s * 64 + o], acc);
+                } else {
+                    const int ac = t - 192;
+                    for (int64_t s = 0; s < a.g.S; ++s) acc += a.g.dq[s * 3 + ac];
+                }
+                g = acc;
+            }
+            a.grad[i] = g;
+        } else {
+            g = a.grad[i];
+        }
+        if (!a.apply) continue;
+        // Optimisers.jl RMSProp (rmsprop_kernel order)
+        const float qd = a.u.rho * a.u.acc[i] + omr * (g * g);
+        a.u.acc[i] = qd;
+        const float th = a.u.theta[i] - (g * a.u.lr) / (__builtin_sqrtf(qd) + a.u.eps);
+        a.u.theta[i] = th;
+        const int64_t t = image_index(L, i);
+        if (t >= 0) a.u.wt[t] = th;
+        if (due) {
+            a.u.theta_t[i] = th;
+            if (t >= 0) a.u.wt_t[t] = th;
+        }
+    }
+}
+
+void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
+                        hipStream_t s) {
+    UpdArgs a{};
+    a.L = L;
+    if (pending) a.g = *pending;
+    a.grad = grad;
+    if (apply) a.u = *apply;
+    a.finish = pending != nullptr;
+    a.apply = apply != nullptr;
+    if (!a.finish && !a.apply) return;
+    if (a.apply && !a.u.counter) a.u.rate = 1;
+    grad_update_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.P, 256), 2048), 256, 0, s>>>(a);
+    launch_check("grad_update_kernel");
 }
 
 // ---------------------------------------------------------------- per-sample Jacobian

@@ -94,6 +94,7 @@ struct HeadArgs {
     double *target = nullptr;
     double *loss = nullptr;
     float *dq = nullptr;
+    float *dz1 = nullptr;   // LOSS: also write Dense2's data gradient (the backward's first step)
     int64_t B = 0;
 };
 
@@ -102,9 +103,35 @@ struct HeadArgs {
 // (inputs from a previous full forward; used for per-layer timing)
 void qnet_forward(const QLayout &L, const float *theta, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
                   HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1);
+// Weight-gradient sections a backward left as K-split partial slabs (z > 1),
+// plus Dense2's gradient (a reduction of dq x h1 over the batch): finished
+// inside the update kernel instead of by separate reduce launches.
+struct GradSlabs {
+    const float *slab[4] = {};
+    int z[4] = {};
+    int64_t off[4] = {}, n[4] = {};
+    const float *dq = nullptr, *h1 = nullptr;
+    int64_t S = 0;
+};
+struct BwdOpts {
+    Fork *fork = nullptr;        // weight gradients on side streams
+    GradSlabs *defer = nullptr;  // leave slabs + Dense2 to grad_update_launch
+    bool dz1_ready = false;      // the LOSS head already wrote w.dz1
+};
 // backward of the loss whose dq sits in w.dq (after HEAD_LOSS): grad (packed) overwritten
 void qnet_backward(const QLayout &L, const float *theta, const BoardSrc &src, int64_t S, QWork &w,
-                   float *grad, float *slab, int64_t slab_cap, hipStream_t s);
+                   float *grad, float *slab, int64_t slab_cap, hipStream_t s, const BwdOpts &o = BwdOpts{});
+// finish (slabs, Dense2 -> grad) and/or apply (RMSProp, forward weight image,
+// update_target_net! when *counter % rate == 0) in one pass over theta
+struct UpdateTarget {
+    float *theta, *acc, *wt;
+    float *theta_t, *wt_t;
+    const int64_t *counter;   // nullptr: no target copy
+    int64_t rate;
+    float lr, rho, eps;
+};
+void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
+                        hipStream_t s);
 int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S);
 // per-sample Jacobian rows J[s] = dQ(x_s)[a_s]/dtheta (packed order, row
 // stride ldJ), a_s = act[idx[s]] % 3 (written to act_out). The conv sections

@@ -50,12 +50,13 @@ __global__ void replay_gather_kernel(ReplayDev R, const int64_t *__restrict__ id
 __global__ __launch_bounds__(256) void replay_sample_kernel(const int64_t *__restrict__ count, int64_t cap,
                                                             int32_t batch, uint64_t seed, uint64_t draw,
                                                             const int64_t *__restrict__ draw_dev,
-                                                            int64_t *__restrict__ out, int32_t *__restrict__ b_out) {
+                                                            int64_t *__restrict__ out, int32_t *__restrict__ b_out,
+                                                            int64_t pending) {
     constexpr int HS = 8192;   // >= 2 * max batch (4096)
     __shared__ int64_t set[HS];
     __shared__ int64_t cand[4096];
     if (draw_dev) draw = (uint64_t)*draw_dev;
-    const int64_t len = min(*count, cap);
+    const int64_t len = min(*count + pending, cap);   // pending: transitions stored before the draw is used
     const int B = (int)min((int64_t)batch, len);
     int hs = 128;
     while (hs < 2 * B) hs <<= 1;
@@ -275,8 +276,8 @@ extern "C" int snk_replay_empty(snk_replay h) {
 
 namespace snk {
 void replay_launch_sample(const ReplayDev &d, int32_t batch, uint64_t seed, uint64_t draw,
-                          const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s) {
-    replay_sample_kernel<<<1, 256, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev);
+                          const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s, int64_t pending) {
+    replay_sample_kernel<<<1, 256, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev, pending);
     launch_check("replay_sample_kernel");
 }
 }  // namespace snk
@@ -288,7 +289,7 @@ extern "C" int snk_replay_sample(snk_replay h, uint64_t seed, uint64_t draw, int
         int64_t len = 0;
         if (snk_replay_length(h, &len) != SNK_OK) throw Error{SNK_ERR_HIP};
         SNK_CHECK(len > 0, SNK_ERR_STATE, "cannot sample an empty buffer");
-        replay_launch_sample(h->d, h->batch_size, seed, draw, nullptr, idx_dev, nullptr, stream());
+        replay_launch_sample(h->d, h->batch_size, seed, draw, nullptr, idx_dev, nullptr, stream(), 0);
         if (B_out) *B_out = (int32_t)std::min<int64_t>(h->batch_size, len);
         SNK_HIP(hipStreamSynchronize(stream()));
     });

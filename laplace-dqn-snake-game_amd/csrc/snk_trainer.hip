@@ -33,7 +33,7 @@ struct alignas(16) TrainStats {
 __global__ __launch_bounds__(1024) void episode_stats_kernel(const uint8_t *__restrict__ done,
                                                              const float *__restrict__ ep_reward,
                                                              const uint8_t *__restrict__ score, int64_t n,
-                                                             TrainStats *st) {
+                                                             TrainStats *st, Ctl *ctl, int64_t *replay_count) {
     __shared__ double s_r[1024];
     __shared__ int64_t s_n[1024], s_s[1024];
     __shared__ float s_m[1024];
@@ -74,13 +74,29 @@ __global__ __launch_bounds__(1024) void episode_stats_kernel(const uint8_t *__re
             st->score_max = max(st->score_max, s_sm[0]);
         }
         st->env_steps += n;
+        // env_advance_kernel folded in: the step is complete
+        ctl->t += 1;
+        if (replay_count) *replay_count += n;
     }
 }
 
-__global__ void post_update_kernel(TrainStats *st, const double *loss, double *log, int64_t log_cap, float decay,
-                                   float eps_end) {
+// tr.losses / epsilon decay / nb += 1 after an update (utils.jl:456-481), with
+// the Huber mean over the batch reduced here (loss_mean_kernel's order)
+__global__ __launch_bounds__(256) void post_update_kernel(TrainStats *st, const double *__restrict__ loss, int64_t B,
+                                                          double *loss_out, double *log, int64_t log_cap,
+                                                          float decay, float eps_end) {
+    __shared__ double sh[256];
+    double v = 0.0;
+    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) v += loss[i];
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
     if (threadIdx.x != 0) return;
-    const double l = *loss;
+    const double l = sh[0] / (double)B;
+    *loss_out = l;
     st->last_loss = l;
     if (log) log[st->updates % log_cap] = l;          // track_loss! (utils.jl:404-406)
     st->epsilon = fmaxf(st->epsilon - decay, eps_end); // utils.jl:480
@@ -110,13 +126,28 @@ struct snk_trainer_s {
     hipGraph_t graph[2] = {nullptr, nullptr};
     hipGraphExec_t exec[2] = {nullptr, nullptr};
     hipStream_t graph_stream = nullptr;
+    Fork fork;   // side streams: parallel branches of the iteration
 };
 
-// One iteration's launch sequence (capturable: no host sync, no allocation)
+// One iteration's launch sequence (capturable: no host sync, no allocation).
+// Side branches: the first update's replay draw runs beside the act forward
+// (it only needs the transition count, which it offsets by the n transitions
+// this step stores; the advance kernel waits for it), episode statistics run
+// beside the update, and the update itself forks the target forward and the
+// weight gradients (dqn_loss_grad / qnet_backward).
 static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
     const EnvDev &E = env_dev(h->env);
     const ReplayDev &R = replay_dev(h->rb);
     snk_dqn_s *q = h->dqn;
+    Fork &F = h->fork;
+    F.main = s;
+    F.next = 0;
+    const bool upd = learn && h->cfg.updates_per_iter > 0;
+    const uint64_t sseed = h->cfg.seed ^ 0x5A4D504C45ULL;
+    if (upd) {
+        hipStream_t q2 = F.fork(2, FK_SAMPLE);
+        replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, q2, E.n);
+    }
     HeadArgs ha;
     ha.act = h->act;
     ha.seed = h->cfg.seed;
@@ -124,27 +155,42 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
     ha.eps_dev = &h->stats->epsilon;
     qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s);
     env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s);
-    env_launch_advance(E, &R, s);
-    episode_stats_kernel<<<1, 1024, 0, s>>>(E.out_done, E.out_ep_reward, E.out_score, E.n, h->stats);
+    if (upd) F.join(2, FK_SAMPLE);
+    hipStream_t q1 = F.fork(1, FK_STATS);
+    episode_stats_kernel<<<1, 1024, 0, q1>>>(E.out_done, E.out_ep_reward, E.out_score, E.n, h->stats, E.ctl,
+                                             R.count);
     launch_check("episode_stats_kernel");
-    if (!learn) return;
-    for (int u = 0; u < h->cfg.updates_per_iter; ++u) {
-        replay_launch_sample(R, h->B, h->cfg.seed ^ 0x5A4D504C45ULL, 0, &h->stats->updates, h->idx, nullptr, s);
-        HeadArgs m;
-        m.idx = h->idx;
-        m.rew = R.reward;
-        m.done = R.done;
-        m.mask = R.mask;
-        m.act_idx = R.act;
-        dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s);
-        if (h->comm) comm_allreduce_mean(h->comm, q->grad, q->L.P, s);   // data-parallel replicas
-        rmsprop_launch(q->L.P, q->theta_q, q->acc, q->grad, q->lr, q->rho, q->eps, s);
-        dqn_q_changed(q, s);
-        dqn_sync_target_launch(q, &h->stats->updates, h->cfg.target_update_rate, s);
-        post_update_kernel<<<1, 64, 0, s>>>(h->stats, q->loss_dev, h->loss_log, h->log_cap, h->cfg.decay,
-                                            h->cfg.epsilon_end);
-        launch_check("post_update_kernel");
+    if (upd) {
+        for (int u = 0; u < h->cfg.updates_per_iter; ++u) {
+            if (u > 0)
+                replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s);
+            HeadArgs m;
+            m.idx = h->idx;
+            m.rew = R.reward;
+            m.done = R.done;
+            m.mask = R.mask;
+            m.act_idx = R.act;
+            GradSlabs pend;
+            LossOpts lo;
+            lo.fork = &F;
+            lo.defer = &pend;
+            lo.loss_mean = false;
+            dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s, lo);
+            // one pass: finish the gradient, RMSProp, forward image, update_target_net! when due
+            const UpdateTarget ut = dqn_update_target(q, &h->stats->updates, h->cfg.target_update_rate);
+            if (h->comm) {   // data-parallel replicas: mean gradient before the step
+                grad_update_launch(q->L, &pend, q->grad, nullptr, s);
+                comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
+                grad_update_launch(q->L, nullptr, q->grad, &ut, s);
+            } else {
+                grad_update_launch(q->L, &pend, q->grad, &ut, s);
+            }
+            post_update_kernel<<<1, 256, 0, s>>>(h->stats, q->trn.loss, h->B, q->loss_dev, h->loss_log, h->log_cap,
+                                                 h->cfg.decay, h->cfg.epsilon_end);
+            launch_check("post_update_kernel");
+        }
     }
+    F.join(1, FK_STATS);
 }
 
 extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, snk_replay rb,
@@ -169,6 +215,11 @@ extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, sn
         h->act = dalloc<uint8_t>(E.n);
         h->idx = dalloc<int64_t>(h->B);
         h->loss_log = dalloc<double>(h->log_cap);
+        h->fork.create();
+        // parallel graph branches measured slower than one serial chain on
+        // this stack (each cross-stream edge cost ~30 us): off unless asked for
+        h->fork.enable = 0;
+        if (const char *e = getenv("SNK_FORK")) h->fork.enable = (unsigned)strtoul(e, nullptr, 0);
         TrainStats st{};
         st.epsilon = cfg->epsilon;
         st.reward_max = -INFINITY;
@@ -200,6 +251,7 @@ extern "C" int snk_trainer_destroy(snk_trainer h) {
             if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
         }
         for (void *p : {(void *)h->stats, (void *)h->act, (void *)h->idx, (void *)h->loss_log}) dfree(p);
+        h->fork.destroy();
         delete h;
     });
 }
