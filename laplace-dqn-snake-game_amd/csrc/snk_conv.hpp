@@ -36,6 +36,8 @@ struct ConvArgs {
     const float *bias;   // EPI_BIAS_RELU
     const float *act;    // EPI_RELU_MASK: mask source, same shape as out
     float *out;          // [M][CN] or slab [split][M][CN]
+    const uint16_t *xb;  // x6 kernels: A pre-split into bf16 planes [S][HIN*HIN][3][CK] (else split x)
+    uint16_t *outb;      // x6 EPI_BIAS_RELU: also write the output's bf16 planes [M][3][CN]
     int M, HIN, HOUT, nkk, kk_per_split;
     uint32_t d2m, d2s, d1m, d1s;   // FastDiv(HOUT*HOUT), FastDiv(HOUT) magic/shift
 };

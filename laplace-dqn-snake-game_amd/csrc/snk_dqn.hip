@@ -2,6 +2,8 @@
 // RMSProp state, plus the C-ABI for forward, epsilon_greedy, the DQN update
 // (utils.jl:442-466) and update_target_net! (utils.jl:174-177).
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "snk_dqn.hpp"
@@ -47,12 +49,21 @@ void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, 
     copy_if_due_kernel<<<(unsigned)std::min<int64_t>(ceil_div(h->L.T, 256), 2048), 256, 0, s>>>(
         h->wt_q, h->wt_t, h->L.T, counter, rate);
     launch_check("copy_if_due_kernel");
+    if (h->wtb_q) {   // 3*T bf16 = 1.5*T words (T is even)
+        copy_if_due_kernel<<<(unsigned)std::min<int64_t>(ceil_div(h->L.T, 256), 2048), 256, 0, s>>>(
+            reinterpret_cast<const float *>(h->wtb_q), reinterpret_cast<float *>(h->wtb_t), 3 * h->L.T / 2, counter,
+            rate);
+        launch_check("copy_if_due_kernel");
+    }
 }
 
-void dqn_q_changed(snk_dqn_s *h, hipStream_t s) { transpose_fwd_launch(h->L, h->theta_q, h->wt_q, s); }
+void dqn_q_changed(snk_dqn_s *h, hipStream_t s) { transpose_fwd_launch(h->L, h->theta_q, h->wt_q, h->wtb_q, s); }
 
 static const float *which_wt(snk_dqn_s *h, int32_t which) {
     return which == SNK_NET_TARGET ? h->wt_t : h->wt_q;
+}
+static const uint16_t *which_wtb(snk_dqn_s *h, int32_t which) {
+    return which == SNK_NET_TARGET ? h->wtb_t : h->wtb_q;
 }
 
 BoardSrc src_env(const EnvDev &E) {
@@ -105,15 +116,15 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
     ta.B = B;
     // t_net(s') (optionally on a side stream beside q_net(s)); the loss head needs both
     hipStream_t q0 = F.fork(0, FK_TARGET);
-    qnet_forward(h->L, h->theta_t, h->wt_t, sn_src, B, h->tgt, HEAD_TARGET, ta, q0);
+    qnet_forward(h->L, h->theta_t, h->wt_t, sn_src, B, h->tgt, HEAD_TARGET, ta, q0, -1, h->wtb_t);
     HeadArgs la = ta;
     la.loss = h->trn.loss;
     la.dq = h->trn.dq;
     la.dz1 = h->trn.dz1;
     for (int layer = 0; layer < 4; ++layer)
-        qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, layer);
+        qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, layer, h->wtb_q);
     F.join(0, FK_TARGET);
-    qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, 4);
+    qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, 4, h->wtb_q);
     hipStream_t q1 = o.loss_mean ? F.fork(1, FK_LOSS) : s;
     if (o.loss_mean) loss_mean_launch(h->trn.loss, B, h->loss_dev, q1);
     BwdOpts bo;
@@ -131,6 +142,8 @@ UpdateTarget dqn_update_target(snk_dqn_s *h, const int64_t *counter, int64_t rat
     u.wt = h->wt_q;
     u.theta_t = h->theta_t;
     u.wt_t = h->wt_t;
+    u.wtb = h->wtb_q;
+    u.wtb_t = h->wtb_t;
     u.counter = counter;
     u.rate = rate;
     u.lr = h->lr;
@@ -188,6 +201,12 @@ extern "C" int snk_dqn_create(snk_dqn *out, int32_t bs, int32_t C, float lr, flo
         SNK_HIP(hipMemcpyAsync(h->tmp, flux.data(), P * 4, hipMemcpyHostToDevice, s));
         h->wt_q = dalloc<float>(h->L.T);
         h->wt_t = dalloc<float>(h->L.T);
+        // forward GEMMs on the exact bf16x6 split (default) or plain fp32 MFMA (SNK_CONV=fp32)
+        const char *cm = getenv("SNK_CONV");
+        if (!(cm && strcmp(cm, "fp32") == 0)) {
+            h->wtb_q = dalloc<uint16_t>(3 * h->L.T);
+            h->wtb_t = dalloc<uint16_t>(3 * h->L.T);
+        }
         dqn_permute(h, h->tmp, h->theta_q, true, s);
         dqn_q_changed(h, s);
         dqn_sync_target_launch(h, nullptr, 1, s);   // t_net = deepcopy(q_net) (structs.jl:177)
@@ -210,7 +229,7 @@ extern "C" int snk_dqn_destroy(snk_dqn h) {
         for (void *p : {(void *)h->jbuf, (void *)h->jidx, (void *)h->jact, (void *)h->theta_q, (void *)h->theta_t,
                         (void *)h->acc, (void *)h->grad, (void *)h->tmp,
                         (void *)h->perm, (void *)h->slab, (void *)h->loss_dev, (void *)h->meta, (void *)h->wt_q,
-                        (void *)h->wt_t})
+                        (void *)h->wt_t, (void *)h->wtb_q, (void *)h->wtb_t})
             dfree(p);
         delete h;
     });
@@ -242,7 +261,7 @@ extern "C" int snk_dqn_set_params(snk_dqn h, int32_t which, const float *flux_ho
         SNK_HIP(hipMemcpyAsync(h->tmp, flux_host, h->L.P * 4, hipMemcpyHostToDevice, s));
         dqn_permute(h, h->tmp, dst, true, s);
         if (which == SNK_NET_Q) dqn_q_changed(h, s);
-        if (which == SNK_NET_TARGET) transpose_fwd_launch(h->L, h->theta_t, h->wt_t, s);
+        if (which == SNK_NET_TARGET) transpose_fwd_launch(h->L, h->theta_t, h->wt_t, h->wtb_t, s);
         SNK_HIP(hipStreamSynchronize(s));
     });
 }
@@ -278,7 +297,8 @@ extern "C" int snk_dqn_forward(snk_dqn h, int32_t which, const float *x_dev, int
         SNK_CHECK(which == SNK_NET_Q || which == SNK_NET_TARGET, SNK_ERR_INVALID, "forward needs q or target net");
         hipStream_t s = stream();
         qwork_ensure(h->act, h->L, B, false);
-        qnet_forward(h->L, which_buf(h, which), which_wt(h, which),src_float(h->L, x_dev), B, h->act, HEAD_Q, HeadArgs{}, s);
+        qnet_forward(h->L, which_buf(h, which), which_wt(h, which), src_float(h->L, x_dev), B, h->act, HEAD_Q,
+                     HeadArgs{}, s, -1, which_wtb(h, which));
         SNK_HIP(hipMemcpyAsync(q_dev, h->act.q, B * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
     });
 }
@@ -290,7 +310,8 @@ extern "C" int snk_dqn_forward_env(snk_dqn h, int32_t which, snk_env env, float 
         SNK_CHECK(E.bs == h->L.bs && E.C == h->L.C, SNK_ERR_INVALID, "env/model geometry mismatch");
         hipStream_t s = stream();
         qwork_ensure(h->act, h->L, E.n, false);
-        qnet_forward(h->L, which_buf(h, which), which_wt(h, which),src_env(E), E.n, h->act, HEAD_Q, HeadArgs{}, s);
+        qnet_forward(h->L, which_buf(h, which), which_wt(h, which), src_env(E), E.n, h->act, HEAD_Q, HeadArgs{}, s,
+                     -1, which_wtb(h, which));
         SNK_HIP(hipMemcpyAsync(q_dev, h->act.q, E.n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
     });
 }
@@ -307,7 +328,7 @@ extern "C" int snk_dqn_act(snk_dqn h, snk_env env, float epsilon, uint64_t seed,
         ha.epsilon = epsilon;
         ha.seed = seed;
         ha.tptr = &E.ctl->t;
-        qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s);
+        qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, -1, h->wtb_q);
     });
 }
 
@@ -328,13 +349,14 @@ extern "C" int snk_dqn_time_act_layers(snk_dqn h, snk_env env, int32_t reps, dou
         ha.act = h->meta;
         ha.epsilon = 0.05f;
         ha.tptr = &E.ctl->t;
-        qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s);
+        qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, -1, h->wtb_q);
         hipEvent_t a, b;
         SNK_HIP(hipEventCreate(&a));
         SNK_HIP(hipEventCreate(&b));
         for (int layer = 0; layer < 5; ++layer) {
             SNK_HIP(hipEventRecord(a, s));
-            for (int r = 0; r < reps; ++r) qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, layer);
+            for (int r = 0; r < reps; ++r)
+                qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, layer, h->wtb_q);
             SNK_HIP(hipEventRecord(b, s));
             SNK_HIP(hipEventSynchronize(b));
             float ms = 0.0f;

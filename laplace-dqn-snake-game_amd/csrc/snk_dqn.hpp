@@ -7,6 +7,7 @@ struct snk_dqn_s {
     float lr = 5e-4f, rho = 0.9f, eps = 1e-8f;
     float *theta_q = nullptr, *theta_t = nullptr, *acc = nullptr, *grad = nullptr, *tmp = nullptr;
     float *wt_q = nullptr, *wt_t = nullptr;   // forward weight images of q_net / t_net
+    uint16_t *wtb_q = nullptr, *wtb_t = nullptr;   // their exact bf16 split planes (x6 forward); null = fp32 MFMA
     int32_t *perm = nullptr;        // packed index -> Flux.destructure index
     snk::QWork act, tgt, trn;       // workspaces: acting (n_envs), target net, training batch
     float *slab = nullptr;

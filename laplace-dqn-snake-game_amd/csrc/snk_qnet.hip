@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "snk_conv_x6.hpp"
 #include "snk_qnet.hpp"
 
 namespace snk {
@@ -42,8 +43,10 @@ QLayout make_layout(int bs, int C) {
     return L;
 }
 
-// block [nkk][CK][CN] of theta -> [nkk][CN][CK] of the image (c contiguous per output)
-__global__ void transpose_fwd_kernel(const float *__restrict__ th, float *__restrict__ wt, QLayout L) {
+// block [nkk][CK][CN] of theta -> [nkk][CN][CK] of the image (c contiguous per output),
+// and (wtb) its exact bf16 split planes [nkk][plane][CN][CK]
+__global__ void transpose_fwd_kernel(const float *__restrict__ th, float *__restrict__ wt, uint16_t *__restrict__ wtb,
+                                     QLayout L) {
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < L.T; t += (int64_t)gridDim.x * blockDim.x) {
         int64_t base, u;
         int CK, CN;
@@ -57,12 +60,18 @@ __global__ void transpose_fwd_kernel(const float *__restrict__ th, float *__rest
         const int64_t kk = u / (CK * CN);
         const int r = (int)(u - kk * CK * CN);
         const int n = r / CK, c = r - n * CK;
-        wt[t] = th[base + (kk * CK + c) * CN + n];
+        const float v = th[base + (kk * CK + c) * CN + n];
+        wt[t] = v;
+        if (wtb) {
+            const int64_t x6 = 3 * (t - u) + kk * 3 * CK * CN + r;   // section base * 3 + [kk][plane][n][c]
+#pragma unroll
+            for (int p = 0; p < 3; ++p) wtb[x6 + p * CK * CN] = split_part(v, p);
+        }
     }
 }
 
-void transpose_fwd_launch(const QLayout &L, const float *theta, float *wt, hipStream_t s) {
-    transpose_fwd_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.T, 256), 2048), 256, 0, s>>>(theta, wt, L);
+void transpose_fwd_launch(const QLayout &L, const float *theta, float *wt, uint16_t *wtb, hipStream_t s) {
+    transpose_fwd_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.T, 256), 2048), 256, 0, s>>>(theta, wt, wtb, L);
     launch_check("transpose_fwd_kernel");
 }
 
@@ -277,13 +286,32 @@ static int conv_splits(int64_t M, int nkk) {
     return (int)std::min<int64_t>(std::min(nkk, 16), ceil_div(512, wgs));
 }
 
+// wb != nullptr: the bf16x6 split-precision kernel on the weight planes wb
 template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
-static void conv_launch(ConvArgs a, int splits, hipStream_t s) {
+static void conv_launch(ConvArgs a, int splits, hipStream_t s, const uint16_t *wb = nullptr) {
     a.kk_per_split = ceil_div(a.nkk, splits);
     splits = ceil_div(a.nkk, a.kk_per_split);
     const FastDiv d2((uint32_t)std::max(1, a.HOUT * a.HOUT)), d1((uint32_t)std::max(1, a.HOUT));
     a.d2m = d2.m; a.d2s = d2.s; a.d1m = d1.m; a.d1s = d1.s;
     dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)splits);
+    if constexpr (MODE != MODE_DX) {
+        if (wb) {
+            if constexpr (MODE == MODE_FWD && CK % 32 == 0 && EPI != EPI_RELU_MASK) {
+                if (a.xb) {   // pre-split input, 32-channel chunks: the 16x16x32 layout
+                    conv_x6m16_kernel<CK, CN, KS, PAD, EPI><<<grid, 256, 0, s>>>(a, wb);
+                    launch_check("conv_x6m16_kernel");
+                    return;
+                }
+            }
+            if (a.xb)
+                conv_x6_kernel<CK, CN, KS, PAD, MODE, EPI, true><<<grid, 256, 0, s>>>(a, wb);
+            else
+                conv_x6_kernel<CK, CN, KS, PAD, MODE, EPI, false><<<grid, 256, 0, s>>>(a, wb);
+            launch_check("conv_x6_kernel");
+            return;
+        }
+    }
+    SNK_CHECK(!a.xb && !a.outb, SNK_ERR_INTERNAL, "bf16 planes need the x6 kernels");
     conv_mfma_kernel<CK, CN, KS, PAD, MODE, EPI><<<grid, 256, 0, s>>>(a);
     launch_check("conv_mfma_kernel");
 }
@@ -291,13 +319,20 @@ static void conv_launch(ConvArgs a, int splits, hipStream_t s) {
 // finish a kk-split conv: out = relu(sum_z slab[z] + bias)  or  (act > 0) * sum_z slab[z]
 __global__ void conv_reduce_kernel(const float *__restrict__ slab, int splits, int64_t MN, int N,
                                    const float *__restrict__ bias, const float *__restrict__ act,
-                                   float *__restrict__ out) {
+                                   float *__restrict__ out, uint16_t *__restrict__ outb = nullptr) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += (int64_t)gridDim.x * blockDim.x) {
         float v = 0.0f;
         for (int z = 0; z < splits; ++z) v += slab[(int64_t)z * MN + i];
         if (bias) {
             v += bias[i % N];
-            out[i] = v > 0.0f ? v : 0.0f;
+            v = v > 0.0f ? v : 0.0f;
+            if (out) out[i] = v;
+            if (outb) {   // bf16 planes [row][3][N]
+                const int64_t row = i / N;
+                const int col = (int)(i - row * N);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) outb[(row * 3 + p) * N + col] = split_part(v, p);
+            }
         } else {
             out[i] = act[i] > 0.0f ? v : 0.0f;
         }
@@ -305,65 +340,96 @@ __global__ void conv_reduce_kernel(const float *__restrict__ slab, int splits, i
 }
 
 // out = conv (bias + relu), kk-split through the conv slab when the grid is small
+// xb / outb (x6 only): pre-split input planes / also write the output's planes
 template <int CK, int CN, int KS, int PAD>
 static void conv_fwd(const float *x, const float *w, const float *bias, float *out, int64_t M, int HIN, int HOUT,
-                     QWork &wk, hipStream_t s) {
+                     QWork &wk, hipStream_t s, const uint16_t *wb, const uint16_t *xb = nullptr,
+                     uint16_t *outb = nullptr) {
     ConvArgs a{};
     a.x = x; a.w = w; a.bias = bias; a.M = (int)M; a.HIN = HIN; a.HOUT = HOUT; a.nkk = KS * KS;
+    a.xb = xb;
     const int sp = conv_splits(M, a.nkk);
     if (sp == 1) {
         a.out = out;
-        conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_BIAS_RELU>(a, 1, s);
+        a.outb = outb;
+        conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_BIAS_RELU>(a, 1, s, wb);
         return;
     }
     a.out = wk.cslab;
     SNK_CHECK((int64_t)sp * M * CN <= wk.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
-    conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_SLAB>(a, sp, s);
+    conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_SLAB>(a, sp, s, wb);
     const int used = ceil_div(a.nkk, ceil_div(a.nkk, sp));
     conv_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(M * CN, 256), 4096), 256, 0, s>>>(
-        wk.cslab, used, M * CN, CN, bias, nullptr, out);
+        wk.cslab, used, M * CN, CN, bias, nullptr, out, outb);
     launch_check("conv_reduce_kernel");
 }
 
 // ---------------------------------------------------------------- conv1 (VALU)
+// 3x3, C -> 16, pad 1 (K = 9C is too small for MFMA). A workgroup owns NS
+// samples: their input planes go to LDS once as floats inside a zero border
+// ((bs+2)^2 per plane), so the 9C taps of an output are unconditional LDS
+// reads; one thread per output position writes its 16 channels as 4 float4.
+// yb (optional): the output also as bf16 split planes [S*bs*bs][3][16] (x6 conv2 input);
+// y may then be null. NS samples per workgroup (fewer for small batches: more CUs busy).
 template <int C>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(BoardSrc src, const float *__restrict__ w,
                                                         const float *__restrict__ b, float *__restrict__ y,
-                                                        int64_t S, int bs) {
-    __shared__ float sw[9 * C * 16 + 16];
+                                                        uint16_t *__restrict__ yb, int64_t S, int bs, int NS) {
+    extern __shared__ float sm[];
+    float *sw = sm;                       // [9*C*16 + 16]
+    float *sx = sm + 9 * C * 16 + 16;     // [NS][C][(bs+2)^2]
+    const int bp = bs + 2, plane = bp * bp, ncell = bs * bs;
     for (int i = threadIdx.x; i < 9 * C * 16; i += blockDim.x) sw[i] = w[i];
     if (threadIdx.x < 16) sw[9 * C * 16 + threadIdx.x] = b[threadIdx.x];
+    const int64_t s0 = (int64_t)blockIdx.x * NS;
+    const int ns = (int)min((int64_t)NS, S - s0);
+    for (int i = threadIdx.x; i < NS * C * plane; i += blockDim.x) sx[i] = 0.0f;
     __syncthreads();
-    const int ncell = bs * bs;
-    const int64_t total = S * ncell;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t s = q / ncell;
-        const int p = (int)(q - s * ncell);
+    for (int i = threadIdx.x; i < ns * C * ncell; i += blockDim.x) {
+        const int sc = i / ncell, cell = i - sc * ncell;
+        const int sl = sc / C, c = sc - sl * C;
+        const int jj = cell / bs, ii = cell - jj * bs;
+        const int8_t *pl = src.plane(s0 + sl, c);
+        const float v = pl ? (float)pl[cell] : src.fbase[((s0 + sl) * C + c) * ncell + cell];
+        sx[sc * plane + (ii + 1) + (jj + 1) * bp] = v;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < ns * ncell; q += blockDim.x) {
+        const int sl = q / ncell, p = q - sl * ncell;
         const int j = p / bs, i = p - j * bs;
         float acc[16];
 #pragma unroll
         for (int co = 0; co < 16; ++co) acc[co] = sw[9 * C * 16 + co];
-        const int8_t *pl[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) pl[c] = src.plane(s, c);
 #pragma unroll
         for (int kk = 0; kk < 9; ++kk) {
-            const int du = kk % 3, dv = kk / 3;
-            const int xi = i + du - 1, xj = j + dv - 1;
-            if (xi < 0 || xi >= bs || xj < 0 || xj >= bs) continue;
+            const int du = kk % 3, dv = kk / 3;   // input (i+du-1, j+dv-1) = bordered (i+du, j+dv)
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const int cell = xi + xj * bs;
-                const float v = pl[c] ? (float)pl[c][cell] : src.fbase[(s * C + c) * ncell + cell];
+                const float v = sx[(sl * C + c) * plane + (i + du) + (j + dv) * bp];
 #pragma unroll
                 for (int co = 0; co < 16; ++co) acc[co] = __builtin_fmaf(v, sw[(kk * C + c) * 16 + co], acc[co]);
             }
         }
-        float4 *o = reinterpret_cast<float4 *>(y + q * 16);
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
-            o[v] = make_float4(fmaxf(acc[4 * v], 0.f), fmaxf(acc[4 * v + 1], 0.f), fmaxf(acc[4 * v + 2], 0.f),
-                               fmaxf(acc[4 * v + 3], 0.f));
+        for (int co = 0; co < 16; ++co) acc[co] = fmaxf(acc[co], 0.f);
+        const int64_t row = s0 * ncell + q;
+        if (y) {
+            float4 *o = reinterpret_cast<float4 *>(y + row * 16);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) o[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+        }
+        if (yb) {
+            u32x4 *o = reinterpret_cast<u32x4 *>(yb + row * 48);
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const Split3 sp = split3(f32x4{acc[8 * half], acc[8 * half + 1], acc[8 * half + 2], acc[8 * half + 3]},
+                                         f32x4{acc[8 * half + 4], acc[8 * half + 5], acc[8 * half + 6],
+                                               acc[8 * half + 7]});
+                o[0 + half] = sp.h;   // plane p, channels 8*half..8*half+7
+                o[2 + half] = sp.m;
+                o[4 + half] = sp.l;
+            }
+        }
     }
 }
 
@@ -510,7 +576,8 @@ __global__ void loss_mean_kernel(const double *__restrict__ loss, int64_t B, dou
 
 // ---------------------------------------------------------------- workspace
 void qwork_free(QWork &w) {
-    for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a3, (void *)w.slab, (void *)w.cslab, (void *)w.h1, (void *)w.q,
+    for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a2b, (void *)w.a1b, (void *)w.a3, (void *)w.slab, (void *)w.cslab,
+                    (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.target,
                     (void *)w.loss})
         dfree(p);
@@ -553,6 +620,8 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     w.cslab = dalloc<float>((size_t)std::max<int64_t>(cslab, 1));
     w.a1 = dalloc<float>((size_t)cap * L.ncell * 16);
     w.a2 = dalloc<float>((size_t)cap * L.ncell * 32);
+    w.a2b = dalloc<uint16_t>((size_t)cap * L.ncell * 96);
+    w.a1b = dalloc<uint16_t>((size_t)cap * L.ncell * 48);
     w.a3 = dalloc<float>((size_t)cap * L.K1);
     w.slab = dalloc<float>((size_t)slab);
     w.h1 = dalloc<float>((size_t)cap * 64);
@@ -571,22 +640,29 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
 
 // ---------------------------------------------------------------- forward
 void qnet_forward(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
-                  HeadMode mode,
-                  const HeadArgs &ha, hipStream_t s, int only) {
+                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only, const uint16_t *wtb) {
     const int bs = L.bs, nc = L.ncell;
     if (only < 0 || only == 0) {
-        const int64_t total = S * nc;
-        const int grid = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
+        const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S / 256));
+        const int grid = ceil_div(S, ns);
+        const size_t lds = (size_t)(9 * L.C * 16 + 16 + ns * L.C * (bs + 2) * (bs + 2)) * sizeof(float);
+        // x6: a1 also (acting: only) as bf16 planes for conv2
+        float *y = (wtb && !w.has_train) ? nullptr : w.a1;
+        uint16_t *yb = wtb ? w.a1b : nullptr;
         if (L.C == 1)
-            conv1_fwd_kernel<1><<<grid, 256, 0, s>>>(src, th + L.off_w1, th + L.off_b1, w.a1, S, bs);
+            conv1_fwd_kernel<1><<<grid, 256, lds, s>>>(src, th + L.off_w1, th + L.off_b1, y, yb, S, bs, ns);
         else
-            conv1_fwd_kernel<2><<<grid, 256, 0, s>>>(src, th + L.off_w1, th + L.off_b1, w.a1, S, bs);
+            conv1_fwd_kernel<2><<<grid, 256, lds, s>>>(src, th + L.off_w1, th + L.off_b1, y, yb, S, bs, ns);
         launch_check("conv1_fwd_kernel");
     }
     if (only < 0 || only == 1)   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
-        conv_fwd<16, 32, 3, 1>(w.a1, wt + L.off_t2, th + L.off_b2, w.a2, S * nc, bs, bs, w, s);
+        // x6: a2 also (acting: only) as bf16 planes for conv3; training keeps fp32 a2 for the backward
+        conv_fwd<16, 32, 3, 1>(w.a1, wt + L.off_t2, th + L.off_b2, (wtb && !w.has_train) ? nullptr : w.a2, S * nc,
+                               bs, bs, w, s, wtb ? wtb + 3 * L.off_t2 : nullptr, wtb ? w.a1b : nullptr,
+                               wtb ? w.a2b : nullptr);
     if (only < 0 || only == 2)   // conv3: M = S*Wo^2, K = 36 offsets x 32, N = 64
-        conv_fwd<32, 64, 6, 0>(w.a2, wt + L.off_t3, th + L.off_b3, w.a3, S * L.Wo * L.Wo, bs, L.Wo, w, s);
+        conv_fwd<32, 64, 6, 0>(w.a2, wt + L.off_t3, th + L.off_b3, w.a3, S * L.Wo * L.Wo, bs, L.Wo, w, s,
+                               wtb ? wtb + 3 * L.off_t3 : nullptr, wtb ? w.a2b : nullptr);
     int kc;
     const int ks = d1_split(L, S, kc);
     // Dense1 (split over the Wo^2 positions into partial slabs; bias + relu in the head)
@@ -594,7 +670,7 @@ void qnet_forward(const QLayout &L, const float *th, const float *wt, const Boar
         ConvArgs a{};
         a.x = w.a3; a.w = wt + L.off_td; a.out = w.slab; a.M = (int)S; a.HIN = L.Wo; a.HOUT = 1;
         a.nkk = L.Wo * L.Wo;
-        conv_launch<64, 64, 0, 0, MODE_DENSE, EPI_SLAB>(a, ks, s);
+        conv_launch<64, 64, 0, 0, MODE_DENSE, EPI_SLAB>(a, ks, s, wtb ? wtb + 3 * L.off_td : nullptr);
     }
     if (only >= 0 && only != 4) return;
     const int grid = ceil_div(S, 4);
@@ -778,8 +854,9 @@ struct UpdArgs {
     int finish, apply;
 };
 
-// index of packed parameter i in the forward weight image, or -1
-__device__ __forceinline__ int64_t image_index(const QLayout &L, int64_t i) {
+// index of packed parameter i in the forward weight image, or -1; x6 = its
+// plane-0 index in the bf16 split image (planes CK*CN apart)
+__device__ __forceinline__ int64_t image_index(const QLayout &L, int64_t i, int64_t &x6, int &pstride) {
     int64_t u, base;
     int CK, CN;
     if (i >= L.off_w2 && i < L.off_b2) {
@@ -794,6 +871,8 @@ __device__ __forceinline__ int64_t image_index(const QLayout &L, int64_t i) {
     const int64_t kk = u / (CK * CN);
     const int r = (int)(u - kk * CK * CN);
     const int c = r / CN, n = r - c * CN;
+    x6 = 3 * base + kk * 3 * CK * CN + (int64_t)n * CK + c;
+    pstride = CK * CN;
     return base + kk * CK * CN + (int64_t)n * CK + c;
 }
 
@@ -817,13 +896,21 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
             if (i >= L.off_d2w) {   // d2_grad order
                 const int t = (int)(i - L.off_d2w);
                 float acc = 0.0f;
-                if (t < 192) {
-                    const int ac = t >> 6, o = t & 63;
-                    for (int64_t s = 0; s < a.g.S; ++s) acc = __builtin_fmaf(a.g.dq[s * 3 + ac], a.g.h1[s * 64 + o], acc);
-                } else {
-                    const int ac = t - 192;
-                    for (int64_t s = 0; s < a.g.S; ++s) acc += a.g.dq[s * 3 + ac];
+                // same sequential order as d2_grad_kernel; loads batched 16 deep (they do not depend on acc)
+                const int ac = t < 192 ? t >> 6 : t - 192, o = t & 63;
+                int64_t s = 0;
+                for (; s + 16 <= a.g.S; s += 16) {
+                    float dv[16], hv[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        dv[u] = a.g.dq[(s + u) * 3 + ac];
+                        hv[u] = t < 192 ? a.g.h1[(s + u) * 64 + o] : 1.0f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) acc = t < 192 ? __builtin_fmaf(dv[u], hv[u], acc) : acc + dv[u];
                 }
+                for (; s < a.g.S; ++s)
+                    acc = t < 192 ? __builtin_fmaf(a.g.dq[s * 3 + ac], a.g.h1[s * 64 + o], acc) : acc + a.g.dq[s * 3 + ac];
                 g = acc;
             }
             a.grad[i] = g;
@@ -836,11 +923,21 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
         a.u.acc[i] = qd;
         const float th = a.u.theta[i] - (g * a.u.lr) / (__builtin_sqrtf(qd) + a.u.eps);
         a.u.theta[i] = th;
-        const int64_t t = image_index(L, i);
-        if (t >= 0) a.u.wt[t] = th;
+        int64_t x6 = 0;
+        int ps = 0;
+        const int64_t t = image_index(L, i, x6, ps);
+        if (t >= 0) {
+            a.u.wt[t] = th;
+            if (a.u.wtb)
+                for (int p = 0; p < 3; ++p) a.u.wtb[x6 + p * ps] = split_part(th, p);
+        }
         if (due) {
             a.u.theta_t[i] = th;
-            if (t >= 0) a.u.wt_t[t] = th;
+            if (t >= 0) {
+                a.u.wt_t[t] = th;
+                if (a.u.wtb_t)
+                    for (int p = 0; p < 3; ++p) a.u.wtb_t[x6 + p * ps] = split_part(th, p);
+            }
         }
     }
 }

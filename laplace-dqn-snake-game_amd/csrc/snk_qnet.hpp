@@ -30,7 +30,8 @@ QLayout make_layout(int bs, int C);
 // flux index of every packed index (host)
 void packed_to_flux_index(const QLayout &L, int32_t *perm);
 // theta -> forward weight image (after every change of theta)
-void transpose_fwd_launch(const QLayout &L, const float *theta, float *wt, hipStream_t s);
+// wtb (optional): the exact bf16 split planes of the image (3*T uint16) for the x6 kernels
+void transpose_fwd_launch(const QLayout &L, const float *theta, float *wt, uint16_t *wtb, hipStream_t s);
 
 // Source of the Q-net input planes: env frame ring, replay slots, or a
 // float tensor in Julia (bs,bs,C,B) memory.
@@ -66,6 +67,8 @@ struct QWork {
     int64_t cap = 0, slab_floats = 0, cslab_floats = 0;
     float *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *slab = nullptr, *h1 = nullptr, *q = nullptr;
     float *cslab = nullptr;   // partial sums of kk-split convolutions
+    uint16_t *a2b = nullptr;  // x6 forward: a2 as bf16 planes [S*ncell][3][32]
+    uint16_t *a1b = nullptr;  // x6 forward: a1 as bf16 planes [S*ncell][3][16]
     // training only
     float *dq = nullptr, *dz1 = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dzc1 = nullptr;
     double *target = nullptr, *loss = nullptr;
@@ -101,8 +104,9 @@ struct HeadArgs {
 // forward: q[S][3] into w.q (and w.h1); mode-specific epilogue
 // only = -1: the whole chain; 0..4: just conv1 / conv2 / conv3 / dense1 / head
 // (inputs from a previous full forward; used for per-layer timing)
+// wtb (optional): bf16 split planes of the image -> conv2/conv3/Dense1 on the x6 kernels
 void qnet_forward(const QLayout &L, const float *theta, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
-                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1);
+                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1, const uint16_t *wtb = nullptr);
 // Weight-gradient sections a backward left as K-split partial slabs (z > 1),
 // plus Dense2's gradient (a reduction of dq x h1 over the batch): finished
 // inside the update kernel instead of by separate reduce launches.
@@ -126,6 +130,7 @@ void qnet_backward(const QLayout &L, const float *theta, const BoardSrc &src, in
 struct UpdateTarget {
     float *theta, *acc, *wt;
     float *theta_t, *wt_t;
+    uint16_t *wtb = nullptr, *wtb_t = nullptr;   // bf16 split planes of the images
     const int64_t *counter;   // nullptr: no target copy
     int64_t rate;
     float lr, rho, eps;

@@ -153,7 +153,7 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
     ha.seed = h->cfg.seed;
     ha.tptr = &E.ctl->t;
     ha.eps_dev = &h->stats->epsilon;
-    qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s);
+    qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q);
     env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s);
     if (upd) F.join(2, FK_SAMPLE);
     hipStream_t q1 = F.fork(1, FK_STATS);
