@@ -42,10 +42,18 @@ struct ConvArgs {
     uint32_t d2m, d2s, d1m, d1s;   // FastDiv(HOUT*HOUT), FastDiv(HOUT) magic/shift
 };
 
+// one launch can run the same convolution for two independent nets
+// (grid.z = group): the target and online forwards of a DQN update
+struct ConvPair {
+    ConvArgs g[2];
+    const uint16_t *wb[2];   // x6 kernels: weight planes per group
+};
+
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
 
 template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvPair pr) {
+    const ConvArgs &a = pr.g[blockIdx.z];
     constexpr int NT = CN / 32;
     constexpr int KB = CK / 8;
     constexpr int LDB = CK + 4;

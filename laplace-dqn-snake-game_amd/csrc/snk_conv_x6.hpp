@@ -75,7 +75,9 @@ __device__ __forceinline__ uint16_t split_part(float x, int p) {
 // PRE: A comes pre-split (a.xb, written by the producing layer's epilogue),
 // so the main loop does no conversion work at all
 template <int CK, int CN, int KS, int PAD, int MODE, int EPI, bool PRE>
-__global__ __launch_bounds__(256) void conv_x6_kernel(ConvArgs a, const uint16_t *__restrict__ wb) {
+__global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
+    const ConvArgs &a = pr.g[blockIdx.z];
+    const uint16_t *__restrict__ wb = pr.wb[blockIdx.z];
     constexpr int NT = CN / 32;
     constexpr int KC = CK / 16;                  // 16-channel MFMA chunks per offset
     constexpr int LDB = CK + 8;                  // bf16 per LDS row
@@ -264,7 +266,9 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 // B rows in LDS are padded to CK + 16 bf16 (96 B at CK = 32): conflict-free
 // for the four ds_read_b128 lane groups.
 template <int CK, int CN, int KS, int PAD, int EPI>
-__global__ __launch_bounds__(256) void conv_x6m16_kernel(ConvArgs a, const uint16_t *__restrict__ wb) {
+__global__ __launch_bounds__(256) void conv_x6m16_kernel(ConvPair pr) {
+    const ConvArgs &a = pr.g[blockIdx.z];
+    const uint16_t *__restrict__ wb = pr.wb[blockIdx.z];
     static_assert(CK % 32 == 0 && CN % 16 == 0, "shape");
     constexpr int NCT = CN / 16;                 // 16-column tiles
     constexpr int KC = CK / 32;                  // 32-channel MFMA chunks per offset

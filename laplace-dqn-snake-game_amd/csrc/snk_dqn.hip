@@ -114,17 +114,24 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
     ta.gamma = gamma;
     ta.target = h->trn.target;
     ta.B = B;
-    // t_net(s') (optionally on a side stream beside q_net(s)); the loss head needs both
-    hipStream_t q0 = F.fork(0, FK_TARGET);
-    qnet_forward(h->L, h->theta_t, h->wt_t, sn_src, B, h->tgt, HEAD_TARGET, ta, q0, -1, h->wtb_t);
+    // t_net(s') and q_net(s) share every layer launch; the loss head needs the target first
     HeadArgs la = ta;
     la.loss = h->trn.loss;
     la.dq = h->trn.dq;
     la.dz1 = h->trn.dz1;
-    for (int layer = 0; layer < 4; ++layer)
-        qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, layer, h->wtb_q);
-    F.join(0, FK_TARGET);
-    qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, 4, h->wtb_q);
+    if (o.fork && o.fork->on_side(FK_TARGET)) {   // separate branches (measured slower)
+        hipStream_t q0 = F.fork(0, FK_TARGET);
+        qnet_forward(h->L, h->theta_t, h->wt_t, sn_src, B, h->tgt, HEAD_TARGET, ta, q0, -1, h->wtb_t);
+        for (int layer = 0; layer < 4; ++layer)
+            qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, layer, h->wtb_q);
+        F.join(0, FK_TARGET);
+    } else {
+        const FwdNet nets[2] = {FwdNet{h->theta_t, h->wt_t, h->wtb_t, sn_src, &h->tgt},
+                                FwdNet{h->theta_q, h->wt_q, h->wtb_q, s_src, &h->trn}};
+        qnet_forward_pair(h->L, nets, B, s);
+        qnet_head(h->L, h->theta_t, B, h->tgt, HEAD_TARGET, ta, s);
+    }
+    qnet_head(h->L, h->theta_q, B, h->trn, HEAD_LOSS, la, s);
     hipStream_t q1 = o.loss_mean ? F.fork(1, FK_LOSS) : s;
     if (o.loss_mean) loss_mean_launch(h->trn.loss, B, h->loss_dev, q1);
     BwdOpts bo;

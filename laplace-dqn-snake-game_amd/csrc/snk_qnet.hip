@@ -287,81 +287,125 @@ static int conv_splits(int64_t M, int nkk) {
 }
 
 // wb != nullptr: the bf16x6 split-precision kernel on the weight planes wb
+// ng groups (1 or 2) of the same geometry in one launch (grid.z = group);
+// wb[g] != nullptr: the bf16x6 split-precision kernels on those weight planes
 template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
-static void conv_launch(ConvArgs a, int splits, hipStream_t s, const uint16_t *wb = nullptr) {
-    a.kk_per_split = ceil_div(a.nkk, splits);
-    splits = ceil_div(a.nkk, a.kk_per_split);
-    const FastDiv d2((uint32_t)std::max(1, a.HOUT * a.HOUT)), d1((uint32_t)std::max(1, a.HOUT));
-    a.d2m = d2.m; a.d2s = d2.s; a.d1m = d1.m; a.d1s = d1.s;
-    dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)splits);
+static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, const uint16_t *const *wb = nullptr) {
+    ConvPair pr{};
+    const int kper = ceil_div(ga[0].nkk, splits);
+    splits = ceil_div(ga[0].nkk, kper);
+    const FastDiv d2((uint32_t)std::max(1, ga[0].HOUT * ga[0].HOUT)), d1((uint32_t)std::max(1, ga[0].HOUT));
+    for (int g = 0; g < 2; ++g) {
+        ConvArgs a = ga[g < ng ? g : 0];
+        a.kk_per_split = kper;
+        a.d2m = d2.m; a.d2s = d2.s; a.d1m = d1.m; a.d1s = d1.s;
+        pr.g[g] = a;
+        pr.wb[g] = wb ? wb[g < ng ? g : 0] : nullptr;
+    }
+    const ConvArgs &a = pr.g[0];
+    dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)splits, (unsigned)ng);
     if constexpr (MODE != MODE_DX) {
-        if (wb) {
+        if (pr.wb[0]) {
             if constexpr (MODE == MODE_FWD && CK % 32 == 0 && EPI != EPI_RELU_MASK) {
                 if (a.xb) {   // pre-split input, 32-channel chunks: the 16x16x32 layout
-                    conv_x6m16_kernel<CK, CN, KS, PAD, EPI><<<grid, 256, 0, s>>>(a, wb);
+                    conv_x6m16_kernel<CK, CN, KS, PAD, EPI><<<grid, 256, 0, s>>>(pr);
                     launch_check("conv_x6m16_kernel");
                     return;
                 }
             }
             if (a.xb)
-                conv_x6_kernel<CK, CN, KS, PAD, MODE, EPI, true><<<grid, 256, 0, s>>>(a, wb);
+                conv_x6_kernel<CK, CN, KS, PAD, MODE, EPI, true><<<grid, 256, 0, s>>>(pr);
             else
-                conv_x6_kernel<CK, CN, KS, PAD, MODE, EPI, false><<<grid, 256, 0, s>>>(a, wb);
+                conv_x6_kernel<CK, CN, KS, PAD, MODE, EPI, false><<<grid, 256, 0, s>>>(pr);
             launch_check("conv_x6_kernel");
             return;
         }
     }
     SNK_CHECK(!a.xb && !a.outb, SNK_ERR_INTERNAL, "bf16 planes need the x6 kernels");
-    conv_mfma_kernel<CK, CN, KS, PAD, MODE, EPI><<<grid, 256, 0, s>>>(a);
+    conv_mfma_kernel<CK, CN, KS, PAD, MODE, EPI><<<grid, 256, 0, s>>>(pr);
     launch_check("conv_mfma_kernel");
+}
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
+static void conv_launch(ConvArgs a, int splits, hipStream_t s, const uint16_t *wb = nullptr) {
+    conv_launch<CK, CN, KS, PAD, MODE, EPI>(&a, 1, splits, s, &wb);
 }
 
 // finish a kk-split conv: out = relu(sum_z slab[z] + bias)  or  (act > 0) * sum_z slab[z]
-__global__ void conv_reduce_kernel(const float *__restrict__ slab, int splits, int64_t MN, int N,
-                                   const float *__restrict__ bias, const float *__restrict__ act,
-                                   float *__restrict__ out, uint16_t *__restrict__ outb = nullptr) {
+struct ReduceArgs {
+    const float *slab, *bias, *act;
+    float *out;
+    uint16_t *outb;   // bf16 planes [row][3][N]
+};
+struct ReducePair {
+    ReduceArgs g[2];
+};
+__global__ void conv_reduce_kernel(ReducePair rp, int splits, int64_t MN, int N) {
+    const ReduceArgs &r = rp.g[blockIdx.y];
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += (int64_t)gridDim.x * blockDim.x) {
         float v = 0.0f;
-        for (int z = 0; z < splits; ++z) v += slab[(int64_t)z * MN + i];
-        if (bias) {
-            v += bias[i % N];
+        for (int z = 0; z < splits; ++z) v += r.slab[(int64_t)z * MN + i];
+        if (r.bias) {
+            v += r.bias[i % N];
             v = v > 0.0f ? v : 0.0f;
-            if (out) out[i] = v;
-            if (outb) {   // bf16 planes [row][3][N]
+            if (r.out) r.out[i] = v;
+            if (r.outb) {
                 const int64_t row = i / N;
                 const int col = (int)(i - row * N);
 #pragma unroll
-                for (int p = 0; p < 3; ++p) outb[(row * 3 + p) * N + col] = split_part(v, p);
+                for (int p = 0; p < 3; ++p) r.outb[(row * 3 + p) * N + col] = split_part(v, p);
             }
         } else {
-            out[i] = act[i] > 0.0f ? v : 0.0f;
+            r.out[i] = r.act[i] > 0.0f ? v : 0.0f;
         }
     }
 }
+static void conv_reduce_launch(const ReduceArgs *ra, int ng, int splits, int64_t MN, int N, hipStream_t s) {
+    ReducePair rp{};
+    rp.g[0] = ra[0];
+    rp.g[1] = ra[ng > 1 ? 1 : 0];
+    dim3 grid((unsigned)std::min<int64_t>(ceil_div(MN, 256), 4096), (unsigned)ng);
+    conv_reduce_kernel<<<grid, 256, 0, s>>>(rp, splits, MN, N);
+    launch_check("conv_reduce_kernel");
+}
 
-// out = conv (bias + relu), kk-split through the conv slab when the grid is small
-// xb / outb (x6 only): pre-split input planes / also write the output's planes
+// one forward layer's operands for one net
+struct FwdIO {
+    const float *x, *w, *bias;
+    float *out;
+    const uint16_t *wb, *xb;   // x6: weight planes, pre-split input planes
+    uint16_t *outb;            // x6: also write the output's planes
+    QWork *wk;                 // its workspace (conv slab)
+};
+
+// out = conv (bias + relu) for ng nets at once, kk-split through the conv slabs when the grid is small
 template <int CK, int CN, int KS, int PAD>
-static void conv_fwd(const float *x, const float *w, const float *bias, float *out, int64_t M, int HIN, int HOUT,
-                     QWork &wk, hipStream_t s, const uint16_t *wb, const uint16_t *xb = nullptr,
-                     uint16_t *outb = nullptr) {
-    ConvArgs a{};
-    a.x = x; a.w = w; a.bias = bias; a.M = (int)M; a.HIN = HIN; a.HOUT = HOUT; a.nkk = KS * KS;
-    a.xb = xb;
-    const int sp = conv_splits(M, a.nkk);
+static void conv_fwd(const FwdIO *io, int ng, int64_t M, int HIN, int HOUT, hipStream_t s) {
+    ConvArgs ga[2];
+    const uint16_t *wb[2];
+    const int sp = conv_splits(M * ng, KS * KS);
+    for (int g = 0; g < ng; ++g) {
+        ConvArgs a{};
+        a.x = io[g].x; a.w = io[g].w; a.bias = io[g].bias; a.M = (int)M; a.HIN = HIN; a.HOUT = HOUT;
+        a.nkk = KS * KS; a.xb = io[g].xb;
+        if (sp == 1) {
+            a.out = io[g].out;
+            a.outb = io[g].outb;
+        } else {
+            a.out = io[g].wk->cslab;
+            SNK_CHECK((int64_t)sp * M * CN <= io[g].wk->cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
+        }
+        ga[g] = a;
+        wb[g] = io[g].wb;
+    }
     if (sp == 1) {
-        a.out = out;
-        a.outb = outb;
-        conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_BIAS_RELU>(a, 1, s, wb);
+        conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_BIAS_RELU>(ga, ng, 1, s, wb);
         return;
     }
-    a.out = wk.cslab;
-    SNK_CHECK((int64_t)sp * M * CN <= wk.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
-    conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_SLAB>(a, sp, s, wb);
-    const int used = ceil_div(a.nkk, ceil_div(a.nkk, sp));
-    conv_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(M * CN, 256), 4096), 256, 0, s>>>(
-        wk.cslab, used, M * CN, CN, bias, nullptr, out, outb);
-    launch_check("conv_reduce_kernel");
+    conv_launch<CK, CN, KS, PAD, MODE_FWD, EPI_SLAB>(ga, ng, sp, s, wb);
+    const int used = ceil_div(KS * KS, ceil_div(KS * KS, sp));
+    ReduceArgs ra[2];
+    for (int g = 0; g < ng; ++g) ra[g] = ReduceArgs{io[g].wk->cslab, io[g].bias, nullptr, io[g].out, io[g].outb};
+    conv_reduce_launch(ra, ng, used, M * CN, CN, s);
 }
 
 // ---------------------------------------------------------------- conv1 (VALU)
@@ -371,10 +415,24 @@ static void conv_fwd(const float *x, const float *w, const float *bias, float *o
 // reads; one thread per output position writes its 16 channels as 4 float4.
 // yb (optional): the output also as bf16 split planes [S*bs*bs][3][16] (x6 conv2 input);
 // y may then be null. NS samples per workgroup (fewer for small batches: more CUs busy).
+// Two nets per launch (grid.y = group) as for the conv_* kernels.
+struct Conv1Args {
+    BoardSrc src;
+    const float *w, *b;
+    float *y;
+    uint16_t *yb;
+};
+struct Conv1Pair {
+    Conv1Args g[2];
+};
 template <int C>
-__global__ __launch_bounds__(256) void conv1_fwd_kernel(BoardSrc src, const float *__restrict__ w,
-                                                        const float *__restrict__ b, float *__restrict__ y,
-                                                        uint16_t *__restrict__ yb, int64_t S, int bs, int NS) {
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S, int bs, int NS) {
+    const Conv1Args &ca = cp.g[blockIdx.y];
+    const BoardSrc &src = ca.src;
+    const float *__restrict__ w = ca.w;
+    const float *__restrict__ b = ca.b;
+    float *__restrict__ y = ca.y;
+    uint16_t *__restrict__ yb = ca.yb;
     extern __shared__ float sm[];
     float *sw = sm;                       // [9*C*16 + 16]
     float *sx = sm + 9 * C * 16 + 16;     // [NS][C][(bs+2)^2]
@@ -639,40 +697,81 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
 }
 
 // ---------------------------------------------------------------- forward
-void qnet_forward(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
-                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only, const uint16_t *wtb) {
+// conv1 .. Dense1 (layers lo..hi) of ng nets over S samples each, one launch per layer
+static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi) {
     const int bs = L.bs, nc = L.ncell;
-    if (only < 0 || only == 0) {
-        const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S / 256));
-        const int grid = ceil_div(S, ns);
+    if (lo <= 0 && hi >= 0) {
+        const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S * ng / 256));
+        const dim3 grid((unsigned)ceil_div(S, ns), (unsigned)ng);
         const size_t lds = (size_t)(9 * L.C * 16 + 16 + ns * L.C * (bs + 2) * (bs + 2)) * sizeof(float);
-        // x6: a1 also (acting: only) as bf16 planes for conv2
-        float *y = (wtb && !w.has_train) ? nullptr : w.a1;
-        uint16_t *yb = wtb ? w.a1b : nullptr;
+        Conv1Pair cp{};
+        for (int g = 0; g < 2; ++g) {
+            const FwdNet &n = net[g < ng ? g : 0];
+            // x6: a1 also (acting: only) as bf16 planes for conv2
+            cp.g[g] = Conv1Args{n.src, n.th + L.off_w1, n.th + L.off_b1, (n.wtb && !n.w->has_train) ? nullptr : n.w->a1,
+                                n.wtb ? n.w->a1b : nullptr};
+        }
         if (L.C == 1)
-            conv1_fwd_kernel<1><<<grid, 256, lds, s>>>(src, th + L.off_w1, th + L.off_b1, y, yb, S, bs, ns);
+            conv1_fwd_kernel<1><<<grid, 256, lds, s>>>(cp, S, bs, ns);
         else
-            conv1_fwd_kernel<2><<<grid, 256, lds, s>>>(src, th + L.off_w1, th + L.off_b1, y, yb, S, bs, ns);
+            conv1_fwd_kernel<2><<<grid, 256, lds, s>>>(cp, S, bs, ns);
         launch_check("conv1_fwd_kernel");
     }
-    if (only < 0 || only == 1)   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
+    FwdIO io[2];
+    if (lo <= 1 && hi >= 1) {   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
         // x6: a2 also (acting: only) as bf16 planes for conv3; training keeps fp32 a2 for the backward
-        conv_fwd<16, 32, 3, 1>(w.a1, wt + L.off_t2, th + L.off_b2, (wtb && !w.has_train) ? nullptr : w.a2, S * nc,
-                               bs, bs, w, s, wtb ? wtb + 3 * L.off_t2 : nullptr, wtb ? w.a1b : nullptr,
-                               wtb ? w.a2b : nullptr);
-    if (only < 0 || only == 2)   // conv3: M = S*Wo^2, K = 36 offsets x 32, N = 64
-        conv_fwd<32, 64, 6, 0>(w.a2, wt + L.off_t3, th + L.off_b3, w.a3, S * L.Wo * L.Wo, bs, L.Wo, w, s,
-                               wtb ? wtb + 3 * L.off_t3 : nullptr, wtb ? w.a2b : nullptr);
+        for (int g = 0; g < ng; ++g) {
+            const FwdNet &n = net[g];
+            io[g] = FwdIO{n.w->a1, n.wt + L.off_t2, n.th + L.off_b2, (n.wtb && !n.w->has_train) ? nullptr : n.w->a2,
+                          n.wtb ? n.wtb + 3 * L.off_t2 : nullptr, n.wtb ? n.w->a1b : nullptr,
+                          n.wtb ? n.w->a2b : nullptr, n.w};
+        }
+        conv_fwd<16, 32, 3, 1>(io, ng, S * nc, bs, bs, s);
+    }
+    if (lo <= 2 && hi >= 2) {   // conv3: M = S*Wo^2, K = 36 offsets x 32, N = 64
+        for (int g = 0; g < ng; ++g) {
+            const FwdNet &n = net[g];
+            io[g] = FwdIO{n.w->a2, n.wt + L.off_t3, n.th + L.off_b3, n.w->a3, n.wtb ? n.wtb + 3 * L.off_t3 : nullptr,
+                          n.wtb ? n.w->a2b : nullptr, nullptr, n.w};
+        }
+        conv_fwd<32, 64, 6, 0>(io, ng, S * L.Wo * L.Wo, bs, L.Wo, s);
+    }
+    if (lo <= 3 && hi >= 3) {   // Dense1 (split over the Wo^2 positions into partial slabs; bias + relu in the head)
+        int kc;
+        const int ks = d1_split(L, S, kc);
+        ConvArgs ga[2];
+        const uint16_t *wb[2];
+        for (int g = 0; g < ng; ++g) {
+            const FwdNet &n = net[g];
+            ConvArgs a{};
+            a.x = n.w->a3; a.w = n.wt + L.off_td; a.out = n.w->slab; a.M = (int)S; a.HIN = L.Wo; a.HOUT = 1;
+            a.nkk = L.Wo * L.Wo;
+            ga[g] = a;
+            wb[g] = n.wtb ? n.wtb + 3 * L.off_td : nullptr;
+        }
+        conv_launch<64, 64, 0, 0, MODE_DENSE, EPI_SLAB>(ga, ng, ks, s, wb);
+    }
+}
+
+void qnet_forward(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
+                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only, const uint16_t *wtb) {
+    const FwdNet net{th, wt, wtb, src, &w};
+    if (only < 0)
+        forward_layers(L, &net, 1, S, s, 0, 3);
+    else if (only < 4)
+        forward_layers(L, &net, 1, S, s, only, only);
+    if (only >= 0 && only != 4) return;
+    qnet_head(L, th, S, w, mode, ha, s);
+}
+
+void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s) {
+    forward_layers(L, net, 2, S, s, 0, 3);
+}
+
+void qnet_head(const QLayout &L, const float *th, int64_t S, QWork &w, HeadMode mode, const HeadArgs &ha,
+               hipStream_t s) {
     int kc;
     const int ks = d1_split(L, S, kc);
-    // Dense1 (split over the Wo^2 positions into partial slabs; bias + relu in the head)
-    if (only < 0 || only == 3) {
-        ConvArgs a{};
-        a.x = w.a3; a.w = wt + L.off_td; a.out = w.slab; a.M = (int)S; a.HIN = L.Wo; a.HOUT = 1;
-        a.nkk = L.Wo * L.Wo;
-        conv_launch<64, 64, 0, 0, MODE_DENSE, EPI_SLAB>(a, ks, s, wtb ? wtb + 3 * L.off_td : nullptr);
-    }
-    if (only >= 0 && only != 4) return;
     const int grid = ceil_div(S, 4);
     switch (mode) {
         case HEAD_Q: head_kernel<HEAD_Q><<<grid, 256, 0, s>>>(w.slab, ks, S, th, L, w.h1, w.q, ha); break;
@@ -742,9 +841,8 @@ static void backward_data_chain(const QLayout &L, const float *th, int64_t S, QW
             SNK_CHECK((int64_t)sp * S * nc * 32 <= w.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
             conv_launch<64, 32, 6, 0, MODE_DX, EPI_SLAB>(a, sp, s);
             const int used = ceil_div(36, ceil_div(36, sp));
-            conv_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(S * nc * 32, 256), 4096), 256, 0, s>>>(
-                w.cslab, used, S * nc * 32, 32, nullptr, w.a2, w.dz2);
-            launch_check("conv_reduce_kernel");
+            const ReduceArgs ra{w.cslab, nullptr, w.a2, w.dz2, nullptr};
+            conv_reduce_launch(&ra, 1, used, S * nc * 32, 32, s);
         }
     }
     gemm<1>(AConvDx<32, 3, 1>{w.dz2, bs, bs, FastDiv(nc), FastDiv(bs)}, BConvT<16, 32>{th + L.off_w2, 288},
@@ -819,9 +917,8 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             SNK_CHECK((int64_t)sp * S * nc * 32 <= w.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
             conv_launch<64, 32, 6, 0, MODE_DX, EPI_SLAB>(a, sp, s);
             const int used = ceil_div(36, ceil_div(36, sp));
-            conv_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(S * nc * 32, 256), 4096), 256, 0, s>>>(
-                w.cslab, used, S * nc * 32, 32, nullptr, w.a2, w.dz2);
-            launch_check("conv_reduce_kernel");
+            const ReduceArgs ra{w.cslab, nullptr, w.a2, w.dz2, nullptr};
+            conv_reduce_launch(&ra, 1, used, S * nc * 32, 32, s);
         }
     }
     {

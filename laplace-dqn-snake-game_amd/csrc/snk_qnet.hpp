@@ -104,6 +104,18 @@ struct HeadArgs {
 // forward: q[S][3] into w.q (and w.h1); mode-specific epilogue
 // only = -1: the whole chain; 0..4: just conv1 / conv2 / conv3 / dense1 / head
 // (inputs from a previous full forward; used for per-layer timing)
+// one net's forward operands
+struct FwdNet {
+    const float *th, *wt;
+    const uint16_t *wtb;
+    BoardSrc src;
+    QWork *w;
+};
+// conv1 .. Dense1 of two independent nets over S samples each, both in every launch (grid z/y = net)
+void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s);
+// the head (Dense1 bias + relu, Dense2, mode epilogue) after the layers
+void qnet_head(const QLayout &L, const float *theta, int64_t S, QWork &w, HeadMode mode, const HeadArgs &ha,
+               hipStream_t s);
 // wtb (optional): bf16 split planes of the image -> conv2/conv3/Dense1 on the x6 kernels
 void qnet_forward(const QLayout &L, const float *theta, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
                   HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1, const uint16_t *wtb = nullptr);
