@@ -9,6 +9,7 @@
 // weight-gradient loaders; RMSProp (Optimisers.jl, utils.jl:429,466) is
 // element-wise over the packed parameter vector.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "snk_conv_x6.hpp"
@@ -255,12 +256,15 @@ struct GemmPlan {
 static GemmPlan plan_gemm(int64_t M, int N, int NT, int64_t K, bool allow_z) {
     const int64_t tiles = ceil_div(M, 32) * ceil_div(N, NT * 32);
     // these GEMMs (the B = 64 backward) are latency-bound: many short waves
-    const int64_t target = 4096;
+    // env overrides for tuning: SNK_GEMM_WAVES (4096), SNK_GEMM_MINK (32); measured flat from 4096/32
+    // to 16384/8 on the B = 64 update
+    static const int64_t target = getenv("SNK_GEMM_WAVES") ? atoll(getenv("SNK_GEMM_WAVES")) : 4096;
+    static const int64_t mink = getenv("SNK_GEMM_MINK") ? atoll(getenv("SNK_GEMM_MINK")) : 32;
     int kw = 1;
-    while (kw < 8 && tiles * kw * 2 <= target && K / (kw * 2) >= 32) kw *= 2;
+    while (kw < 8 && tiles * kw * 2 <= target && K / (kw * 2) >= mink) kw *= 2;
     int z = 1;
     if (allow_z)
-        while (z < 64 && tiles * kw * z * 2 <= target && K / ((int64_t)kw * z * 2) >= 32) z *= 2;
+        while (z < 64 && tiles * kw * z * 2 <= target && K / ((int64_t)kw * z * 2) >= mink) z *= 2;
     int64_t chunk = ceil_div(K, z);
     chunk = (chunk + 7) & ~int64_t(7);
     return GemmPlan{kw, (int)ceil_div(K, chunk), (int)chunk};
@@ -953,18 +957,8 @@ struct UpdArgs {
 
 // index of packed parameter i in the forward weight image, or -1; x6 = its
 // plane-0 index in the bf16 split image (planes CK*CN apart)
-__device__ __forceinline__ int64_t image_index(const QLayout &L, int64_t i, int64_t &x6, int &pstride) {
-    int64_t u, base;
-    int CK, CN;
-    if (i >= L.off_w2 && i < L.off_b2) {
-        u = i - L.off_w2; base = L.off_t2; CK = 16; CN = 32;
-    } else if (i >= L.off_w3 && i < L.off_b3) {
-        u = i - L.off_w3; base = L.off_t3; CK = 32; CN = 64;
-    } else if (i >= L.off_d1w && i < L.off_d1b) {
-        u = i - L.off_d1w; base = L.off_td; CK = 64; CN = 64;
-    } else {
-        return -1;
-    }
+template <int CK, int CN>
+__device__ __forceinline__ int64_t image_index_of(int64_t u, int64_t base, int64_t &x6, int &pstride) {
     const int64_t kk = u / (CK * CN);
     const int r = (int)(u - kk * CK * CN);
     const int c = r / CN, n = r - c * CN;
@@ -972,70 +966,97 @@ __device__ __forceinline__ int64_t image_index(const QLayout &L, int64_t i, int6
     pstride = CK * CN;
     return base + kk * CK * CN + (int64_t)n * CK + c;
 }
+__device__ __forceinline__ int64_t image_index(const QLayout &L, int64_t i, int64_t &x6, int &pstride) {
+    if (i >= L.off_w2 && i < L.off_b2) return image_index_of<16, 32>(i - L.off_w2, L.off_t2, x6, pstride);
+    if (i >= L.off_w3 && i < L.off_b3) return image_index_of<32, 64>(i - L.off_w3, L.off_t3, x6, pstride);
+    if (i >= L.off_d1w && i < L.off_d1b) return image_index_of<64, 64>(i - L.off_d1w, L.off_td, x6, pstride);
+    return -1;
+}
 
+// one parameter: optional target copy, images, RMSProp (rmsprop_kernel order)
+__device__ __forceinline__ void apply_one(const UpdArgs &a, const QLayout &L, int64_t i, float g, bool due,
+                                          float omr) {
+    const float qd = a.u.rho * a.u.acc[i] + omr * (g * g);
+    a.u.acc[i] = qd;
+    const float th = a.u.theta[i] - (g * a.u.lr) / (__builtin_sqrtf(qd) + a.u.eps);
+    a.u.theta[i] = th;
+    int64_t x6 = 0;
+    int ps = 0;
+    const int64_t t = image_index(L, i, x6, ps);
+    if (t >= 0) {
+        a.u.wt[t] = th;
+        if (a.u.wtb)
+            for (int p = 0; p < 3; ++p) a.u.wtb[x6 + p * ps] = split_part(th, p);
+    }
+    if (due) {
+        a.u.theta_t[i] = th;
+        if (t >= 0) {
+            a.u.wt_t[t] = th;
+            if (a.u.wtb_t)
+                for (int p = 0; p < 3; ++p) a.u.wtb_t[x6 + p * ps] = split_part(th, p);
+        }
+    }
+}
+
+// grid-stride over [0, off_d2w); the LAST block owns Dense2 (195 params): it
+// stages dq and h1 through LDS and reduces over the batch (d2_grad_kernel's order)
 __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
     const QLayout &L = a.L;
     const bool due = a.apply && a.u.counter && (*a.u.counter % a.u.rate) == 0;   // utils.jl:469-472
     const float omr = 1.0f - a.u.rho;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L.P; i += (int64_t)gridDim.x * blockDim.x) {
-        float g;
+    if (blockIdx.x == gridDim.x - 1) {
+        const int t = threadIdx.x;
+        float g = 0.0f;
+        const int64_t i = L.off_d2w + t;
         if (a.finish) {
+            __shared__ float sdq[64 * 3], sh[64 * 64];
+            const int ac = t < 192 ? t >> 6 : t - 192, o = t & 63;
+            for (int64_t s0 = 0; s0 < a.g.S; s0 += 64) {
+                const int n = (int)min((int64_t)64, a.g.S - s0);
+                __syncthreads();
+                for (int e = t; e < n * 64; e += 256) sh[e] = a.g.h1[s0 * 64 + e];
+                if (t < n * 3) sdq[t] = a.g.dq[s0 * 3 + t];
+                __syncthreads();
+                if (t < 192)
+                    for (int k = 0; k < n; ++k) g = __builtin_fmaf(sdq[k * 3 + ac], sh[k * 64 + o], g);
+                else if (t < 195)
+                    for (int k = 0; k < n; ++k) g += sdq[k * 3 + ac];
+            }
+            if (t < 195) a.grad[i] = g;
+        } else if (t < 195) {
             g = a.grad[i];
+        }
+        if (a.apply && t < 195) apply_one(a, L, i, g, due, omr);
+        return;
+    }
+    const int64_t nthreads = (int64_t)(gridDim.x - 1) * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L.off_d2w; i += nthreads) {
+        float g = a.grad[i];
+        if (a.finish) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int64_t j = i - a.g.off[k];
                 if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
-                    float v = 0.0f;   // slab_reduce order
-                    for (int z = 0; z < a.g.z[k]; ++z) v += a.g.slab[k][(int64_t)z * a.g.n[k] + j];
+                    // slab_reduce order; the loads of 8 slabs go out together
+                    const float *sl = a.g.slab[k] + j;
+                    const int64_t n = a.g.n[k];
+                    const int zc = a.g.z[k];
+                    float v = 0.0f;
+                    int z = 0;
+                    for (; z + 8 <= zc; z += 8) {
+                        float x[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) x[u] = sl[(int64_t)(z + u) * n];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) v += x[u];
+                    }
+                    for (; z < zc; ++z) v += sl[(int64_t)z * n];
                     g = v;
                 }
             }
-            if (i >= L.off_d2w) {   // d2_grad order
-                const int t = (int)(i - L.off_d2w);
-                float acc = 0.0f;
-                // same sequential order as d2_grad_kernel; loads batched 16 deep (they do not depend on acc)
-                const int ac = t < 192 ? t >> 6 : t - 192, o = t & 63;
-                int64_t s = 0;
-                for (; s + 16 <= a.g.S; s += 16) {
-                    float dv[16], hv[16];
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        dv[u] = a.g.dq[(s + u) * 3 + ac];
-                        hv[u] = t < 192 ? a.g.h1[(s + u) * 64 + o] : 1.0f;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) acc = t < 192 ? __builtin_fmaf(dv[u], hv[u], acc) : acc + dv[u];
-                }
-                for (; s < a.g.S; ++s)
-                    acc = t < 192 ? __builtin_fmaf(a.g.dq[s * 3 + ac], a.g.h1[s * 64 + o], acc) : acc + a.g.dq[s * 3 + ac];
-                g = acc;
-            }
             a.grad[i] = g;
-        } else {
-            g = a.grad[i];
         }
-        if (!a.apply) continue;
-        // Optimisers.jl RMSProp (rmsprop_kernel order)
-        const float qd = a.u.rho * a.u.acc[i] + omr * (g * g);
-        a.u.acc[i] = qd;
-        const float th = a.u.theta[i] - (g * a.u.lr) / (__builtin_sqrtf(qd) + a.u.eps);
-        a.u.theta[i] = th;
-        int64_t x6 = 0;
-        int ps = 0;
-        const int64_t t = image_index(L, i, x6, ps);
-        if (t >= 0) {
-            a.u.wt[t] = th;
-            if (a.u.wtb)
-                for (int p = 0; p < 3; ++p) a.u.wtb[x6 + p * ps] = split_part(th, p);
-        }
-        if (due) {
-            a.u.theta_t[i] = th;
-            if (t >= 0) {
-                a.u.wt_t[t] = th;
-                if (a.u.wtb_t)
-                    for (int p = 0; p < 3; ++p) a.u.wtb_t[x6 + p * ps] = split_part(th, p);
-            }
-        }
+        if (a.apply) apply_one(a, L, i, g, due, omr);
     }
 }
 
@@ -1050,7 +1071,7 @@ void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad,
     a.apply = apply != nullptr;
     if (!a.finish && !a.apply) return;
     if (a.apply && !a.u.counter) a.u.rate = 1;
-    grad_update_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.P, 256), 2048), 256, 0, s>>>(a);
+    grad_update_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.off_d2w, 256), 2048) + 1, 256, 0, s>>>(a);
     launch_check("grad_update_kernel");
 }
 

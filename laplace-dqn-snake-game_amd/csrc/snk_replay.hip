@@ -85,6 +85,30 @@ __global__ __launch_bounds__(256) void replay_sample_kernel(const int64_t *__res
     }
 }
 
+// The same draw for B <= 64 in one wave: lane n holds candidate t_n; the serial
+// pass broadcasts t_n and asks all earlier lanes at once (ballot) whether it
+// was already chosen. Same output as the LDS-set version.
+__global__ __launch_bounds__(64) void replay_sample_wave_kernel(const int64_t *__restrict__ count, int64_t cap,
+                                                                int32_t batch, uint64_t seed, uint64_t draw,
+                                                                const int64_t *__restrict__ draw_dev,
+                                                                int64_t *__restrict__ out, int32_t *__restrict__ b_out,
+                                                                int64_t pending) {
+    const int lane = threadIdx.x;
+    if (draw_dev) draw = (uint64_t)*draw_dev;
+    const int64_t len = min(*count + pending, cap);
+    const int B = (int)min((int64_t)batch, len);
+    const int64_t t = lane < B ? (int64_t)__umul64hi(rng_hash(seed, draw, (uint64_t)lane), (uint64_t)(len - B + lane + 1))
+                               : -1;
+    int64_t v = -2;
+    for (int n = 0; n < B; ++n) {
+        const int64_t tn = __shfl(t, n, 64);
+        const bool hit = __ballot(lane < n && v == tn) != 0;
+        if (lane == n) v = hit ? len - B + n : tn;
+    }
+    if (lane < B) out[lane] = v;
+    if (lane == 0 && b_out) *b_out = B;
+}
+
 __global__ void replay_store_kernel(ReplayDev R, int64_t B, const int8_t *__restrict__ frames,
                                     const uint8_t *__restrict__ act, const float *__restrict__ rew,
                                     const uint8_t *__restrict__ done, const uint8_t *__restrict__ mask,
@@ -277,7 +301,10 @@ extern "C" int snk_replay_empty(snk_replay h) {
 namespace snk {
 void replay_launch_sample(const ReplayDev &d, int32_t batch, uint64_t seed, uint64_t draw,
                           const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s, int64_t pending) {
-    replay_sample_kernel<<<1, 256, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev, pending);
+    if (batch <= 64)
+        replay_sample_wave_kernel<<<1, 64, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev, pending);
+    else
+        replay_sample_kernel<<<1, 256, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev, pending);
     launch_check("replay_sample_kernel");
 }
 }  // namespace snk

@@ -146,3 +146,38 @@ def test_replay_ring_wrap_and_sample(snk):
     assert Bs == 64 and len(set(ids.tolist())) == 64 and ids.min() >= 0 and ids.max() < 100
     idx2, _ = snk.sample(rb, seed=7, draw=1)
     assert not np.array_equal(idx2.numpy(), ids)
+
+
+def _floyd_ref(seed, draw, n_len, batch):
+    """Floyd's algorithm with the device's counter RNG (snk_common.hpp rng_hash)."""
+    M = (1 << 64) - 1
+
+    def sm(x):
+        z = (x + 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    B = min(batch, n_len)
+    chosen, out = set(), []
+    for n in range(B):
+        h = sm(sm(seed ^ ((draw * 0xD1B54A32D192ED03) & M)) ^ n)
+        t = (h * (n_len - B + n + 1)) >> 64
+        v = n_len - B + n if t in chosen else t
+        chosen.add(v)
+        out.append(v)
+    return out
+
+
+@pytest.mark.parametrize("batch", [64, 17, 100])
+def test_sample_matches_floyd_reference(snk, batch):
+    """The wave-ballot sampler (batch <= 64) and the LDS-set sampler draw the
+    exact subset Floyd's algorithm gives for the same counter RNG."""
+    bs, C = 10, 2
+    rb = snk.ReplayBuffer(200, board_size=bs, n_frames=C, batch_size=batch)
+    for k in range(5):
+        fr = np.zeros((30, C + 1, bs * bs), np.int8)
+        snk.store_(rb, fr, np.zeros(30), np.zeros(30, np.float32), np.zeros(30), np.zeros((30, 3)), np.zeros(30))
+    for draw in range(4):
+        idx, B = snk.sample(rb, seed=11, draw=draw)
+        assert idx.numpy()[:B].tolist() == _floyd_ref(11, draw, 150, batch)
