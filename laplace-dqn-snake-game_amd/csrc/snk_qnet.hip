@@ -311,8 +311,34 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
     if constexpr (MODE != MODE_DX) {
         if (pr.wb[0]) {
             if constexpr (MODE == MODE_FWD && CK % 32 == 0 && EPI != EPI_RELU_MASK) {
-                if (a.xb) {   // pre-split input, 32-channel chunks: the 16x16x32 layout
-                    conv_x6m16_kernel<CK, CN, KS, PAD, EPI><<<grid, 256, 0, s>>>(pr);
+                if (a.xb) {   // pre-split input, 32-channel chunks: the 16x16x32 layouts
+                    if constexpr (CN == 64 && PAD == 0) {
+                        // whole input of the workgroup resident in LDS when it fits
+                        const int ho2 = a.HOUT * a.HOUT;
+                        const int nsmax = ceil_div(127, ho2) + 1;
+                        const size_t xs = (size_t)a.HIN * (a.HIN * (3 * CK + 16) + 80);   // conv_x6a A image
+                        const size_t lds = ((nsmax * xs + 7) & ~size_t(7)) * 2 + (3 * CN * (CK + 16) + 8) * 2;
+                        // measured slower than x6m16 (one workgroup per CU): opt-in
+                        static const bool x6a = getenv("SNK_X6A") != nullptr;
+                        if (lds <= 160 * 1024 && x6a) {
+                            static bool attr = false;
+                            if (!attr) {
+                                SNK_HIP(hipFuncSetAttribute((const void *)conv_x6a_kernel<CK, CN, KS, PAD, EPI>,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                                attr = true;
+                            }
+                            conv_x6a_kernel<CK, CN, KS, PAD, EPI><<<grid, 512, lds, s>>>(pr, nsmax);
+                            launch_check("conv_x6a_kernel");
+                            return;
+                        }
+                    }
+                    static const int rows = getenv("SNK_M16_ROWS") ? atoi(getenv("SNK_M16_ROWS")) : 128;
+                    if (rows == 256) {
+                        dim3 g2((unsigned)ceil_div(a.M, 256), grid.y, grid.z);
+                        conv_x6m16_kernel<CK, CN, KS, PAD, EPI, 8><<<g2, 512, 0, s>>>(pr);
+                    } else {
+                        conv_x6m16_kernel<CK, CN, KS, PAD, EPI, 4><<<grid, 256, 0, s>>>(pr);
+                    }
                     launch_check("conv_x6m16_kernel");
                     return;
                 }
