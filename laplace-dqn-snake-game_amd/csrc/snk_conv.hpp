@@ -52,8 +52,8 @@ struct ConvPair {
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, uint32_t s) { return (__umulhi(n, m) + n) >> s; }
 
 template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvPair pr) {
-    const ConvArgs &a = pr.g[blockIdx.z];
+__device__ __forceinline__ void conv_mfma_body(const ConvPair &pr, dim3 bid) {
+    const ConvArgs &a = pr.g[bid.z];
     constexpr int NT = CN / 32;
     constexpr int KB = CK / 8;
     constexpr int LDB = CK + 4;
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvPair pr) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int m = blockIdx.x * 128 + wave * 32 + r;
+    const int m = bid.x * 128 + wave * 32 + r;
     const bool ok = m < a.M;
     const int mm = ok ? m : 0;
     int s, i = 0, j = 0;
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvPair pr) {
         i = p - j * a.HOUT;
     }
     const float *xs = a.x + (int64_t)s * a.HIN * a.HIN * CK + 4 * h;
-    const int kk0 = blockIdx.y * a.kk_per_split;
+    const int kk0 = bid.y * a.kk_per_split;
     const int kk1 = min(a.nkk, kk0 + a.kk_per_split);
 
     f32x16 acc[NT];
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvPair pr) {
     }
 
     // epilogue: acc register g of lane l is C[(g&3) + 8*(g>>2) + 4*(l>>5)][l&31]
-    const int mrow0 = blockIdx.x * 128 + wave * 32;
+    const int mrow0 = bid.x * 128 + wave * 32;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         const int col = nt * 32 + r;
@@ -188,12 +188,17 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvPair pr) {
                 const float v = acc[nt][g] + b;
                 a.out[o] = v > 0.0f ? v : 0.0f;
             } else if (EPI == EPI_SLAB) {
-                a.out[(int64_t)blockIdx.y * a.M * CN + o] = acc[nt][g];
+                a.out[(int64_t)bid.y * a.M * CN + o] = acc[nt][g];
             } else {
                 a.out[o] = a.act[o] > 0.0f ? acc[nt][g] : 0.0f;
             }
         }
     }
+}
+
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvPair pr) {
+    conv_mfma_body<CK, CN, KS, PAD, MODE, EPI>(pr, blockIdx);
 }
 
 }  // namespace snk

@@ -129,9 +129,9 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
         const FwdNet nets[2] = {FwdNet{h->theta_t, h->wt_t, h->wtb_t, sn_src, &h->tgt},
                                 FwdNet{h->theta_q, h->wt_q, h->wtb_q, s_src, &h->trn}};
         qnet_forward_pair(h->L, nets, B, s);
-        qnet_head(h->L, h->theta_t, B, h->tgt, HEAD_TARGET, ta, s);
+        qnet_head_pair(h->L, h->theta_t, h->tgt, h->theta_q, h->trn, B, la, s);
     }
-    qnet_head(h->L, h->theta_q, B, h->trn, HEAD_LOSS, la, s);
+    if (o.fork && o.fork->on_side(FK_TARGET)) qnet_head(h->L, h->theta_q, B, h->trn, HEAD_LOSS, la, s);
     hipStream_t q1 = o.loss_mean ? F.fork(1, FK_LOSS) : s;
     if (o.loss_mean) loss_mean_launch(h->trn.loss, B, h->loss_dev, q1);
     BwdOpts bo;

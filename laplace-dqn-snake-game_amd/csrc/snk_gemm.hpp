@@ -24,14 +24,16 @@ __device__ __forceinline__ int acc_row(int g, int lane) { return (g & 3) + 8 * (
 // write partial slabs (EpSlab) when even that is too little parallelism.
 // The k loop moves 8 k (4 MFMA steps) per iteration with the next
 // iteration's operands loaded ahead (software pipeline).
+// body with an explicit block index (also run as one half of a paired launch)
 template <int NT, int KW, class AL, class BL, class EP>
-__global__ __launch_bounds__(64 * KW) void gemm_kernel(AL al, BL bl, EP ep, int M, int K, int kchunk) {
+__device__ __forceinline__ void gemm_body(const AL &al, const BL &bl, const EP &ep, int M, int K, int kchunk,
+                                          dim3 bid) {
     __shared__ float red[KW > 1 ? KW * NT * 16 * 64 : 1];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int m0 = blockIdx.x * 32;
+    const int m0 = bid.x * 32;
     const int r = lane & 31, h = lane >> 5;
-    const int n0 = blockIdx.y * (NT * 32);
-    const int kb = blockIdx.z * kchunk;
+    const int n0 = bid.y * (NT * 32);
+    const int kb = bid.z * kchunk;
     const int ke = min(K, kb + kchunk);
     const int sub = (((ke - kb) + KW - 1) / KW + 7) & ~7;
     const int wb = kb + wave * sub;
@@ -86,13 +88,18 @@ __global__ __launch_bounds__(64 * KW) void gemm_kernel(AL al, BL bl, EP ep, int 
 #pragma unroll
             for (int w = 1; w < KW; ++w) v += red[w * NT * 16 * 64 + e];
             const int nt = e >> 10, g = (e >> 6) & 15, ln = e & 63;
-            ep.store1(v, m0 + acc_row(g, ln), n0 + nt * 32 + (ln & 31), (int)blockIdx.z);
+            ep.store1(v, m0 + acc_row(g, ln), n0 + nt * 32 + (ln & 31), (int)bid.z);
         }
         return;
     }
     if (m0 >= M) return;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) ep.store(acc[nt], m0, n0 + nt * 32, lane, (int)blockIdx.z);
+    for (int nt = 0; nt < NT; ++nt) ep.store(acc[nt], m0, n0 + nt * 32, lane, (int)bid.z);
+}
+
+template <int NT, int KW, class AL, class BL, class EP>
+__global__ __launch_bounds__(64 * KW) void gemm_kernel(AL al, BL bl, EP ep, int M, int K, int kchunk) {
+    gemm_body<NT, KW>(al, bl, ep, M, K, kchunk, blockIdx);
 }
 
 // ---------------------------------------------------------------- epilogues

@@ -270,6 +270,66 @@ static GemmPlan plan_gemm(int64_t M, int N, int NT, int64_t K, bool allow_z) {
     return GemmPlan{kw, (int)ceil_div(K, chunk), (int)chunk};
 }
 
+// the same with the waves per tile fixed (paired launches need equal block sizes)
+static GemmPlan plan_gemm_kw(int64_t M, int N, int NT, int64_t K, bool allow_z, int kw) {
+    const int64_t tiles = ceil_div(M, 32) * ceil_div(N, NT * 32);
+    int z = 1;
+    if (allow_z)
+        while (z < 64 && tiles * kw * z * 2 <= 4096 && K / ((int64_t)kw * z * 2) >= 32) z *= 2;
+    int64_t chunk = ceil_div(K, z);
+    chunk = (chunk + 7) & ~int64_t(7);
+    return GemmPlan{kw, (int)ceil_div(K, chunk), (int)chunk};
+}
+
+// ---------------------------------------------------------------- paired launches
+// Two independent jobs in one launch: blocks [0, n1) run job 1, the rest job 2
+// (equal block sizes). The backward's weight and data gradients of a layer
+// only share inputs, so each such pair costs one launch and runs side by side.
+__device__ __forceinline__ dim3 unflatten(unsigned b, dim3 g) {
+    dim3 r;
+    r.x = b % g.x;
+    b /= g.x;
+    r.y = b % g.y;
+    r.z = b / g.y;
+    return r;
+}
+template <int NT, int KW, class AL, class BL, class EP>
+struct GemmJob {
+    AL al;
+    BL bl;
+    EP ep;
+    int M, K, kchunk;
+    dim3 grid;
+    __device__ void operator()(dim3 bid) const { gemm_body<NT, KW>(al, bl, ep, M, K, kchunk, bid); }
+};
+template <int NT, int KW, class AL, class BL, class EP>
+static GemmJob<NT, KW, AL, BL, EP> gemm_job(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int64_t K,
+                                           const GemmPlan &p) {
+    SNK_CHECK(p.kw == KW, SNK_ERR_INTERNAL, "paired GEMM plan has %d waves, job %d", p.kw, KW);
+    return GemmJob<NT, KW, AL, BL, EP>{al, bl, ep, (int)M, (int)K, p.kchunk,
+                                       dim3((unsigned)ceil_div(M, 32), (unsigned)ceil_div(N, NT * 32), (unsigned)p.z)};
+}
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
+struct ConvJob {
+    ConvPair pr;
+    dim3 grid;
+    __device__ void operator()(dim3 bid) const { conv_mfma_body<CK, CN, KS, PAD, MODE, EPI>(pr, bid); }
+};
+template <int NTH, class J1, class J2>
+__global__ __launch_bounds__(NTH) void pair_kernel(J1 j1, J2 j2) {
+    const unsigned n1 = j1.grid.x * j1.grid.y * j1.grid.z;
+    if (blockIdx.x < n1)
+        j1(unflatten(blockIdx.x, j1.grid));
+    else
+        j2(unflatten(blockIdx.x - n1, j2.grid));
+}
+template <int NTH, class J1, class J2>
+static void pair_launch(const J1 &j1, const J2 &j2, hipStream_t s) {
+    const unsigned n = j1.grid.x * j1.grid.y * j1.grid.z + j2.grid.x * j2.grid.y * j2.grid.z;
+    pair_kernel<NTH><<<n, NTH, 0, s>>>(j1, j2);
+    launch_check("pair_kernel");
+}
+
 template <int NT, class AL, class BL, class EP>
 static void gemm(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int64_t K, const GemmPlan &p,
                  hipStream_t s) {
@@ -293,8 +353,8 @@ static int conv_splits(int64_t M, int nkk) {
 // wb != nullptr: the bf16x6 split-precision kernel on the weight planes wb
 // ng groups (1 or 2) of the same geometry in one launch (grid.z = group);
 // wb[g] != nullptr: the bf16x6 split-precision kernels on those weight planes
-template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
-static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, const uint16_t *const *wb = nullptr) {
+// kernel arguments of ng (1 or 2) groups, kk split in `splits` (updated to the used count)
+static ConvPair make_conv_pair(const ConvArgs *ga, int ng, int &splits, const uint16_t *const *wb) {
     ConvPair pr{};
     const int kper = ceil_div(ga[0].nkk, splits);
     splits = ceil_div(ga[0].nkk, kper);
@@ -306,6 +366,12 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
         pr.g[g] = a;
         pr.wb[g] = wb ? wb[g < ng ? g : 0] : nullptr;
     }
+    return pr;
+}
+
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
+static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, const uint16_t *const *wb = nullptr) {
+    const ConvPair pr = make_conv_pair(ga, ng, splits, wb);
     const ConvArgs &a = pr.g[0];
     dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)splits, (unsigned)ng);
     if constexpr (MODE != MODE_DX) {
@@ -521,6 +587,152 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
     }
 }
 
+// ---------------------------------------------------------------- conv1 + conv2 fused (x6)
+// One workgroup = 128 conv2 output rows (positions) of at most 2 samples. It
+// computes conv1 for those samples straight into LDS as bf16 split planes
+// inside a zero border ((bs+2)^2 positions, 112-byte rows), then runs conv2's
+// 9 kernel offsets on 32x32x16 bf16 MFMA (6 products per offset, as
+// conv_x6_kernel) with every operand in LDS: no barrier inside the offset
+// loop, no a1 round trip through HBM/L2. Outputs as conv_fwd: a2 (fp32,
+// training) and/or its planes a2b; a1 (fp32) too when training needs it.
+// LDS: conv1 weights, boards (floats, bordered), a1 planes, all conv2 planes.
+struct Conv12Args {
+    BoardSrc src;
+    const float *w1, *b1;        // conv1 packed weights / bias
+    const uint16_t *wb2;         // conv2 weight planes [9][3][32][16]
+    const float *b2;
+    float *a1;                   // optional fp32 a1 [S*bs*bs][16]
+    float *a2;                   // optional fp32 a2 [S*bs*bs][32]
+    uint16_t *a2b;               // optional planes [S*bs*bs][3][32]
+};
+struct Conv12Pair {
+    Conv12Args g[2];
+};
+template <int C>
+__global__ __launch_bounds__(256) void conv12_x6_kernel(Conv12Pair cp, int64_t S, int bs, int nsmax) {
+    constexpr int A1ST = 56;   // bf16 per bordered position: 3 planes x 16 + 8 pad
+    const Conv12Args &ca = cp.g[blockIdx.z];
+    extern __shared__ __attribute__((aligned(16))) float sm12[];
+    const int bp = bs + 2, bp2 = bp * bp, nc = bs * bs;
+    float *sw = sm12;                                   // [9C*16 + 16]
+    float *sx = sw + ((9 * C * 16 + 16 + 3) & ~3);      // [nsmax][C][bp2]
+    uint16_t *A1 = reinterpret_cast<uint16_t *>(sx + ((nsmax * C * bp2 + 3) & ~3));   // [nsmax][bp2][A1ST]
+    uint16_t *Bw = A1 + ((nsmax * bp2 * A1ST + 7) & ~7);                              // [9][3][32][16]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t M = S * nc;
+    const int64_t m0 = (int64_t)blockIdx.x * 128;
+    const int64_t s_lo = m0 / nc;
+    const int64_t s_hi = (min(M, m0 + 128) - 1) / nc;
+    const int ns = (int)(s_hi - s_lo + 1);
+    // ---- stage: conv1 weights, zeroed board borders and a1 image, conv2 planes, boards
+    for (int e = tid; e < 9 * C * 16; e += 256) sw[e] = ca.w1[e];
+    if (tid < 16) sw[9 * C * 16 + tid] = ca.b1[tid];
+    for (int e = tid; e < nsmax * C * bp2; e += 256) sx[e] = 0.0f;
+    {
+        u32x4 *a = reinterpret_cast<u32x4 *>(A1);
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        for (int e = tid; e < nsmax * bp2 * A1ST / 8; e += 256) a[e] = z;
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(ca.wb2);
+        u32x4 *dst = reinterpret_cast<u32x4 *>(Bw);
+        for (int e = tid; e < 9 * 3 * 32 * 16 / 8; e += 256) dst[e] = src[e];
+    }
+    __syncthreads();
+    for (int e = tid; e < ns * C * nc; e += 256) {
+        const int sc = e / nc, cell = e - sc * nc;
+        const int sl = sc / C, c = sc - sl * C;
+        const int jj = cell / bs, ii = cell - jj * bs;
+        const int8_t *pl = ca.src.plane(s_lo + sl, c);
+        const float v = pl ? (float)pl[cell] : ca.src.fbase[((s_lo + sl) * C + c) * nc + cell];
+        sx[sc * bp2 + (ii + 1) + (jj + 1) * bp] = v;
+    }
+    __syncthreads();
+    // ---- conv1 for every position of the staged samples -> a1 planes (bordered)
+    for (int q = tid; q < ns * nc; q += 256) {
+        const int sl = q / nc, p = q - sl * nc;
+        const int j = p / bs, i = p - j * bs;
+        float acc[16];
+#pragma unroll
+        for (int co = 0; co < 16; ++co) acc[co] = sw[9 * C * 16 + co];
+#pragma unroll
+        for (int kk = 0; kk < 9; ++kk) {
+            const int du = kk % 3, dv = kk / 3;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const float v = sx[(sl * C + c) * bp2 + (i + du) + (j + dv) * bp];
+#pragma unroll
+                for (int co = 0; co < 16; ++co) acc[co] = __builtin_fmaf(v, sw[(kk * C + c) * 16 + co], acc[co]);
+            }
+        }
+#pragma unroll
+        for (int co = 0; co < 16; ++co) acc[co] = fmaxf(acc[co], 0.f);
+        if (ca.a1) {
+            float4 *o = reinterpret_cast<float4 *>(ca.a1 + ((s_lo + sl) * nc + p) * 16);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) o[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
+        }
+        u32x4 *o = reinterpret_cast<u32x4 *>(A1 + (sl * bp2 + (i + 1) + (j + 1) * bp) * A1ST);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const Split3 sp = split3(f32x4{acc[8 * half], acc[8 * half + 1], acc[8 * half + 2], acc[8 * half + 3]},
+                                     f32x4{acc[8 * half + 4], acc[8 * half + 5], acc[8 * half + 6], acc[8 * half + 7]});
+            o[0 + half] = sp.h;   // plane p at bf16 16p, channels 8*half..
+            o[2 + half] = sp.m;
+            o[4 + half] = sp.l;
+        }
+    }
+    __syncthreads();
+    // ---- conv2: wave = 32 rows x 32 columns, 9 offsets x 6 products
+    const int r = lane & 31, h = lane >> 5;
+    const int64_t m = m0 + wave * 32 + r;
+    const int64_t mm = m < M ? m : M - 1;
+    const int64_t sidx = mm / nc;
+    const int p = (int)(mm - sidx * nc);
+    const int j = p / bs, i = p - j * bs;
+    const int rowb = (int)(sidx - s_lo) * bp2 + i + j * bp;   // bordered position at offset (0, 0)
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+#pragma unroll
+    for (int kk = 0; kk < 9; ++kk) {
+        const int du = kk % 3, dv = kk / 3;
+        const uint16_t *pa = A1 + (rowb + du + dv * bp) * A1ST + 8 * h;
+        const uint16_t *pb = Bw + kk * 3 * 512 + r * 16 + 8 * h;
+        const bf16x8 ah = as_bf(*reinterpret_cast<const u32x4 *>(pa));
+        const bf16x8 am = as_bf(*reinterpret_cast<const u32x4 *>(pa + 16));
+        const bf16x8 al = as_bf(*reinterpret_cast<const u32x4 *>(pa + 32));
+        const bf16x8 bh = as_bf(*reinterpret_cast<const u32x4 *>(pb));
+        const bf16x8 bm = as_bf(*reinterpret_cast<const u32x4 *>(pb + 512));
+        const bf16x8 bl = as_bf(*reinterpret_cast<const u32x4 *>(pb + 1024));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+    }
+    const float b = ca.b2[r];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+        const int64_t row = m0 + wave * 32 + acc_row(g, lane);
+        if (row >= M) continue;
+        float v = acc[g] + b;
+        v = v > 0.0f ? v : 0.0f;
+        if (ca.a2) ca.a2[row * 32 + r] = v;
+        if (ca.a2b) {
+            uint16_t *pb2 = ca.a2b + row * 96 + r;
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) pb2[pl * 32] = split_part(v, pl);
+        }
+    }
+}
+
+static int conv12_nsmax(int bs) { return ceil_div(127, bs * bs) + 1; }
+static size_t conv12_lds(int C, int bs) {
+    const int bp2 = (bs + 2) * (bs + 2), ns = conv12_nsmax(bs);
+    return (((9 * C * 16 + 16 + 3) & ~3) + ((ns * C * bp2 + 3) & ~3)) * 4 + ((ns * bp2 * 56 + 7) & ~7) * 2 +
+           9 * 3 * 32 * 16 * 2;
+}
+
 // ---------------------------------------------------------------- heads
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -591,6 +803,62 @@ __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ sla
 #pragma unroll
         for (int k = 0; k < 3; ++k) ha.dq[s * 3 + k] = k == a ? (float)g : 0.0f;
     }
+}
+
+// HEAD_TARGET of t_net then HEAD_LOSS of q_net for the same sample in one wave
+// (the loss needs exactly that sample's target): the two head launches of an
+// update in one, same arithmetic as head_kernel<HEAD_TARGET> / <HEAD_LOSS>.
+struct HeadNet {
+    const float *slab, *theta;
+    float *h1, *q;
+};
+__global__ __launch_bounds__(256) void head_pair_kernel(HeadNet tn, HeadNet qn, int ks, int64_t S, QLayout L,
+                                                        HeadArgs ha) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= S) return;
+    const int64_t m = ha.idx ? ha.idx[s] : s;
+    // t_net(s'): TD target (utils.jl:448-451)
+    float h = tn.theta[L.off_d1b + lane];
+    for (int z = 0; z < ks; ++z) h += tn.slab[((int64_t)z * S + s) * 64 + lane];
+    h = h > 0.0f ? h : 0.0f;
+    tn.h1[s * 64 + lane] = h;
+    float q[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) q[a] = tn.theta[L.off_d2b + a] + wave_sum(tn.theta[L.off_d2w + a * 64 + lane] * h);
+    const uint8_t mk = ha.mask[m];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float v = ((mk >> a) & 1) ? -100.0f : q[a];
+        mx = v > mx ? v : mx;
+    }
+    const double tgt = (double)ha.rew[m] + ha.gamma * (double)mx * (double)(1 - (int)ha.done[m]);
+    if (lane == 0) {
+        tn.q[s * 3 + 0] = q[0];
+        tn.q[s * 3 + 1] = q[1];
+        tn.q[s * 3 + 2] = q[2];
+        ha.target[s] = tgt;
+    }
+    // q_net(s): Huber loss, dq and dz1 (utils.jl:453-464)
+    h = qn.theta[L.off_d1b + lane];
+    for (int z = 0; z < ks; ++z) h += qn.slab[((int64_t)z * S + s) * 64 + lane];
+    h = h > 0.0f ? h : 0.0f;
+    qn.h1[s * 64 + lane] = h;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) q[a] = qn.theta[L.off_d2b + a] + wave_sum(qn.theta[L.off_d2w + a * 64 + lane] * h);
+    const int a = ha.act_idx[m] % 3;
+    const double e = (double)q[a] - tgt;
+    const double ae = fabs(e);
+    const double g = (ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / (double)ha.B;
+    if (ha.dz1) ha.dz1[s * 64 + lane] = h > 0.0f ? (float)g * qn.theta[L.off_d2w + a * 64 + lane] : 0.0f;
+    if (lane != 0) return;
+    qn.q[s * 3 + 0] = q[0];
+    qn.q[s * 3 + 1] = q[1];
+    qn.q[s * 3 + 2] = q[2];
+    ha.loss[s] = ae < 1.0 ? 0.5 * e * e : ae - 0.5;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ha.dq[s * 3 + k] = k == a ? (float)g : 0.0f;
 }
 
 // backward of Dense2 + relu: dz1[s][o] = (h1 > 0) * sum_a dq[s][a] W2[a][o]
@@ -730,6 +998,34 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
 // conv1 .. Dense1 (layers lo..hi) of ng nets over S samples each, one launch per layer
 static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi) {
     const int bs = L.bs, nc = L.ncell;
+    // x6: conv1 + conv2 fused into one kernel (layer 0; layer 1 is then empty)
+    // measured slower than conv1 + conv2 (per-workgroup staging dominates): opt-in
+    static const bool use12 = getenv("SNK_CONV12") != nullptr;
+    const bool fused12 = net[0].wtb && use12 && conv12_lds(L.C, bs) <= 160 * 1024;
+    if (fused12 && lo <= 0 && hi >= 0) {
+        const size_t lds = conv12_lds(L.C, bs);
+        Conv12Pair cp{};
+        for (int g = 0; g < 2; ++g) {
+            const FwdNet &n = net[g < ng ? g : 0];
+            cp.g[g] = Conv12Args{n.src, n.th + L.off_w1, n.th + L.off_b1, n.wtb + 3 * L.off_t2, n.th + L.off_b2,
+                                 n.w->has_train ? n.w->a1 : nullptr, n.w->has_train ? n.w->a2 : nullptr, n.w->a2b};
+        }
+        const dim3 grid((unsigned)ceil_div(S * nc, 128), 1, (unsigned)ng);
+        static size_t attr = 0;
+        if (lds > attr) {
+            SNK_HIP(hipFuncSetAttribute((const void *)conv12_x6_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds));
+            SNK_HIP(hipFuncSetAttribute((const void *)conv12_x6_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds));
+            attr = lds;
+        }
+        if (L.C == 1)
+            conv12_x6_kernel<1><<<grid, 256, lds, s>>>(cp, S, bs, conv12_nsmax(bs));
+        else
+            conv12_x6_kernel<2><<<grid, 256, lds, s>>>(cp, S, bs, conv12_nsmax(bs));
+        launch_check("conv12_x6_kernel");
+    }
+    if (fused12) lo = std::max(lo, 2);
     if (lo <= 0 && hi >= 0) {
         const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S * ng / 256));
         const dim3 grid((unsigned)ceil_div(S, ns), (unsigned)ng);
@@ -798,6 +1094,15 @@ void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream
     forward_layers(L, net, 2, S, s, 0, 3);
 }
 
+void qnet_head_pair(const QLayout &L, const float *th_t, QWork &wt_, const float *th_q, QWork &wq, int64_t S,
+                    const HeadArgs &ha, hipStream_t s) {
+    int kc;
+    const int ks = d1_split(L, S, kc);
+    head_pair_kernel<<<ceil_div(S, 4), 256, 0, s>>>(HeadNet{wt_.slab, th_t, wt_.h1, wt_.q},
+                                                    HeadNet{wq.slab, th_q, wq.h1, wq.q}, ks, S, L, ha);
+    launch_check("head_pair_kernel");
+}
+
 void qnet_head(const QLayout &L, const float *th, int64_t S, QWork &w, HeadMode mode, const HeadArgs &ha,
                hipStream_t s) {
     int kc;
@@ -818,14 +1123,16 @@ void qnet_head(const QLayout &L, const float *th, int64_t S, QWork &w, HeadMode 
 struct BwdPlan {
     GemmPlan d1, c3, c2, c1, d1x, c2x;
 };
+// waves per tile fixed so that the layer pairs (d1 wgrad | d1x: 2, c3 wgrad |
+// conv3 data grad: 4 = the conv kernel's 256 threads, c2 wgrad | c2x: 8) launch together
 static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
     BwdPlan p;
-    p.d1 = plan_gemm(L.K1 + 1, 64, 2, S, true);
-    p.c3 = plan_gemm(1153, 64, 2, S * L.Wo * L.Wo, true);
-    p.c2 = plan_gemm(145, 32, 1, S * L.ncell, true);
+    p.d1 = plan_gemm_kw(L.K1 + 1, 64, 2, S, true, 2);
+    p.c3 = plan_gemm_kw(1153, 64, 2, S * L.Wo * L.Wo, true, 4);
+    p.c2 = plan_gemm_kw(145, 32, 1, S * L.ncell, true, 8);
     p.c1 = plan_gemm(9 * L.C + 1, 16, 1, S * L.ncell, true);
-    p.d1x = plan_gemm(S, L.K1, 2, 64, false);
-    p.c2x = plan_gemm(S * L.ncell, 16, 1, 288, false);
+    p.d1x = plan_gemm_kw(S, L.K1, 2, 64, false, 2);
+    p.c2x = plan_gemm_kw(S * L.ncell, 16, 1, 288, false, 8);
     return p;
 }
 static int64_t zslab(const GemmPlan &g, int64_t MN) { return g.z > 1 ? (int64_t)g.z * MN : 0; }
@@ -894,6 +1201,77 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         D->dq = w.dq;
         D->h1 = w.h1;
         D->S = S;
+    }
+    if (!F.on_side(FK_WGRAD)) {
+        // each layer's weight gradient and data gradient in ONE launch
+        auto dst = [&](int k, const GemmPlan &g, int64_t off, int64_t n, float *sl) -> float * {
+            if (g.z == 1) return grad + off;
+            if (D) {
+                D->slab[k] = sl; D->z[k] = g.z; D->off[k] = off; D->n[k] = n;
+            }
+            return sl;
+        };
+        auto fin = [&](const GemmPlan &g, int64_t off, int64_t n, float *sl) {
+            if (g.z > 1 && !D) reduce_into(sl, g.z, n, grad + off, s);
+        };
+        if (!o.dz1_ready) {
+            head_bwd_kernel<<<ceil_div(S, 4), 256, 0, s>>>(w.dq, w.h1, th, L, S, w.dz1);
+            launch_check("head_bwd_kernel");
+        }
+        if (!D) {
+            d2_grad_kernel<<<1, 256, 0, s>>>(w.dq, w.h1, S, L, grad);
+            launch_check("d2_grad_kernel");
+        }
+        // Dense1: dW (+ bias row) | dX with the relu mask of a3
+        const int64_t M1 = L.K1 + 1;
+        float *d1d = dst(0, p.d1, L.off_d1w, M1 * 64, slab + sr.d1);
+        pair_launch<128>(gemm_job<2, 2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, EpSlab{d1d, (int)M1, 64}, M1,
+                                        64, S, p.d1),
+                         gemm_job<2, 2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + L.off_d1w, 64, L.K1, 64},
+                                        EpReluMask{w.dz3, w.a3, (int)S, L.K1}, S, L.K1, 64, p.d1x),
+                         s);
+        fin(p.d1, L.off_d1w, M1 * 64, slab + sr.d1);
+        // conv3: dW over rows (s, pout) | dX onto the bs x bs x 32 input (relu mask on a2)
+        {
+            float *c3d = dst(1, p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
+            const auto wj = gemm_job<2, 4>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)},
+                                           BRows{w.dz3, S * no, 64}, EpSlab{c3d, 1153, 64}, 1153, 64, S * no, p.c3);
+            ConvArgs a{};
+            a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs;
+            a.nkk = 36;
+            int sp = conv_splits(S * nc, 36);
+            const dim3 cg((unsigned)ceil_div(S * nc, 128), 1, 1);
+            if (sp == 1) {
+                a.out = w.dz2;
+                ConvJob<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
+                pair_launch<256>(wj, cj, s);
+            } else {
+                a.out = w.cslab;
+                SNK_CHECK((int64_t)sp * S * nc * 32 <= w.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
+                ConvJob<64, 32, 6, 0, MODE_DX, EPI_SLAB> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
+                cj.grid.y = (unsigned)sp;
+                pair_launch<256>(wj, cj, s);
+                const ReduceArgs ra{w.cslab, nullptr, w.a2, w.dz2, nullptr};
+                conv_reduce_launch(&ra, 1, sp, S * nc * 32, 32, s);
+            }
+            fin(p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
+        }
+        // conv2: dW | dX (relu mask on a1)
+        float *c2d = dst(2, p.c2, L.off_w2, 145 * 32, slab + sr.c2);
+        pair_launch<512>(gemm_job<1, 8>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)},
+                                        BRows{w.dz2, S * nc, 32}, EpSlab{c2d, 145, 32}, 145, 32, S * nc, p.c2),
+                         gemm_job<1, 8>(AConvDx<32, 3, 1>{w.dz2, bs, bs, FastDiv(nc), FastDiv(bs)},
+                                        BConvT<16, 32>{th + L.off_w2, 288}, EpReluMask{w.dzc1, w.a1, (int)(S * nc), 16},
+                                        S * nc, 16, 288, p.c2x),
+                         s);
+        fin(p.c2, L.off_w2, 145 * 32, slab + sr.c2);
+        // conv1: weights only
+        const int64_t Mc1 = 9 * L.C + 1;
+        float *c1d = dst(3, p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
+        gemm<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
+                EpSlab{c1d, (int)Mc1, 16}, Mc1, 16, S * nc, p.c1, s);
+        fin(p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
+        return;
     }
     // a weight gradient: straight into grad, through slabs + reduce, or left
     // as slabs for grad_update_launch (section k of D)

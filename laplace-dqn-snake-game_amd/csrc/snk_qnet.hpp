@@ -113,6 +113,9 @@ struct FwdNet {
 };
 // conv1 .. Dense1 of two independent nets over S samples each, both in every launch (grid z/y = net)
 void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s);
+// TD-target head of t_net and loss head of q_net (HeadArgs as for HEAD_LOSS) in one launch
+void qnet_head_pair(const QLayout &L, const float *theta_t, QWork &wt, const float *theta_q, QWork &wq, int64_t S,
+                    const HeadArgs &ha, hipStream_t s);
 // the head (Dense1 bias + relu, Dense2, mode epilogue) after the layers
 void qnet_head(const QLayout &L, const float *theta, int64_t S, QWork &w, HeadMode mode, const HeadArgs &ha,
                hipStream_t s);
