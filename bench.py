@@ -28,6 +28,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+PEAK_BF16_TFLOPS = 2516.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak (2.5 PF, no sparsity)
+X6_PRODUCTS = 6            # bf16 MFMA products per fp32 product in the exact-split forward
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
 
 
@@ -207,7 +209,10 @@ def main():
                                f"{args.updates_per_iter} B=64 update(s) per step",
                    "n_envs_per_gpu": n, "board_size": bs, "n_frames": C, "replay_capacity": args.capacity,
                    "batch_size": 64, "epsilon": args.epsilon, "parallelism": f"dp{world}" if world > 1 else "none",
-                   "hipgraph": graph},
+                   "hipgraph": graph,
+                   "gemm_arithmetic": ("f32 operands split exactly into 3 bf16 parts, 6 bf16 MFMA products, "
+                                       "f32 accumulation (fp32 error class)" if os.environ.get("SNK_CONV", "") != "fp32"
+                                       else "native f32 MFMA")},
         "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
                         "food_faults": faults},
         "roofline": None,
@@ -222,10 +227,18 @@ def main():
         flop_conv3 = 2.0 * n * wo * wo * (36 * 32) * 64
         flop_total = 2.0 * n * (bs * bs * 16 * 9 * C + bs * bs * 32 * 144 + wo * wo * 64 * 1152 + wo * wo * 64 * 64 + 64 * 3)
         tf = flop_conv3 / (ms[2] * 1e-3) / 1e12
-        out["roofline"] = {"bound": "mfma", "kernel": "conv3 implicit GEMM (act forward, 32x32x2 f32 MFMA)",
-                           "achieved": tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_TFLOPS,
-                           "traffic": None, "avg_launch_ms": ms[2],
-                           "flop_per_launch": flop_conv3}
+        # the forward GEMMs run fp32 products as 6 exact bf16 split products on the
+        # bf16 MFMA (SNK_CONV=fp32: native f32 MFMA): the fp32-equivalent peak is
+        # the bf16 dense peak / 6
+        x6 = os.environ.get("SNK_CONV", "") != "fp32"
+        peak = PEAK_BF16_TFLOPS / X6_PRODUCTS if x6 else PEAK_FP32_TFLOPS
+        out["roofline"] = {"bound": "mfma",
+                           "kernel": "conv3 implicit GEMM, act forward (" +
+                                     ("bf16x6 split on v_mfma_f32_16x16x32_bf16" if x6 else "v_mfma_f32_32x32x2_f32") + ")",
+                           "achieved": tf, "peak": peak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / peak,
+                           "traffic": None, "avg_launch_ms": ms[2], "flop_per_launch": flop_conv3,
+                           "bf16_mfma_tflops_executed": tf * X6_PRODUCTS if x6 else None,
+                           "fp32_mfma_peak": PEAK_FP32_TFLOPS}
         out["act_forward_ms"] = {"conv1": ms[0], "conv2": ms[1], "conv3": ms[2], "dense1": ms[3], "head": ms[4],
                                  "total": float(ms.sum()),
                                  "tflops_total": flop_total / (ms.sum() * 1e-3) / 1e12}
@@ -240,6 +253,26 @@ def main():
         out["step_kernel"] = {"avg_launch_ms": sms.value, "bytes_per_env_step": step_bytes,
                               "achieved_GBs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS,
                               "env_steps_per_s": n / (sms.value * 1e-3)}
+        # configs[2]-scale step kernel (65,536 envs, 20x20, replay store fused): the HBM-bound case
+        try:
+            gl = snk.SnakeGame(20, C, n_envs=65536, autoreset=True)
+            rl = snk.ReplayBuffer(65536 * 4, board_size=20, n_frames=C, batch_size=64)
+            al = snk.DeviceArray(65536, np.uint8)
+            for t in range(20):
+                snk.synth_actions_dev(gl, 7 + t, al)
+                snk.step_indices_dev(gl, al.ptr, replay=rl)
+            snk.synth_actions_dev(gl, 99, al)
+            lms = _lib.f64(0)
+            _lib.call("snk_env_time_step", gl.handle, rl.handle, al.ptr, 50, ctypes.byref(lms))
+            lb = (C + 4) * 400 + 57
+            lg = 65536 * lb / (lms.value * 1e-3) / 1e9
+            out["step_kernel_large"] = {"config": "65536 envs, 20x20, store fused (configs[2] env scale)",
+                                        "avg_launch_ms": lms.value, "bytes_per_env_step": lb,
+                                        "achieved_GBs": lg, "frac_hbm": lg / PEAK_HBM_GBS,
+                                        "env_steps_per_s": 65536 / (lms.value * 1e-3)}
+            del gl, rl, al
+        except Exception as e:   # report, do not fail the headline line
+            out["step_kernel_large"] = {"error": str(e)}
     if rank == 0 and not args.no_dbuild:
         out.update(d_build(args, snk, tr))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
