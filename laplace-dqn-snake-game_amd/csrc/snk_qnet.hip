@@ -346,7 +346,9 @@ static void gemm(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int
 // ---------------------------------------------------------------- LDS-staged conv
 static int conv_splits(int64_t M, int nkk) {
     const int64_t wgs = ceil_div(M, 128);
-    if (wgs >= 512) return 1;
+    // offsets at or below this count run unsplit (no reduce launch); SNK_SPLIT_MIN_KK
+    static const int min_kk = getenv("SNK_SPLIT_MIN_KK") ? atoi(getenv("SNK_SPLIT_MIN_KK")) : 0;
+    if (wgs >= 512 || nkk <= min_kk) return 1;
     return (int)std::min<int64_t>(std::min(nkk, 16), ceil_div(512, wgs));
 }
 
@@ -517,6 +519,7 @@ struct Conv1Args {
     const float *w, *b;
     float *y;
     uint16_t *yb;
+    float *x0;   // optional: the input planes as floats [S][C][bs*bs] (training: conv1 weight gradient)
 };
 struct Conv1Pair {
     Conv1Args g[2];
@@ -546,6 +549,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
         const int8_t *pl = src.plane(s0 + sl, c);
         const float v = pl ? (float)pl[cell] : src.fbase[((s0 + sl) * C + c) * ncell + cell];
         sx[sc * plane + (ii + 1) + (jj + 1) * bp] = v;
+        if (ca.x0) ca.x0[s0 * C * ncell + i] = v;
     }
     __syncthreads();
     for (int q = threadIdx.x; q < ns * ncell; q += blockDim.x) {
@@ -934,7 +938,7 @@ __global__ void loss_mean_kernel(const double *__restrict__ loss, int64_t B, dou
 void qwork_free(QWork &w) {
     for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a2b, (void *)w.a1b, (void *)w.a3, (void *)w.slab, (void *)w.cslab,
                     (void *)w.h1, (void *)w.q,
-                    (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.target,
+                    (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.x0, (void *)w.target,
                     (void *)w.loss})
         dfree(p);
     w = QWork{};
@@ -989,6 +993,7 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
         w.dz3 = dalloc<float>((size_t)cap * L.K1);
         w.dz2 = dalloc<float>((size_t)cap * L.ncell * 32);
         w.dzc1 = dalloc<float>((size_t)cap * L.ncell * 16);
+        w.x0 = dalloc<float>((size_t)cap * L.ncell * L.C);
         w.target = dalloc<double>(cap);
         w.loss = dalloc<double>(cap);
     }
@@ -1025,7 +1030,10 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             conv12_x6_kernel<2><<<grid, 256, lds, s>>>(cp, S, bs, conv12_nsmax(bs));
         launch_check("conv12_x6_kernel");
     }
-    if (fused12) lo = std::max(lo, 2);
+    if (fused12) {
+        lo = std::max(lo, 2);
+        for (int g = 0; g < ng; ++g) net[g].w->x0_valid = 0;
+    }
     if (lo <= 0 && hi >= 0) {
         const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S * ng / 256));
         const dim3 grid((unsigned)ceil_div(S, ns), (unsigned)ng);
@@ -1035,13 +1043,14 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             const FwdNet &n = net[g < ng ? g : 0];
             // x6: a1 also (acting: only) as bf16 planes for conv2
             cp.g[g] = Conv1Args{n.src, n.th + L.off_w1, n.th + L.off_b1, (n.wtb && !n.w->has_train) ? nullptr : n.w->a1,
-                                n.wtb ? n.w->a1b : nullptr};
+                                n.wtb ? n.w->a1b : nullptr, n.w->has_train ? n.w->x0 : nullptr};
         }
         if (L.C == 1)
             conv1_fwd_kernel<1><<<grid, 256, lds, s>>>(cp, S, bs, ns);
         else
             conv1_fwd_kernel<2><<<grid, 256, lds, s>>>(cp, S, bs, ns);
         launch_check("conv1_fwd_kernel");
+        for (int g = 0; g < ng; ++g) net[g].w->x0_valid = net[g].w->has_train ? 1 : 0;
     }
     FwdIO io[2];
     if (lo <= 1 && hi >= 1) {   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
@@ -1268,7 +1277,14 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         // conv1: weights only
         const int64_t Mc1 = 9 * L.C + 1;
         float *c1d = dst(3, p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
-        gemm<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
+        BoardSrc xs = src;   // the forward's float copy of the input planes when it made one
+        if (w.x0_valid) {
+            xs = BoardSrc{};
+            xs.fbase = w.x0;
+            xs.C = L.C;
+            xs.ncell = nc;
+        }
+        gemm<1>(ABoardDw{xs, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
                 EpSlab{c1d, (int)Mc1, 16}, Mc1, 16, S * nc, p.c1, s);
         fin(p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
         return;

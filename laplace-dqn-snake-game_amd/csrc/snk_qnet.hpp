@@ -71,6 +71,8 @@ struct QWork {
     uint16_t *a1b = nullptr;  // x6 forward: a1 as bf16 planes [S*ncell][3][16]
     // training only
     float *dq = nullptr, *dz1 = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dzc1 = nullptr;
+    float *x0 = nullptr;      // input planes as floats, written by the training forward's conv1
+    int x0_valid = 0;         // set by the forward that wrote x0 (the unfused conv1 path)
     double *target = nullptr, *loss = nullptr;
     int has_train = 0;
 };
