@@ -81,6 +81,38 @@ class LaplaceD:
         call("snk_laplace_gram", self._h, C.byref(ms))
         return self._get(_lib.SNK_LAP_GRAM, (self.K, self.K), np.float64), ms.value
 
+    def eig(self, G: np.ndarray | None = None):
+        """Eigen-decomposition of the device Gram D'D: (lambda, V) with
+        lambda = S.^2/(K-1) in svd order (descending) and V the right singular
+        vectors of D (plot_traj.jl:10-16: U, S, V = svd(D))."""
+        if G is None:
+            G, _ = self.gram()
+        w, V = np.linalg.eigh(G)
+        order = np.argsort(w)[::-1]
+        w = np.clip(w[order], 0.0, None)
+        return w / (self.K - 1), V[:, order]
+
+    @staticmethod
+    def n_cols(lam: np.ndarray, frac: float = 0.99) -> int:
+        """plot_traj.jl:47-63 compute_n_cols: how many leading eigenvalues of
+        D'D/(K-1) (svd order) account for 99 % of their sum."""
+        lim = frac * float(np.sum(lam))
+        cum, n = 0.0, 0
+        for v in lam:
+            cum += float(v)
+            n += 1
+            if cum >= lim:
+                break
+        return n
+
+    def trajectory_2d(self, G: np.ndarray | None = None) -> np.ndarray:
+        """plot_traj.jl:65-67 Y = U[:, 1:2]' * D: the K snapshots projected on
+        the two leading directions, [2, K]. With D = U S V', U[:, i]' D = S_i V[:, i]',
+        so it follows from the Gram alone."""
+        lam, V = self.eig(G)
+        S = np.sqrt(lam[:2] * (self.K - 1))
+        return S[:, None] * V[:, :2].T
+
     def spectrum(self, G: np.ndarray | None = None, floor: float = 1e-7) -> np.ndarray:
         """plot_traj.jl:10-19: lambda = S.^2/(K-1) of svd(D), the eigenvalues of
         D'D/(K-1), keeping those > 1e-7 (host analysis of the device Gram,

@@ -138,3 +138,27 @@ def test_jacobian_gram_matches_device_jacobian(snk):
     J = snk.jacobian(m, rb, n).astype(np.float64)
     Gref = J @ J.T
     assert _gram_close(G.astype(np.float64), Gref) <= 2e-6
+
+
+def test_spectrum_ncols_and_trajectory_match_svd(snk):
+    """plot_traj.jl's analysis from the device Gram equals numpy's svd of the
+    (oracle-)centred D: eigenvalues S^2/(K-1), compute_n_cols, and the 2-D
+    trajectory U[:, 1:2]' D (up to the sign of each singular vector)."""
+    K, P = 60, 3000
+    rng = np.random.default_rng(7)
+    D0 = rng.standard_normal(P)[None, :] + np.cumsum(rng.standard_normal((K, P)) * 1e-2, axis=0)
+    lap = snk.LaplaceD(P, K)
+    for k in range(K):
+        lap.set_column(k, D0[k])
+    lap.fit_center()
+    Dc, _, _ = oracle.welford_center(D0)
+    U, S, Vt = np.linalg.svd(Dc.T, full_matrices=False)   # Julia's D is P x K
+    lam_ref = S ** 2 / (K - 1)
+    lam, _ = lap.eig()
+    assert np.allclose(lam[:10], lam_ref[:10], rtol=1e-5)
+    assert snk.LaplaceD.n_cols(lam) == snk.LaplaceD.n_cols(lam_ref)
+    Y = lap.trajectory_2d()
+    Yref = U[:, :2].T @ Dc.T
+    for i in range(2):
+        sgn = np.sign(np.dot(Y[i], Yref[i]))
+        assert np.allclose(sgn * Y[i], Yref[i], rtol=1e-4, atol=1e-6 * np.abs(Yref[i]).max())
