@@ -113,15 +113,21 @@ def d_build(args, snk, tr) -> dict:
     flop_gram = float(n) * (n + 1) * Kc                          # lower triangle incl. diagonal, 2 flop / MAC
     tf = flop_gram / (ms[2] * 1e-3) / 1e12
     P = tr.model.P
+    # syrk_kernel runs the fp32 products as 6 exact bf16 split products (SNK_SYRK=fp32: native f32 MFMA)
+    x6 = os.environ.get("SNK_SYRK", "") != "fp32"
+    speak = PEAK_BF16_TFLOPS / X6_PRODUCTS if x6 else PEAK_FP32_TFLOPS
     res = {"d_build_sec": wall,
-           "d_build": {"kind": "per-sample Jacobian Gram G = J J' (n x n, fp32 MFMA, fp64 accumulation)",
+           "d_build": {"kind": "per-sample Jacobian Gram G = J J' (n x n, fp32-accurate "
+                               + ("bf16x6 split MFMA" if x6 else "f32 MFMA") + ", fp64 accumulation)",
                        "n_samples": n, "n_params": P, "conv_columns": Kc,
                        "phase_ms": {"forward_and_data_grads": ms[0], "per_sample_conv_jacobians": ms[1],
                                     "conv_gram": ms[2], "dense_terms_and_mirror": ms[3]},
                        "naive_flop": 2.0 * n * n * P, "executed_gram_flop": flop_gram,
                        "roofline": {"bound": "mfma", "kernel": "syrk_kernel (conv-column Gram)", "achieved": tf,
-                                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": tf / PEAK_FP32_TFLOPS,
-                                    "avg_launch_ms": ms[2], "flop_per_launch": flop_gram, "traffic": None}}}
+                                    "peak": speak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / speak,
+                                    "avg_launch_ms": ms[2], "flop_per_launch": flop_gram, "traffic": None,
+                                    "bf16_mfma_tflops_executed": tf * X6_PRODUCTS if x6 else None,
+                                    "fp32_mfma_peak": PEAK_FP32_TFLOPS}}}
     del G
     K = args.d_snapshots
     if K > 1:

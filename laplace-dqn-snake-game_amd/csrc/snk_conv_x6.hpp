@@ -21,6 +21,8 @@
 // MFMA 32x32x16 bf16 operand map: lane l (r = l&31, h = l>>5) holds
 // A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7; C/D as the f32 form.
 #pragma once
+#include <type_traits>
+
 #include "snk_conv.hpp"
 
 namespace snk {
@@ -606,6 +608,205 @@ __global__ __launch_bounds__(512) void conv_x6a_kernel(ConvPair pr, int nsmax) {
             }
         }
     }
+}
+
+}  // namespace snk
+
+namespace snk {
+
+// conv3 (CK = 32 -> CN = 64, pad 0) of a large batch with the input of FOUR
+// samples resident in LDS: the 36 kernel offsets read A from LDS, so L2 moves
+// each sample's planes once plus one weight stream per four samples
+// (~0.6 GB per 4096-sample launch against the ~2.1 GB x6m16 re-reads).
+// Tile rows interleave the samples: row q of a workgroup is output position
+// p = q >> 2 of sample q & 3, so the 16 rows of an MFMA tile are 4 positions
+// x 4 samples. LDS image of A, in 16-byte slots (8 channels of one plane):
+//   slot(s, g, pl, j, i) = s*XS + g*GG + pl*PL + j*XW + i
+//   XW = HOUT + 8 (== HOUT mod 4: a row wrap advances the slot by 1 mod 4,
+//   like a step inside the row), PL = HIN*XW rounded to 4, GG = 3*PL,
+//   XS = 4*GG + 4 (samples 4 slots apart)
+// so the 16 lanes of every ds_read_b128 lane group land on 16 distinct slots
+// of a 256-byte bank row (bank simulation: 4.3 LDS cycles per read, 4 ideal).
+// B (the offset's three weight planes, [pl][n][c]) is double buffered with
+// an XOR swizzle of the 16-byte chunk by (n >> 2) & 3 instead of padding.
+// 8 waves: wave w owns columns 32*(w & 1) .. +31 and row tiles
+// (w >> 1) + 4k. The 6 part products accumulate in x6m16's order: the result
+// equals x6m16's bit for bit.
+__device__ __forceinline__ int x6s_bswz(int e) { return e ^ ((4 - ((e >> 4) & 3)) & 3); }
+
+template <int KS, int EPI>
+__global__ __launch_bounds__(512) void conv_x6s_kernel(ConvPair pr, int S) {
+    constexpr int CN = 64, NSG = 4, NB = 3 * CN * 32 / 8;   // 768 B chunks per offset
+    const ConvArgs &a = pr.g[blockIdx.z];
+    const u32x4 *__restrict__ wsrc = reinterpret_cast<const u32x4 *>(pr.wb[blockIdx.z]);
+    extern __shared__ __attribute__((aligned(16))) u32x4 x6s_lds[];
+    u32x4 *Bs = x6s_lds;            // [2][NB]
+    u32x4 *As = x6s_lds + 2 * NB;   // A image
+    const int hin = a.HIN, ho = a.HOUT, ho2 = ho * ho, hin2 = hin * hin;
+    const int XW = ho + 8, PL = (hin * XW + 3) & ~3, GG = 3 * PL, XS = 4 * GG + 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int s0 = blockIdx.x * NSG;
+    const int ns = min(NSG, S - s0);
+
+    // B register sets: set kk & 1 carries B(kk) from global to LDS
+    u32x4 bst[2][2];
+    constexpr int NKK = KS * KS;
+    auto b_load = [&](int kk, int set) {
+        const int kc = min(kk, NKK - 1);
+        bst[set][0] = wsrc[(int64_t)kc * NB + tid];
+        bst[set][1] = wsrc[(int64_t)kc * NB + 512 + (tid & 255)];
+    };
+    auto b_store = [&](int buf, int set) {
+        Bs[buf * NB + x6s_bswz(tid)] = bst[set][0];
+        if (tid < NB - 512) Bs[buf * NB + x6s_bswz(512 + tid)] = bst[set][1];
+    };
+    b_load(0, 0);
+    b_load(1, 1);
+    {   // stage the group's planes: global [s][pos][pl][g] -> As
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(a.xb) + (int64_t)s0 * hin2 * 12;
+        const int n16 = ns * hin2 * 12;
+        for (int e0 = 0; e0 < n16; e0 += 14 * 512) {
+            u32x4 v[14];   // branch-free (clamped) loads: one round trip for a 12 x 12 group
+#pragma unroll
+            for (int u = 0; u < 14; ++u) v[u] = src[min(e0 + u * 512 + tid, n16 - 1)];
+#pragma unroll
+            for (int u = 0; u < 14; ++u) {
+                const int e = e0 + u * 512 + tid;
+                if (e < n16) {
+                    const int pos = e / 12, c = e - pos * 12;
+                    const int sr = pos / hin2, qq = pos - sr * hin2;
+                    const int j = qq / hin, i = qq - j * hin;
+                    As[sr * XS + (c & 3) * GG + (c >> 2) * PL + j * XW + i] = v[u];
+                }
+            }
+        }
+    }
+    b_store(0, 0);
+    b_store(1, 1);
+
+    const int T = (NSG * ho2 + 15) / 16;
+    const int rg = wave >> 1, cg = wave & 1;
+    // tiles rg, rg+4, ... of this wave (wave-uniform)
+    const int nt = __builtin_amdgcn_readfirstlane(T > rg ? (T - rg + 3) / 4 : 0);
+    const int bslot = (cg * 32 + r) * 4 + (g ^ ((4 - ((r >> 2) & 3)) & 3));
+    __syncthreads();
+
+    // Pipeline: offset kk's MFMAs run on fragments read during offset kk-1.
+    // B(kk+1) sits in Bs[(kk+1)&1] (stored at kk-1, before its barrier);
+    // B(kk+2), loaded from global one offset earlier, goes into Bs[kk&1]
+    // (whose B(kk) every wave read before the last barrier) while B(kk+3)
+    // is in flight. Indices past the last offset clamp to it (redundant,
+    // harmless loads, reads and stores), so the loop body has no branches
+    // and the waitcnt counts stay exact. The tile count per wave is a
+    // template constant for the same reason.
+    auto run = [&](auto ntc) {
+        constexpr int NT = decltype(ntc)::value;
+        int abase[NT];
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+            const int q = 16 * (rg + 4 * k) + r;
+            const int p = min(q >> 2, ho2 - 1), sr = q & 3;
+            const int j = p / ho, i = p - j * ho;
+            abase[k] = sr * XS + g * GG + j * XW + i;
+        }
+        f32x4v acc[NT][2];
+#pragma unroll
+        for (int k = 0; k < NT; ++k)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) acc[k][ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        struct Frag {
+            u32x4 a[NT][3], b[2][3];
+        };
+        auto frag_read = [&](int kk, Frag &f) {
+            kk = min(kk, NKK - 1);
+            const int dv = kk / KS, du = kk - dv * KS;
+            const int off = dv * XW + du;
+            const u32x4 *pb = Bs + (kk & 1) * NB + bslot;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) f.b[ct][pl] = pb[ct * 64 + pl * 256];
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+                const u32x4 *pa = As + abase[k] + off;
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) f.a[k][pl] = pa[pl * PL];
+            }
+        };
+        auto mfma_block = [&](const Frag &f) {
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+                const bf16x8 ah = as_bf(f.a[k][0]), am = as_bf(f.a[k][1]), al = as_bf(f.a[k][2]);
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    const bf16x8 bh = as_bf(f.b[ct][0]), bm = as_bf(f.b[ct][1]), bl = as_bf(f.b[ct][2]);
+                    f32x4v c = acc[k][ct];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+                    acc[k][ct] = c;
+                }
+            }
+        };
+        // kk even: B(kk+2) is in set 0, B(kk+3) loads into set 1; kk odd: the reverse
+        auto step = [&](int kk, const Frag &cur, Frag &nxt, int set) {
+            b_load(kk + 3, set ^ 1);
+            frag_read(kk + 1, nxt);
+            mfma_block(cur);
+            b_store(kk & 1, set);
+            __syncthreads();
+        };
+        Frag f0, f1;
+        frag_read(0, f0);
+        b_load(2, 0);
+        __syncthreads();   // every wave has B(0) in registers before step 0 overwrites Bs[0]
+        static_assert(NKK % 2 == 0, "offsets come in pairs");
+        for (int kk = 0; kk < NKK; kk += 2) {
+            step(kk, f0, f1, 0);
+            step(kk + 1, f1, f0, 1);
+        }
+
+        // acc[k][ct][e]: tile row 4g + e = position 4t + g of sample e; column 16ct + r
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+            const int p = 4 * (rg + 4 * k) + g;
+            if (p >= ho2) continue;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int col = cg * 32 + ct * 16 + r;
+                const float bv = EPI == EPI_BIAS_RELU ? a.bias[col] : 0.0f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (e >= ns) continue;
+                    const int64_t row = (int64_t)(s0 + e) * ho2 + p;
+                    float v = acc[k][ct][e] + bv;
+                    v = v > 0.0f ? v : 0.0f;
+                    if (a.out) a.out[row * CN + col] = v;
+                    if (a.outb) {
+                        uint16_t *pb = a.outb + row * 3 * CN + col;
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) pb[pl * CN] = split_part(v, pl);
+                    }
+                }
+            }
+        }
+    };
+    // every wave passes the same number of barriers whatever its tile count
+    if (nt == 4) run(std::integral_constant<int, 4>{});
+    else if (nt == 3) run(std::integral_constant<int, 3>{});
+    else if (nt == 2) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 1>{});
+}
+
+// dynamic LDS bytes of conv_x6s_kernel for an HIN x HIN input (0: does not fit)
+static inline size_t conv_x6s_lds(int hin) {
+    const int ho = hin - 5, XW = ho + 8, PL = (hin * XW + 3) & ~3, XS = 12 * PL + 4;
+    const size_t b = (size_t)(2 * 768 + 4 * XS) * 16;
+    return (ho >= 1 && (4 * ho * ho + 15) / 16 <= 16 && b <= 160 * 1024) ? b : 0;
 }
 
 }  // namespace snk

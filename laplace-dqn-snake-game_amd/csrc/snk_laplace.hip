@@ -15,6 +15,7 @@
 //     (A3 A3' + 1) o (Z Z') + [a_i = a_j] o (H H' + 1) — computed from the
 //     per-sample activations without materialising those 200k columns; only
 //     the 79k conv columns of J go through the big MFMA Gram.
+#include <cstring>
 #include <algorithm>
 #include <vector>
 
@@ -127,17 +128,53 @@ __global__ void jac_permute_kernel(const float *__restrict__ Jp, int64_t ldp, co
     }
 }
 
+// Lower-triangle tiles in supertile order: groups of 8 block rows x 4 block
+// columns, so the ~32 workgroups an XCD runs at once (syrk_xcd_remap hands
+// each XCD a contiguous run of this list) share 8 + 4 row blocks in its L2
+// instead of 1 + 32 in plain row-major order. One device table per N, kept.
+static const int2 *syrk_tile_order(int N) {
+    static std::vector<std::pair<int, int2 *>> cache;
+    for (auto &c : cache)
+        if (c.first == N) return c.second;
+    const int T = (int)ceil_div(N, SY_T);
+    std::vector<int2> t;
+    t.reserve((size_t)T * (T + 1) / 2);
+    constexpr int SI = 8, SJ = 4;
+    for (int i0 = 0; i0 < T; i0 += SI)
+        for (int j0 = 0; j0 <= std::min(T - 1, i0 + SI - 1); j0 += SJ)
+            for (int i = i0; i < std::min(T, i0 + SI); ++i)
+                for (int j = j0; j < std::min(j0 + SJ, i + 1); ++j) t.push_back(int2{i, j});
+    SNK_CHECK((int64_t)t.size() == (int64_t)T * (T + 1) / 2, SNK_ERR_INTERNAL, "syrk tile order");
+    int2 *d = nullptr;
+    SNK_HIP(hipMalloc(&d, t.size() * sizeof(int2)));
+    SNK_HIP(hipMemcpy(d, t.data(), t.size() * sizeof(int2), hipMemcpyHostToDevice));
+    cache.emplace_back(N, d);
+    return d;
+}
+
 static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s) {
     SyrkArgs a = a0;
     const int64_t T = ceil_div(a.N, SY_T);
     a.ntiles = T * (T + 1) / 2;
+    static const bool rowmajor = getenv("SNK_SYRK_ORDER") && strcmp(getenv("SNK_SYRK_ORDER"), "rows") == 0;
+    a.tiles = (rowmajor || T < 16) ? nullptr : syrk_tile_order(a.N);
     SNK_CHECK(a.K % 4 == 0 && a.ld % 4 == 0 && a.kchunk % 4 == 0, SNK_ERR_INTERNAL, "syrk: K/ld not multiples of 4");
     SNK_CHECK(a.ntiles < (int64_t)1 << 31 && z <= 65535, SNK_ERR_INVALID, "syrk: problem too large");
     dim3 grid((unsigned)a.ntiles, (unsigned)z);
-    switch (out) {
-        case SYRK_F32: syrk_kernel<SYRK_F32><<<grid, 256, 0, s>>>(a); break;
-        case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64><<<grid, 256, 0, s>>>(a); break;
-        default: syrk_kernel<SYRK_DENSE_ADD><<<grid, 256, 0, s>>>(a); break;
+    // bf16 x6 split MFMA by default; SNK_SYRK=fp32: the exact-f32 32x32x2 MFMA
+    static const bool f32 = getenv("SNK_SYRK") && strcmp(getenv("SNK_SYRK"), "fp32") == 0;
+    if (f32) {
+        switch (out) {
+            case SYRK_F32: syrk_kernel<SYRK_F32, false><<<grid, 256, 0, s>>>(a); break;
+            case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, false><<<grid, 256, 0, s>>>(a); break;
+            default: syrk_kernel<SYRK_DENSE_ADD, false><<<grid, 256, 0, s>>>(a); break;
+        }
+    } else {
+        switch (out) {
+            case SYRK_F32: syrk_kernel<SYRK_F32, true><<<grid, 256, 0, s>>>(a); break;
+            case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, true><<<grid, 256, 0, s>>>(a); break;
+            default: syrk_kernel<SYRK_DENSE_ADD, true><<<grid, 256, 0, s>>>(a); break;
+        }
     }
     launch_check("syrk_kernel");
 }

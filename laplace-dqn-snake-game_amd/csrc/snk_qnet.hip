@@ -273,9 +273,11 @@ static GemmPlan plan_gemm(int64_t M, int N, int NT, int64_t K, bool allow_z) {
 // the same with the waves per tile fixed (paired launches need equal block sizes)
 static GemmPlan plan_gemm_kw(int64_t M, int N, int NT, int64_t K, bool allow_z, int kw) {
     const int64_t tiles = ceil_div(M, 32) * ceil_div(N, NT * 32);
+    static const int64_t target = getenv("SNK_KW_WAVES") ? atoll(getenv("SNK_KW_WAVES")) : 4096;
+    static const int64_t mink = getenv("SNK_KW_MINK") ? atoll(getenv("SNK_KW_MINK")) : 32;
     int z = 1;
     if (allow_z)
-        while (z < 64 && tiles * kw * z * 2 <= 4096 && K / ((int64_t)kw * z * 2) >= 32) z *= 2;
+        while (z < 64 && tiles * kw * z * 2 <= target && K / ((int64_t)kw * z * 2) >= mink) z *= 2;
     int64_t chunk = ceil_div(K, z);
     chunk = (chunk + 7) & ~int64_t(7);
     return GemmPlan{kw, (int)ceil_div(K, chunk), (int)chunk};
@@ -323,10 +325,22 @@ __global__ __launch_bounds__(NTH) void pair_kernel(J1 j1, J2 j2) {
     else
         j2(unflatten(blockIdx.x - n1, j2.grid));
 }
+template <int NTH, class J>
+__global__ __launch_bounds__(NTH) void job_kernel(J j) {
+    j(unflatten(blockIdx.x, j.grid));
+}
 template <int NTH, class J1, class J2>
 static void pair_launch(const J1 &j1, const J2 &j2, hipStream_t s) {
-    const unsigned n = j1.grid.x * j1.grid.y * j1.grid.z + j2.grid.x * j2.grid.y * j2.grid.z;
-    pair_kernel<NTH><<<n, NTH, 0, s>>>(j1, j2);
+    const unsigned n1 = j1.grid.x * j1.grid.y * j1.grid.z, n2 = j2.grid.x * j2.grid.y * j2.grid.z;
+    // SNK_UNPAIR=1: the two jobs as separate launches (profiling each half)
+    static const bool unpair = getenv("SNK_UNPAIR") && atoi(getenv("SNK_UNPAIR")) != 0;
+    if (unpair) {
+        job_kernel<NTH><<<n1, NTH, 0, s>>>(j1);
+        job_kernel<NTH><<<n2, NTH, 0, s>>>(j2);
+        launch_check("job_kernel");
+        return;
+    }
+    pair_kernel<NTH><<<n1 + n2, NTH, 0, s>>>(j1, j2);
     launch_check("pair_kernel");
 }
 
@@ -350,6 +364,12 @@ static int conv_splits(int64_t M, int nkk) {
     static const int min_kk = getenv("SNK_SPLIT_MIN_KK") ? atoi(getenv("SNK_SPLIT_MIN_KK")) : 0;
     if (wgs >= 512 || nkk <= min_kk) return 1;
     return (int)std::min<int64_t>(std::min(nkk, 16), ceil_div(512, wgs));
+}
+
+// kk splits of the conv3 data gradient (36 offsets): SNK_DX_SPLITS overrides (tuning)
+static int dx_splits(int64_t M) {
+    static const int dxs = getenv("SNK_DX_SPLITS") ? atoi(getenv("SNK_DX_SPLITS")) : 0;
+    return dxs > 0 ? std::min(dxs, 36) : conv_splits(M, 36);
 }
 
 // wb != nullptr: the bf16x6 split-precision kernel on the weight planes wb
@@ -380,6 +400,26 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
         if (pr.wb[0]) {
             if constexpr (MODE == MODE_FWD && CK % 32 == 0 && EPI != EPI_RELU_MASK) {
                 if (a.xb) {   // pre-split input, 32-channel chunks: the 16x16x32 layouts
+                    if constexpr (CN == 64 && PAD == 0 && CK == 32 && KS == 6 && EPI == EPI_BIAS_RELU) {
+                        // large batches: four samples' planes resident in LDS per workgroup
+                        static const bool x6s = !getenv("SNK_X6S") || atoi(getenv("SNK_X6S")) != 0;
+                        static const int smin = getenv("SNK_X6S_MIN") ? atoi(getenv("SNK_X6S_MIN")) : 1024;
+                        const int ho2 = a.HOUT * a.HOUT;
+                        const int S = a.M / ho2;
+                        const size_t lds = conv_x6s_lds(a.HIN);
+                        if (x6s && splits == 1 && lds && S >= smin && S * ho2 == a.M && a.HOUT == a.HIN - 5) {
+                            static bool attr = false;
+                            if (!attr) {
+                                SNK_HIP(hipFuncSetAttribute((const void *)conv_x6s_kernel<KS, EPI>,
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                                attr = true;
+                            }
+                            const dim3 g3((unsigned)ceil_div(S, 4), 1, (unsigned)ng);
+                            conv_x6s_kernel<KS, EPI><<<g3, 512, lds, s>>>(pr, S);
+                            launch_check("conv_x6s_kernel");
+                            return;
+                        }
+                    }
                     if constexpr (CN == 64 && PAD == 0) {
                         // whole input of the workgroup resident in LDS when it fits
                         const int ho2 = a.HOUT * a.HOUT;
@@ -532,7 +572,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
     const float *__restrict__ b = ca.b;
     float *__restrict__ y = ca.y;
     uint16_t *__restrict__ yb = ca.yb;
-    extern __shared__ float sm[];
+    extern __shared__ __attribute__((aligned(16))) float sm[];
     float *sw = sm;                       // [9*C*16 + 16]
     float *sx = sm + 9 * C * 16 + 16;     // [NS][C][(bs+2)^2]
     const int bp = bs + 2, plane = bp * bp, ncell = bs * bs;
@@ -540,24 +580,56 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
     if (threadIdx.x < 16) sw[9 * C * 16 + threadIdx.x] = b[threadIdx.x];
     const int64_t s0 = (int64_t)blockIdx.x * NS;
     const int ns = (int)min((int64_t)NS, S - s0);
+    // plane base pointers once per (sample, channel): the element loads below
+    // are then independent (no per-element ring-counter / slot-index load)
+    __shared__ const int8_t *pbase[8 * C];
+    if ((int)threadIdx.x < ns * C) pbase[threadIdx.x] = src.plane(s0 + threadIdx.x / C, threadIdx.x % C);
     for (int i = threadIdx.x; i < NS * C * plane; i += blockDim.x) sx[i] = 0.0f;
     __syncthreads();
-    for (int i = threadIdx.x; i < ns * C * ncell; i += blockDim.x) {
-        const int sc = i / ncell, cell = i - sc * ncell;
-        const int sl = sc / C, c = sc - sl * C;
-        const int jj = cell / bs, ii = cell - jj * bs;
-        const int8_t *pl = src.plane(s0 + sl, c);
-        const float v = pl ? (float)pl[cell] : src.fbase[((s0 + sl) * C + c) * ncell + cell];
-        sx[sc * plane + (ii + 1) + (jj + 1) * bp] = v;
-        if (ca.x0) ca.x0[s0 * C * ncell + i] = v;
+    const int nel = ns * C * ncell;
+    for (int i0 = 0; i0 < nel; i0 += 8 * 256) {
+        float v[8];   // eight loads in flight, then the stores
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 256 + threadIdx.x;
+            v[u] = 0.0f;
+            if (i < nel) {
+                const int sc = i / ncell, cell = i - sc * ncell;
+                const int8_t *pl = pbase[sc];
+                v[u] = pl ? (float)pl[cell] : src.fbase[(s0 * C + sc) * ncell + cell];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 256 + threadIdx.x;
+            if (i < nel) {
+                const int sc = i / ncell, cell = i - sc * ncell;
+                const int jj = cell / bs, ii = cell - jj * bs;
+                sx[sc * plane + (ii + 1) + (jj + 1) * bp] = v[u];
+                if (ca.x0) ca.x0[s0 * C * ncell + i] = v[u];
+            }
+        }
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < ns * ncell; q += blockDim.x) {
+    // yb rows go out through LDS: 256 rows x 96 B per pass, written back as
+    // consecutive 16-byte pieces (the direct stores were 16 B at a 96-B lane stride)
+    u32x4 *stg = reinterpret_cast<u32x4 *>(sx + ((NS * C * plane + 3) & ~3));
+    const int nq = ns * ncell;
+    for (int q0 = 0; q0 < nq; q0 += 256) {
+        const int q = q0 + threadIdx.x;
+        if (q < nq) {
+        // weights are re-read from LDS (16-byte broadcasts) for every position:
+        // hoisted into registers they took 288 VGPRs at C = 2 (one wave per SIMD)
+        asm volatile("" ::: "memory");
         const int sl = q / ncell, p = q - sl * ncell;
         const int j = p / bs, i = p - j * bs;
+        const float4 *sw4 = reinterpret_cast<const float4 *>(sw);
         float acc[16];
 #pragma unroll
-        for (int co = 0; co < 16; ++co) acc[co] = sw[9 * C * 16 + co];
+        for (int v4 = 0; v4 < 4; ++v4) {
+            const float4 b4 = sw4[9 * C * 4 + v4];
+            acc[4 * v4] = b4.x; acc[4 * v4 + 1] = b4.y; acc[4 * v4 + 2] = b4.z; acc[4 * v4 + 3] = b4.w;
+        }
 #pragma unroll
         for (int kk = 0; kk < 9; ++kk) {
             const int du = kk % 3, dv = kk / 3;   // input (i+du-1, j+dv-1) = bordered (i+du, j+dv)
@@ -565,7 +637,13 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
             for (int c = 0; c < C; ++c) {
                 const float v = sx[(sl * C + c) * plane + (i + du) + (j + dv) * bp];
 #pragma unroll
-                for (int co = 0; co < 16; ++co) acc[co] = __builtin_fmaf(v, sw[(kk * C + c) * 16 + co], acc[co]);
+                for (int v4 = 0; v4 < 4; ++v4) {
+                    const float4 w4 = sw4[(kk * C + c) * 4 + v4];
+                    acc[4 * v4] = __builtin_fmaf(v, w4.x, acc[4 * v4]);
+                    acc[4 * v4 + 1] = __builtin_fmaf(v, w4.y, acc[4 * v4 + 1]);
+                    acc[4 * v4 + 2] = __builtin_fmaf(v, w4.z, acc[4 * v4 + 2]);
+                    acc[4 * v4 + 3] = __builtin_fmaf(v, w4.w, acc[4 * v4 + 3]);
+                }
             }
         }
 #pragma unroll
@@ -577,7 +655,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
             for (int v = 0; v < 4; ++v) o[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
         }
         if (yb) {
-            u32x4 *o = reinterpret_cast<u32x4 *>(yb + row * 48);
+            u32x4 *o = stg + threadIdx.x * 6;
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
                 const Split3 sp = split3(f32x4{acc[8 * half], acc[8 * half + 1], acc[8 * half + 2], acc[8 * half + 3]},
@@ -587,6 +665,14 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
                 o[2 + half] = sp.m;
                 o[4 + half] = sp.l;
             }
+        }
+        }
+        if (yb) {
+            __syncthreads();
+            const int n16 = min(256, nq - q0) * 6;
+            u32x4 *dst = reinterpret_cast<u32x4 *>(yb + (s0 * ncell + q0) * 48);
+            for (int e = threadIdx.x; e < n16; e += 256) dst[e] = stg[e];
+            __syncthreads();
         }
     }
 }
@@ -959,7 +1045,10 @@ static int64_t conv_slab_floats(const QLayout &L, int64_t S, bool train) {
     };
     add(S * L.ncell, 9, 32);
     add(S * L.Wo * L.Wo, 36, 64);
-    if (train) add(S * L.ncell, 36, 32);
+    if (train) {
+        const int sp = dx_splits(S * L.ncell);
+        if (sp > 1) need = std::max(need, (int64_t)sp * S * L.ncell * 32);
+    }
     return need;
 }
 
@@ -1035,9 +1124,12 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         for (int g = 0; g < ng; ++g) net[g].w->x0_valid = 0;
     }
     if (lo <= 0 && hi >= 0) {
-        const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S * ng / 256));
+        // samples per workgroup: S*ng/1024 capped at 8 (4 at the 4096-env act forward: measured
+        // 20 us against 25 at 8; 1 sample per workgroup costs the per-workgroup weight/board latency)
+        static const int c1div = getenv("SNK_C1_DIV") ? atoi(getenv("SNK_C1_DIV")) : 1024;
+        const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S * ng / c1div));
         const dim3 grid((unsigned)ceil_div(S, ns), (unsigned)ng);
-        const size_t lds = (size_t)(9 * L.C * 16 + 16 + ns * L.C * (bs + 2) * (bs + 2)) * sizeof(float);
+        const size_t lds = (size_t)(9 * L.C * 16 + 16 + ((ns * L.C * (bs + 2) * (bs + 2) + 3) & ~3) + 256 * 24) * sizeof(float);
         Conv1Pair cp{};
         for (int g = 0; g < 2; ++g) {
             const FwdNet &n = net[g < ng ? g : 0];
@@ -1178,7 +1270,7 @@ static void backward_data_chain(const QLayout &L, const float *th, int64_t S, QW
     {
         ConvArgs a{};
         a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs; a.nkk = 36;
-        const int sp = conv_splits(S * nc, 36);
+        const int sp = dx_splits(S * nc);
         if (sp == 1) {
             a.out = w.dz2;
             conv_launch<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK>(a, 1, s);
@@ -1248,7 +1340,7 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             ConvArgs a{};
             a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs;
             a.nkk = 36;
-            int sp = conv_splits(S * nc, 36);
+            int sp = dx_splits(S * nc);
             const dim3 cg((unsigned)ceil_div(S * nc, 128), 1, 1);
             if (sp == 1) {
                 a.out = w.dz2;
@@ -1332,7 +1424,7 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
     {
         ConvArgs a{};
         a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs; a.nkk = 36;
-        const int sp = conv_splits(S * nc, 36);
+        const int sp = dx_splits(S * nc);
         if (sp == 1) {
             a.out = w.dz2;
             conv_launch<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK>(a, 1, s);

@@ -20,7 +20,7 @@
 // (1024 k), so the error is that of 1024-long fp32 dot products summed in
 // fp64, independent of K (K is ~79k for the Jacobian Gram).
 #pragma once
-#include "snk_conv.hpp"
+#include "snk_conv_x6.hpp"
 
 namespace snk {
 
@@ -141,6 +141,171 @@ __device__ __forceinline__ void syrk_loop(const float *__restrict__ x, int64_t l
     }
 }
 
+// The same tile on the bf16 x6 split (snk_conv_x6.hpp): each 32-k stage of
+// both 128-row blocks is loaded as fp32 (two float4 per row chunk of 8 k),
+// split once into h/m/l bf16 planes while parked in LDS ([op][plane][row][40]:
+// 80-byte rows, conflict-free ds_read_b128 for both lane halves), and each
+// wave runs 2 k-steps x 2 x 2 tiles x 6 part products of
+// v_mfma_f32_32x32x16_bf16: 1536 MFMA cycles per stage against 4096 for the
+// 32x32x2 f32 form, with the error class of an fp32 dot product. Double
+// buffered (120 KB: the fp64 flush accumulators hold the kernel to one
+// workgroup per CU anyway): the next stage is split and parked right after
+// this stage's MFMAs, one barrier per stage. Accumulator layout and fp64
+// flushing as syrk_loop.
+constexpr int SX_LD = 40;
+struct SyrkX6Lds {
+    uint16_t p[2][2][3][SY_T * SX_LD];   // [buffer][operand][plane]
+};
+
+template <bool FLUSH>
+__device__ __forceinline__ void syrk_loop_x6(const float *__restrict__ x, int64_t ld, int N, int64_t k0, int64_t k1,
+                                             int bi, int bj, SyrkX6Lds &s, f32x16 (&acc)[2][2],
+                                             double (&accd)[2][2][16]) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+    // staging: rows (tid >> 2) + 64q of each block, k chunk 8*(tid & 3) .. +7
+    const int c8 = 8 * (tid & 3);
+    const float *pa[2], *pb[2];
+    float ma[2], mb[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ra = bi * SY_T + (tid >> 2) + 64 * q, rb = bj * SY_T + (tid >> 2) + 64 * q;
+        pa[q] = x + (int64_t)(ra < N ? ra : N - 1) * ld;
+        pb[q] = x + (int64_t)(rb < N ? rb : N - 1) * ld;
+        ma[q] = ra < N ? 1.0f : 0.0f;
+        mb[q] = rb < N ? 1.0f : 0.0f;
+    }
+    const int nst = (int)((k1 - k0 + SY_KS - 1) / SY_KS);
+    // three register sets: stages st+1 .. st+3 in flight while stage st computes
+    // (one 32 KB stage per CU in flight left the loads latency-bound)
+    struct Stage {
+        f32x4 va[2][2], vb[2][2];
+        float km[2];
+    };
+    Stage rs[3];
+    auto issue = [&](int st, Stage &g) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            const int64_t k = k0 + (int64_t)st * SY_KS + c8 + 4 * hf;
+            const bool v = k < k1;
+            const int64_t kk = v ? k : k0;
+            g.km[hf] = v ? 1.0f : 0.0f;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                g.va[q][hf] = *reinterpret_cast<const f32x4 *>(pa[q] + kk);
+                g.vb[q][hf] = *reinterpret_cast<const f32x4 *>(pb[q] + kk);
+            }
+        }
+    };
+    auto park = [&](int buf, const Stage &g) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int off = ((tid >> 2) + 64 * q) * SX_LD + c8;
+            const Split3 sa = split3(g.va[q][0] * (ma[q] * g.km[0]), g.va[q][1] * (ma[q] * g.km[1]));
+            const Split3 sb = split3(g.vb[q][0] * (mb[q] * g.km[0]), g.vb[q][1] * (mb[q] * g.km[1]));
+            *reinterpret_cast<u32x4 *>(&s.p[buf][0][0][off]) = sa.h;
+            *reinterpret_cast<u32x4 *>(&s.p[buf][0][1][off]) = sa.m;
+            *reinterpret_cast<u32x4 *>(&s.p[buf][0][2][off]) = sa.l;
+            *reinterpret_cast<u32x4 *>(&s.p[buf][1][0][off]) = sb.h;
+            *reinterpret_cast<u32x4 *>(&s.p[buf][1][1][off]) = sb.m;
+            *reinterpret_cast<u32x4 *>(&s.p[buf][1][2][off]) = sb.l;
+        }
+    };
+    // one quarter of park(): operand op (0: A rows, 1: B rows), row group q
+    auto park_piece = [&](int buf, const Stage &g, int op, int q) {
+        const int off = ((tid >> 2) + 64 * q) * SX_LD + c8;
+        const float m = op == 0 ? ma[q] : mb[q];
+        const f32x4 *v = op == 0 ? g.va[q] : g.vb[q];
+        const Split3 sp = split3(v[0] * (m * g.km[0]), v[1] * (m * g.km[1]));
+        *reinterpret_cast<u32x4 *>(&s.p[buf][op][0][off]) = sp.h;
+        *reinterpret_cast<u32x4 *>(&s.p[buf][op][1][off]) = sp.m;
+        *reinterpret_cast<u32x4 *>(&s.p[buf][op][2][off]) = sp.l;
+    };
+    // the MFMAs of one stage with the park of the next woven in (source order)
+    auto compute_park = [&](int buf, bool pk, const Stage &nx) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) {
+                    fa[i][pl] = as_bf(*reinterpret_cast<const u32x4 *>(
+                        &s.p[buf][0][pl][(wr + 32 * i + r) * SX_LD + 16 * ks + 8 * h]));
+                    fb[i][pl] = as_bf(*reinterpret_cast<const u32x4 *>(
+                        &s.p[buf][1][pl][(wc + 32 * i + r) * SX_LD + 16 * ks + 8 * h]));
+                }
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    f32x16 c = acc[mi][ni];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][2], fb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][1], fb[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][0], fb[ni][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][1], fb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][0], fb[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][0], fb[ni][0], c, 0, 0, 0);
+                    acc[mi][ni] = c;
+                    if (ks == 1 && pk) park_piece(buf ^ 1, nx, mi, ni);
+                }
+        }
+    };
+    auto flush = [&]() {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    accd[mi][ni][g] += (double)acc[mi][ni][g];
+                    acc[mi][ni][g] = 0.0f;
+                }
+    };
+    // stage st: loads of st+3 go out into set st % 3 (whose stage st was
+    // parked at st-1), stage st+1 (set (st+1) % 3) is parked after the MFMAs.
+    // Stage indices past the end clamp (the loads are masked by km and unused).
+    // BUF = st & 1 is a template constant (the loop is unrolled by 6), so the
+    // compiler sees that the park's LDS stores and this stage's fragment
+    // reads touch different buffers; the split VALU work and the stores are
+    // woven between the MFMAs in source order to fill their issue slots
+    // (one wave per SIMD: nothing else would hide them).
+    auto step = [&](int st, auto bufc, Stage &ld3, Stage &nx) {
+        constexpr int BUF = decltype(bufc)::value;
+        const bool more = st + 1 < nst;
+        issue(st + 3 < nst ? st + 3 : nst - 1, ld3);
+        __builtin_amdgcn_sched_barrier(0);
+        // park of stage st+1 into the other buffer (last read in stage st-1,
+        // before the barrier), woven between the second k-step's MFMAs
+        compute_park(BUF, more, nx);
+        if (FLUSH && (st % SY_FLUSH == SY_FLUSH - 1 || !more)) flush();
+        __syncthreads();
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    issue(0, rs[0]);
+    if (nst > 1) issue(1, rs[1]);
+    if (nst > 2) issue(2, rs[2]);
+    park(0, rs[0]);
+    __syncthreads();
+    int st = 0;
+    for (; st + 6 <= nst; st += 6) {
+        step(st, B0{}, rs[0], rs[1]);
+        step(st + 1, B1{}, rs[1], rs[2]);
+        step(st + 2, B0{}, rs[2], rs[0]);
+        step(st + 3, B1{}, rs[0], rs[1]);
+        step(st + 4, B0{}, rs[1], rs[2]);
+        step(st + 5, B1{}, rs[2], rs[0]);
+    }
+    // tail (< 6 stages): the same rotation
+    if (st < nst) step(st, B0{}, rs[0], rs[1]);
+    if (st + 1 < nst) step(st + 1, B1{}, rs[1], rs[2]);
+    if (st + 2 < nst) step(st + 2, B0{}, rs[2], rs[0]);
+    if (st + 3 < nst) step(st + 3, B1{}, rs[0], rs[1]);
+    if (st + 4 < nst) step(st + 4, B0{}, rs[1], rs[2]);
+}
+
 __device__ __forceinline__ void syrk_zero(f32x16 (&acc)[2][2]) {
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -157,6 +322,7 @@ struct SyrkArgs {
     int64_t ld, K, kchunk;   // reduction range of split z: [z*kchunk, min(K, (z+1)*kchunk))
     int N;
     int64_t ntiles;
+    const int2 *tiles;       // optional tile order (bi, bj), indexed by the XCD remap; null: row-major
     float *g32;              // SYRK_F32 / SYRK_DENSE_ADD: G [N][ldg]
     double *g64;             // SYRK_SLAB64: slab [z][N][N]
     int64_t ldg;
@@ -166,11 +332,25 @@ struct SyrkArgs {
     int64_t ldz;
 };
 
-template <int OUT>
+union SyrkSmem {
+    SyrkLds f32;
+    SyrkX6Lds x6;
+};
+template <int OUT, bool X6>
 __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
-    __shared__ __attribute__((aligned(16))) SyrkLds s;
+    __shared__ __attribute__((aligned(16))) SyrkSmem sm;
+    SyrkLds &s = sm.f32;
     int bi, bj;
-    syrk_tile(syrk_xcd_remap(blockIdx.x, a.ntiles), bi, bj);
+    {
+        const int64_t t = syrk_xcd_remap(blockIdx.x, a.ntiles);
+        if (a.tiles) {
+            const int2 tb = a.tiles[t];
+            bi = tb.x;
+            bj = tb.y;
+        } else {
+            syrk_tile(t, bi, bj);
+        }
+    }
     f32x16 acc[2][2];
     double accd[2][2][16];
     syrk_zero(acc);
@@ -182,7 +362,12 @@ __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
             for (int g = 0; g < 16; ++g) accd[mi][ni][g] = 0.0;
     const int64_t k0 = (int64_t)blockIdx.y * a.kchunk;
     const int64_t k1 = k0 + a.kchunk < a.K ? k0 + a.kchunk : a.K;
-    if (k0 < k1) syrk_loop<true>(a.x, a.ld, a.N, k0, k1, bi, bj, s, acc, accd);
+    if (k0 < k1) {
+        if (X6)
+            syrk_loop_x6<true>(a.x, a.ld, a.N, k0, k1, bi, bj, sm.x6, acc, accd);
+        else
+            syrk_loop<true>(a.x, a.ld, a.N, k0, k1, bi, bj, s, acc, accd);
+    }
     if (OUT == SYRK_DENSE_ADD) {
         // (A3 Gram + 1) * (dz1 Gram)
         syrk_zero(acc);

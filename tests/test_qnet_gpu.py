@@ -186,3 +186,43 @@ def test_x6_split_forward_matches_fp32_and_oracle(snk, bs, C, B, monkeypatch):
             assert e6.max() <= 1e-5 and e32.max() <= 1e-5
         assert e6.max() <= 2 * e32.max() + 1e-7, (scale, e6.max(), e32.max())
         assert e6.mean() <= 2 * e32.mean() + 1e-8, (scale, e6.mean(), e32.mean())
+
+
+def test_large_batch_forward_x6s_vs_oracle(snk):
+    """B >= 1024 routes conv3 through conv_x6s_kernel (four samples' planes in
+    LDS). 1101 samples leave a partial last group of one sample."""
+    bs, C, B = 12, 2, 1101
+    rng = np.random.default_rng(11)
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=13)
+    x = rng.integers(-1, 3, size=(B, C, bs * bs)).astype(np.float32)
+    q = m(x)
+    qref = oracle.qnet_forward(bs, C, m.get_params(), x)
+    assert _qclose(q, qref), np.abs(q - qref).max()
+
+
+_X6S_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import snake_amd as snk
+snk.load()
+rng = np.random.default_rng(4)
+m = snk.DQNModel(12, 3, n_frames=2, seed=21)
+x = rng.integers(-1, 3, size=(2050, 2, 144)).astype(np.float32)
+np.save(sys.argv[2], m(x))
+"""
+
+
+def test_x6s_bitexact_with_x6m16(tmp_path):
+    """conv_x6s accumulates the six part products in x6m16's order: the Q
+    values of a 2050-sample forward are identical with SNK_X6S=1 and 0."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    out = {}
+    for v in ("1", "0"):
+        f = str(tmp_path / f"q{v}.npy")
+        env = dict(os.environ, SNK_X6S=v)
+        subprocess.run([sys.executable, "-c", _X6S_SCRIPT, repo, f], env=env, check=True, timeout=300)
+        out[v] = np.load(f)
+    assert np.array_equal(out["1"], out["0"])

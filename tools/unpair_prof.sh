@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out/up
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/up/t.log 2>&1; rc=$?; tail -n 3 gpurun_out/up/t.log; [ $rc -eq 0 ] || exit 1
+for v in 256 1024; do
+  SNK_C1_DIV=$v timeout -k 10 120 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-dbuild > gpurun_out/up/b$v.json 2>/dev/null || exit 1
+  python -c "import json;d=json.load(open('gpurun_out/up/b$v.json'));a=d['act_forward_ms'];print($v, round(d['ms_per_step'],4), int(d['value']), round(a['conv1']*1e3,1), round(a['conv2']*1e3,1), round(a['conv3']*1e3,1))"
+done
+SNK_UNPAIR=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/up/prof -o run -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-dbuild --no-extras > gpurun_out/up/pb.json 2> gpurun_out/up/prof.err || exit 3
+echo done
