@@ -38,6 +38,8 @@ struct ConvArgs {
     float *out;          // [M][CN] or slab [split][M][CN]
     const uint16_t *xb;  // x6 kernels: A pre-split into bf16 planes [S][HIN*HIN][3][CK] (else split x)
     uint16_t *outb;      // x6 EPI_BIAS_RELU: also write the output's bf16 planes [M][3][CN]
+    const float *wmax;   // h3 kernels: per-block partial max |w| of the weight image (conv1 writes them)
+    int nwmax;           //   their count
     int M, HIN, HOUT, nkk, kk_per_split;
     uint32_t d2m, d2s, d1m, d1s;   // FastDiv(HOUT*HOUT), FastDiv(HOUT) magic/shift
 };

@@ -1,0 +1,295 @@
+// snk_conv_h3.hpp — fp32-accurate conv3 of large batches on fp16 MFMA ("h3").
+//
+// The x6 kernels (snk_conv_x6.hpp) split each fp32 operand into three bf16
+// parts and need six part products. fp16 carries 11 significant bits against
+// bf16's 8, so TWO parts reach the same place: h = f16(x), l = f16(x - h)
+// (x - h is exact in fp32: Sterbenz), |x - h| <= 2^-11 |x|, |x - h - l| <=
+// 2^-22 |x|, and a product needs THREE MFMAs:
+//   x*y ~= hl + lh + hh          (dropped: ll <= 2^-22 |xy|)
+// each part product exact in the fp32 accumulator (11 x 11 bits). That is
+// half the MFMA issue of x6 (v_mfma_f32_16x16x32_f16 runs at the bf16 rate),
+// and A/B move as two 16-bit planes instead of three.
+//
+// fp16's exponent range is what bf16 did not need: the parts are taken of a
+// power-of-two-scaled value, one scale per SAMPLE for the activations (its
+// max |a| lands in [2^14, 2^15): no overflow, l normal down to 2^-18 of the
+// max, below that an absolute error <= 2^-40 of the max) and one per TENSOR
+// for the weights (the same rule on max |w| over the weight image). Both
+// scales factor out of the dot product and come back exactly in the
+// epilogue (one v_ldexp_f32). max |w| arrives as per-block partials that
+// conv1_fwd_kernel (or wmax_scan_kernel) wrote from the same image; each
+// workgroup folds them in its prologue. Activations come in as fp32 (the
+// producing conv2 writes floats, 2/3 of the bytes of the x6 planes), and
+// the per-sample max is a workgroup reduction over the staged samples.
+//
+// Error: per product <= 3 * 2^-22 relative, random in sign across the 1152
+// terms of a conv3 dot product; the fp32 accumulation (shared with the x6 and
+// fp32 MFMA paths) dominates. Pinned against the fp64 oracle (1e-5) and
+// against the fp32-MFMA forward's own error in tests/test_qnet_gpu.py.
+//
+// Geometry and pipeline are conv_x6s_kernel's (four samples' inputs resident
+// in LDS, sample-interleaved 16-row tiles, B double buffered per kernel
+// offset with the XOR chunk swizzle); B is split in registers while it is
+// staged (one float4 of the fp32 image per thread per offset).
+#pragma once
+
+#include "snk_conv_x6.hpp"
+
+namespace snk {
+
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f16x8 as_h(const u32x4 &v) { return __builtin_bit_cast(f16x8, v); }
+
+// e such that max * 2^e < 2^15 (>= 2^14 for a normal max); 0 for a zero or non-finite max
+__device__ __forceinline__ int h3_exp(float m) {
+    const uint32_t b = __float_as_uint(m) & 0x7fffffffu;
+    if (b == 0 || b >= 0x7f800000u) return 0;
+    return 15 - (max((int)(b >> 23), 1) - 126);
+}
+
+// four floats scaled by 2^e, split into fp16 h / l (two halves per dword, RNE)
+__device__ __forceinline__ void h3_split4(const f32x4 &x, int e, u32x2 &h, u32x2 &l) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const f32x2 v{__builtin_ldexpf(x[2 * i], e), __builtin_ldexpf(x[2 * i + 1], e)};
+        const f16x2 hv = __builtin_convertvector(v, f16x2);
+        const f32x2 r = v - __builtin_convertvector(hv, f32x2);
+        h[i] = __builtin_bit_cast(uint32_t, hv);
+        l[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2));
+    }
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// partial max |w| of w[0, n): block b (256 threads) covers a grid-stride share; part[b]
+__device__ __forceinline__ void wmax_block(const float *__restrict__ w, int64_t n, float *__restrict__ part,
+                                           float *red4) {
+    float m = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        m = fmaxf(m, fabsf(w[i]));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
+}
+
+__global__ __launch_bounds__(256) void wmax_scan_kernel(const float *__restrict__ w, int64_t n,
+                                                        float *__restrict__ part) {
+    __shared__ float red4[4];
+    wmax_block(w, n, part, red4);
+}
+
+// conv3 (CK = 32 -> CN = 64, pad 0, EPI_BIAS_RELU) on the h3 split; ConvArgs:
+// x = fp32 input [S][HIN^2][32], w = fp32 weight image [kk][64][32],
+// wmax/nwmax = partial max |w| of that image; out (fp32) and/or outb (x6 planes)
+template <int KS, int EPI>
+__global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
+    constexpr int CN = 64, CK = 32, NSG = 4, NB = 2 * CN * CK / 8;   // 512 16-byte chunks per offset
+    constexpr int NKK = KS * KS, NLA = 11;   // A float4 loads per thread: 4 samples of <= 13 x 13 x 32
+    static_assert(NB == 512 && CN * CK / 4 == 512, "one float4 of the image per thread per offset");
+    const ConvArgs &a = pr.g[blockIdx.z];
+    const f32x4 *__restrict__ wsrc = reinterpret_cast<const f32x4 *>(a.w);
+    extern __shared__ __attribute__((aligned(16))) u32x4 h3s_lds[];
+    __shared__ float red[8][5];
+    u32x4 *Bs = h3s_lds;            // [2][NB]
+    u32x4 *As = h3s_lds + 2 * NB;   // A image, conv_x6s_kernel's slot map with two planes per group
+    u32x2 *Bs2 = reinterpret_cast<u32x2 *>(Bs);
+    u32x2 *As2 = reinterpret_cast<u32x2 *>(As);
+    const int hin = a.HIN, ho = a.HOUT, ho2 = ho * ho, hin2 = hin * hin;
+    const int XW = ho + 8, PL = (hin * XW + 3) & ~3, GG = 2 * PL, XS = 4 * GG + 4;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int s0 = blockIdx.x * NSG;
+    const int ns = min(NSG, S - s0);
+
+    // B register sets: set kk & 1 carries B(kk) (fp32, unsplit) from global to LDS
+    f32x4 bst[2];
+    auto b_load = [&](int kk, int set) { bst[set] = wsrc[(int64_t)min(kk, NKK - 1) * NB + tid]; };
+    const int bch = (tid >> 3) * 4 + ((tid & 7) >> 1);   // 16-byte chunk of column tid >> 3, channels 8*(..)
+    const int bhalf = tid & 1;
+    int ew = 0;
+    auto b_store = [&](int buf, int set) {
+        u32x2 h, l;
+        h3_split4(bst[set], ew, h, l);
+        Bs2[(buf * NB + x6s_bswz(bch)) * 2 + bhalf] = h;
+        Bs2[(buf * NB + x6s_bswz(256 + bch)) * 2 + bhalf] = l;
+    };
+    b_load(0, 0);
+    b_load(1, 1);
+
+    // A: the group's fp32 inputs, then one max per sample and the weight max
+    const int per = hin2 * 8, n4 = ns * per;
+    const f32x4 *src = reinterpret_cast<const f32x4 *>(a.x) + (int64_t)s0 * per;
+    f32x4 av[NLA];
+#pragma unroll
+    for (int u = 0; u < NLA; ++u) av[u] = src[min(u * 512 + tid, n4 - 1)];
+    float wm = 0.0f;
+    for (int i = tid; i < a.nwmax; i += 512) wm = fmaxf(wm, a.wmax[i]);
+    float sm0 = 0.0f, sm1 = 0.0f, sm2 = 0.0f, sm3 = 0.0f;
+#pragma unroll
+    for (int u = 0; u < NLA; ++u) {
+        const int e = u * 512 + tid;
+        const int sr = e < n4 ? e / per : NSG;
+        const f32x4 v = av[u];
+        const float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+        sm0 = sr == 0 ? fmaxf(sm0, m) : sm0;
+        sm1 = sr == 1 ? fmaxf(sm1, m) : sm1;
+        sm2 = sr == 2 ? fmaxf(sm2, m) : sm2;
+        sm3 = sr == 3 ? fmaxf(sm3, m) : sm3;
+    }
+    sm0 = wave_max(sm0);
+    sm1 = wave_max(sm1);
+    sm2 = wave_max(sm2);
+    sm3 = wave_max(sm3);
+    wm = wave_max(wm);
+    if (lane == 0) {
+        red[wave][0] = sm0; red[wave][1] = sm1; red[wave][2] = sm2; red[wave][3] = sm3; red[wave][4] = wm;
+    }
+    __syncthreads();
+    int ea[NSG];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        float m = red[0][q];
+#pragma unroll
+        for (int w8 = 1; w8 < 8; ++w8) m = fmaxf(m, red[w8][q]);
+        if (q < NSG) ea[q] = h3_exp(m);
+        else ew = h3_exp(m);
+    }
+#pragma unroll
+    for (int u = 0; u < NLA; ++u) {
+        const int e = u * 512 + tid;
+        if (e < n4) {
+            const int sr = e / per, loc = e - sr * per;
+            const int pos = loc >> 3, c4 = loc & 7;
+            const int j = pos / hin, i = pos - j * hin;
+            const int slot = sr * XS + (c4 >> 1) * GG + j * XW + i;
+            const int es = sr == 0 ? ea[0] : sr == 1 ? ea[1] : sr == 2 ? ea[2] : ea[3];
+            u32x2 h, l;
+            h3_split4(av[u], es, h, l);
+            As2[slot * 2 + (c4 & 1)] = h;
+            As2[(slot + PL) * 2 + (c4 & 1)] = l;
+        }
+    }
+    b_store(0, 0);
+    b_store(1, 1);
+
+    const int T = (NSG * ho2 + 15) / 16;
+    const int rg = wave >> 1, cg = wave & 1;
+    const int nt = __builtin_amdgcn_readfirstlane(T > rg ? (T - rg + 3) / 4 : 0);
+    const int bslot = (cg * 32 + r) * 4 + (g ^ ((4 - ((r >> 2) & 3)) & 3));
+    __syncthreads();
+
+    // conv_x6s_kernel's pipeline (see there): offset kk's MFMAs on fragments
+    // read during kk-1, B(kk+2) split into LDS while B(kk+3) is in flight
+    auto run = [&](auto ntc) {
+        constexpr int NT = decltype(ntc)::value;
+        int abase[NT];
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+            const int q = 16 * (rg + 4 * k) + r;
+            const int p = min(q >> 2, ho2 - 1), sr = q & 3;
+            const int j = p / ho, i = p - j * ho;
+            abase[k] = sr * XS + g * GG + j * XW + i;
+        }
+        f32x4v acc[NT][2];
+#pragma unroll
+        for (int k = 0; k < NT; ++k)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) acc[k][ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        struct Frag {
+            u32x4 a[NT][2], b[2][2];
+        };
+        auto frag_read = [&](int kk, Frag &f) {
+            kk = min(kk, NKK - 1);
+            const int dv = kk / KS, du = kk - dv * KS;
+            const int off = dv * XW + du;
+            const u32x4 *pb = Bs + (kk & 1) * NB + bslot;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl) f.b[ct][pl] = pb[ct * 64 + pl * 256];
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+                const u32x4 *pa = As + abase[k] + off;
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl) f.a[k][pl] = pa[pl * PL];
+            }
+        };
+        auto mfma_block = [&](const Frag &f) {
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+                const f16x8 ah = as_h(f.a[k][0]), al = as_h(f.a[k][1]);
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    const f16x8 bh = as_h(f.b[ct][0]), bl = as_h(f.b[ct][1]);
+                    f32x4v c = acc[k][ct];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+                    acc[k][ct] = c;
+                }
+            }
+        };
+        auto step = [&](int kk, const Frag &cur, Frag &nxt, int set) {
+            b_load(kk + 3, set ^ 1);
+            frag_read(kk + 1, nxt);
+            mfma_block(cur);
+            b_store(kk & 1, set);
+            __syncthreads();
+        };
+        Frag f0, f1;
+        frag_read(0, f0);
+        b_load(2, 0);
+        __syncthreads();
+        static_assert(NKK % 2 == 0, "offsets come in pairs");
+        for (int kk = 0; kk < NKK; kk += 2) {
+            step(kk, f0, f1, 0);
+            step(kk + 1, f1, f0, 1);
+        }
+
+        // acc[k][ct][e]: tile row 4g + e = position 4t + g of sample e; column 16ct + r
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+            const int p = 4 * (rg + 4 * k) + g;
+            if (p >= ho2) continue;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int col = cg * 32 + ct * 16 + r;
+                const float bv = EPI == EPI_BIAS_RELU ? a.bias[col] : 0.0f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (e >= ns) continue;
+                    const int64_t row = (int64_t)(s0 + e) * ho2 + p;
+                    float v = __builtin_ldexpf(acc[k][ct][e], -(ea[e] + ew)) + bv;
+                    v = v > 0.0f ? v : 0.0f;
+                    if (a.out) a.out[row * CN + col] = v;
+                    if (a.outb) {
+                        uint16_t *pb = a.outb + row * 3 * CN + col;
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) pb[pl * CN] = split_part(v, pl);
+                    }
+                }
+            }
+        }
+    };
+    if (nt == 4) run(std::integral_constant<int, 4>{});
+    else if (nt == 3) run(std::integral_constant<int, 3>{});
+    else if (nt == 2) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 1>{});
+}
+
+// dynamic LDS bytes of conv_h3s_kernel for an HIN x HIN input (0: does not fit)
+static inline size_t conv_h3s_lds(int hin) {
+    const int ho = hin - 5, XW = ho + 8, PL = (hin * XW + 3) & ~3, XS = 8 * PL + 4;
+    const size_t b = (size_t)(2 * 512 + 4 * XS) * 16;
+    return (ho >= 1 && hin <= 13 && (4 * ho * ho + 15) / 16 <= 16 && b <= 160 * 1024) ? b : 0;
+}
+
+}  // namespace snk

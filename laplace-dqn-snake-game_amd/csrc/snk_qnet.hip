@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "snk_conv_h3.hpp"
 #include "snk_conv_x6.hpp"
 #include "snk_qnet.hpp"
 
@@ -396,6 +397,26 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
     const ConvPair pr = make_conv_pair(ga, ng, splits, wb);
     const ConvArgs &a = pr.g[0];
     dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)splits, (unsigned)ng);
+    if constexpr (MODE == MODE_FWD && CN == 64 && CK == 32 && KS == 6 && PAD == 0 && EPI == EPI_BIAS_RELU) {
+        if (a.wmax) {   // fp16 h3 split, four samples resident in LDS (forward_layers chose it: h3s_ok)
+            const int ho2 = a.HOUT * a.HOUT;
+            const int S = a.M / ho2;
+            const size_t lds = conv_h3s_lds(a.HIN);
+            SNK_CHECK(splits == 1 && lds && S * ho2 == a.M && a.HOUT == a.HIN - 5 && !a.xb && a.x && a.w &&
+                          (ng == 1 || pr.g[1].wmax),
+                      SNK_ERR_INTERNAL, "h3s conv3 geometry");
+            static bool attr = false;
+            if (!attr) {
+                SNK_HIP(hipFuncSetAttribute((const void *)conv_h3s_kernel<KS, EPI>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                attr = true;
+            }
+            const dim3 g3((unsigned)ceil_div(S, 4), 1, (unsigned)ng);
+            conv_h3s_kernel<KS, EPI><<<g3, 512, lds, s>>>(pr, S);
+            launch_check("conv_h3s_kernel");
+            return;
+        }
+    }
     if constexpr (MODE != MODE_DX) {
         if (pr.wb[0]) {
             if constexpr (MODE == MODE_FWD && CK % 32 == 0 && EPI != EPI_RELU_MASK) {
@@ -513,6 +534,8 @@ struct FwdIO {
     const uint16_t *wb, *xb;   // x6: weight planes, pre-split input planes
     uint16_t *outb;            // x6: also write the output's planes
     QWork *wk;                 // its workspace (conv slab)
+    const float *wmax = nullptr;   // h3 conv3: partial max |w| of the fp32 image w
+    int nwmax = 0;
 };
 
 // out = conv (bias + relu) for ng nets at once, kk-split through the conv slabs when the grid is small
@@ -524,7 +547,7 @@ static void conv_fwd(const FwdIO *io, int ng, int64_t M, int HIN, int HOUT, hipS
     for (int g = 0; g < ng; ++g) {
         ConvArgs a{};
         a.x = io[g].x; a.w = io[g].w; a.bias = io[g].bias; a.M = (int)M; a.HIN = HIN; a.HOUT = HOUT;
-        a.nkk = KS * KS; a.xb = io[g].xb;
+        a.nkk = KS * KS; a.xb = io[g].xb; a.wmax = io[g].wmax; a.nwmax = io[g].nwmax;
         if (sp == 1) {
             a.out = io[g].out;
             a.outb = io[g].outb;
@@ -560,6 +583,9 @@ struct Conv1Args {
     float *y;
     uint16_t *yb;
     float *x0;   // optional: the input planes as floats [S][C][bs*bs] (training: conv1 weight gradient)
+    const float *wscan;   // optional: also write per-block partial max |wscan[0, wscan_n)| to wpart
+    int64_t wscan_n;      //   (the h3 conv3's weight scale, see snk_conv_h3.hpp)
+    float *wpart;
 };
 struct Conv1Pair {
     Conv1Args g[2];
@@ -585,6 +611,10 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
     __shared__ const int8_t *pbase[8 * C];
     if ((int)threadIdx.x < ns * C) pbase[threadIdx.x] = src.plane(s0 + threadIdx.x / C, threadIdx.x % C);
     for (int i = threadIdx.x; i < NS * C * plane; i += blockDim.x) sx[i] = 0.0f;
+    if (ca.wscan) {   // block-uniform
+        __shared__ float red4[4];
+        wmax_block(ca.wscan, ca.wscan_n, ca.wpart, red4);
+    }
     __syncthreads();
     const int nel = ns * C * ncell;
     for (int i0 = 0; i0 < nel; i0 += 8 * 256) {
@@ -1025,7 +1055,7 @@ void qwork_free(QWork &w) {
     for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a2b, (void *)w.a1b, (void *)w.a3, (void *)w.slab, (void *)w.cslab,
                     (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.x0, (void *)w.target,
-                    (void *)w.loss})
+                    (void *)w.loss, (void *)w.wmax_part})
         dfree(p);
     w = QWork{};
 }
@@ -1075,6 +1105,7 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     w.slab = dalloc<float>((size_t)slab);
     w.h1 = dalloc<float>((size_t)cap * 64);
     w.q = dalloc<float>((size_t)cap * 3);
+    w.wmax_part = dalloc<float>((size_t)std::max<int64_t>(cap, 256));
     if (tr) {
         w.has_train = 1;
         w.dq = dalloc<float>((size_t)cap * 3);
@@ -1090,8 +1121,22 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
 
 // ---------------------------------------------------------------- forward
 // conv1 .. Dense1 (layers lo..hi) of ng nets over S samples each, one launch per layer
+// conv3 of this forward on the fp16 h3 kernel (snk_conv_h3.hpp): split-precision
+// (x6) nets, large batches, one unsplit launch. SNK_H3S=0: the bf16 x6 kernels.
+static bool h3s_ok(const QLayout &L, const FwdNet *net, int ng, int64_t S) {
+    static const bool on = !getenv("SNK_H3S") || atoi(getenv("SNK_H3S")) != 0;
+    static const int smin = getenv("SNK_X6S_MIN") ? atoi(getenv("SNK_X6S_MIN")) : 1024;
+    for (int g = 0; g < ng; ++g)
+        if (!net[g].wtb) return false;
+    if (getenv("SNK_CONV12")) return false;   // the fused conv1+conv2 kernel writes a2 as x6 planes only
+    return on && S >= smin && conv_h3s_lds(L.bs) && L.Wo == L.bs - 5 &&
+           conv_splits(S * L.Wo * L.Wo * ng, 36) == 1;
+}
+
 static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi) {
     const int bs = L.bs, nc = L.ncell;
+    const bool h3 = h3s_ok(L, net, ng, S);
+    const int64_t n3 = 36LL * 32 * 64;   // conv3 weight image floats
     // x6: conv1 + conv2 fused into one kernel (layer 0; layer 1 is then empty)
     // measured slower than conv1 + conv2 (per-workgroup staging dominates): opt-in
     static const bool use12 = getenv("SNK_CONV12") != nullptr;
@@ -1135,23 +1180,30 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             const FwdNet &n = net[g < ng ? g : 0];
             // x6: a1 also (acting: only) as bf16 planes for conv2
             cp.g[g] = Conv1Args{n.src, n.th + L.off_w1, n.th + L.off_b1, (n.wtb && !n.w->has_train) ? nullptr : n.w->a1,
-                                n.wtb ? n.w->a1b : nullptr, n.w->has_train ? n.w->x0 : nullptr};
+                                n.wtb ? n.w->a1b : nullptr, n.w->has_train ? n.w->x0 : nullptr,
+                                h3 ? n.wt + L.off_t3 : nullptr, n3, h3 ? n.w->wmax_part : nullptr};
         }
         if (L.C == 1)
             conv1_fwd_kernel<1><<<grid, 256, lds, s>>>(cp, S, bs, ns);
         else
             conv1_fwd_kernel<2><<<grid, 256, lds, s>>>(cp, S, bs, ns);
         launch_check("conv1_fwd_kernel");
-        for (int g = 0; g < ng; ++g) net[g].w->x0_valid = net[g].w->has_train ? 1 : 0;
+        for (int g = 0; g < ng; ++g) {
+            net[g].w->x0_valid = net[g].w->has_train ? 1 : 0;
+            net[g].w->wmax_n = h3 ? (int)grid.x : 0;
+            net[g].w->wmax_img = h3 ? net[g].wt + L.off_t3 : nullptr;
+        }
     }
     FwdIO io[2];
     if (lo <= 1 && hi >= 1) {   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
         // x6: a2 also (acting: only) as bf16 planes for conv3; training keeps fp32 a2 for the backward
         for (int g = 0; g < ng; ++g) {
             const FwdNet &n = net[g];
-            io[g] = FwdIO{n.w->a1, n.wt + L.off_t2, n.th + L.off_b2, (n.wtb && !n.w->has_train) ? nullptr : n.w->a2,
+            // h3: conv3 reads fp32 a2 and splits it itself
+            io[g] = FwdIO{n.w->a1, n.wt + L.off_t2, n.th + L.off_b2,
+                          (n.wtb && !n.w->has_train && !h3) ? nullptr : n.w->a2,
                           n.wtb ? n.wtb + 3 * L.off_t2 : nullptr, n.wtb ? n.w->a1b : nullptr,
-                          n.wtb ? n.w->a2b : nullptr, n.w};
+                          (n.wtb && !h3) ? n.w->a2b : nullptr, n.w};
         }
         conv_fwd<16, 32, 3, 1>(io, ng, S * nc, bs, bs, s);
     }
@@ -1159,7 +1211,18 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         for (int g = 0; g < ng; ++g) {
             const FwdNet &n = net[g];
             io[g] = FwdIO{n.w->a2, n.wt + L.off_t3, n.th + L.off_b3, n.w->a3, n.wtb ? n.wtb + 3 * L.off_t3 : nullptr,
-                          n.wtb ? n.w->a2b : nullptr, nullptr, n.w};
+                          (n.wtb && !h3) ? n.w->a2b : nullptr, nullptr, n.w};
+            if (h3) {
+                QWork &w = *n.w;
+                if (!w.wmax_n || w.wmax_img != n.wt + L.off_t3) {   // conv1 did not scan this image
+                    wmax_scan_kernel<<<256, 256, 0, s>>>(n.wt + L.off_t3, n3, w.wmax_part);
+                    launch_check("wmax_scan_kernel");
+                    w.wmax_n = 256;
+                    w.wmax_img = n.wt + L.off_t3;
+                }
+                io[g].wmax = w.wmax_part;
+                io[g].nwmax = w.wmax_n;
+            }
         }
         conv_fwd<32, 64, 6, 0>(io, ng, S * L.Wo * L.Wo, bs, L.Wo, s);
     }

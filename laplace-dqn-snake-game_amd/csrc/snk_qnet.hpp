@@ -73,6 +73,9 @@ struct QWork {
     float *dq = nullptr, *dz1 = nullptr, *dz3 = nullptr, *dz2 = nullptr, *dzc1 = nullptr;
     float *x0 = nullptr;      // input planes as floats, written by the training forward's conv1
     int x0_valid = 0;         // set by the forward that wrote x0 (the unfused conv1 path)
+    float *wmax_part = nullptr;      // h3 conv3: per-block partial max |w| of the conv3 weight image
+    int wmax_n = 0;                  //   valid partials (conv1_fwd_kernel / wmax_scan_kernel wrote them)
+    const float *wmax_img = nullptr; //   of this image
     double *target = nullptr, *loss = nullptr;
     int has_train = 0;
 };

@@ -188,9 +188,10 @@ def test_x6_split_forward_matches_fp32_and_oracle(snk, bs, C, B, monkeypatch):
         assert e6.mean() <= 2 * e32.mean() + 1e-8, (scale, e6.mean(), e32.mean())
 
 
-def test_large_batch_forward_x6s_vs_oracle(snk):
-    """B >= 1024 routes conv3 through conv_x6s_kernel (four samples' planes in
-    LDS). 1101 samples leave a partial last group of one sample."""
+def test_large_batch_forward_h3s_vs_oracle(snk):
+    """B >= 1024 routes conv3 through conv_h3s_kernel (fp16 h3 split, four
+    samples' inputs in LDS). 1101 samples leave a partial last group of one
+    sample. Tolerance: |q - q_ref| <= 1e-5 * max(1, |q_ref|)."""
     bs, C, B = 12, 2, 1101
     rng = np.random.default_rng(11)
     m = snk.DQNModel(bs, 3, n_frames=C, seed=13)
@@ -198,6 +199,37 @@ def test_large_batch_forward_x6s_vs_oracle(snk):
     q = m(x)
     qref = oracle.qnet_forward(bs, C, m.get_params(), x)
     assert _qclose(q, qref), np.abs(q - qref).max()
+
+
+@pytest.mark.parametrize("scale", [1.0, 3.0, 1e-3, 40.0])
+def test_h3s_error_class_vs_fp32(snk, scale, monkeypatch):
+    """The h3 conv3 (fp16 parts of power-of-two-scaled operands, 3 MFMAs per
+    product) keeps the error class of the exact-fp32 MFMA forward
+    (SNK_CONV=fp32) across weight scales that move activations over 10+
+    binades (1e-3x: tiny activations, where unscaled fp16 would underflow;
+    40x: |Q| ~ 1e8, where it would overflow): element-max and mean error
+    against the fp64 oracle within 2x the fp32 forward's, and within 1e-5
+    at the init scale."""
+    bs, C, B = 12, 2, 1030
+    rng = np.random.default_rng(7)
+    mh = snk.DQNModel(bs, 3, n_frames=C, seed=5)
+    monkeypatch.setenv("SNK_CONV", "fp32")
+    m32 = snk.DQNModel(bs, 3, n_frames=C, seed=5)
+    monkeypatch.delenv("SNK_CONV")
+    x = rng.integers(-1, 3, size=(B, C, bs * bs)).astype(np.float32)
+    p = mh.get_params() * np.float32(scale)
+    mh.set_params(p)
+    m32.set_params(p)
+    qh, q32 = mh.forward(x), m32.forward(x)
+    qref = oracle.qnet_forward(bs, C, p, x)
+    if scale == 1.0:
+        assert _qclose(qh, qref) and _qclose(q32, qref)
+    # relative error, floored at 1e-3 of the largest |Q| (scale-free)
+    den = np.maximum(np.abs(qref), 1e-3 * np.abs(qref).max())
+    eh = np.abs(qh - qref) / den
+    e32 = np.abs(q32 - qref) / den
+    assert eh.max() <= 2 * e32.max() + 1e-7, (scale, eh.max(), e32.max())
+    assert eh.mean() <= 2 * e32.mean() + 1e-8, (scale, eh.mean(), e32.mean())
 
 
 _X6S_SCRIPT = r"""
@@ -212,17 +244,21 @@ np.save(sys.argv[2], m(x))
 """
 
 
-def test_x6s_bitexact_with_x6m16(tmp_path):
-    """conv_x6s accumulates the six part products in x6m16's order: the Q
-    values of a 2050-sample forward are identical with SNK_X6S=1 and 0."""
+def test_x6s_bitexact_with_x6m16_and_h3s_close(tmp_path):
+    """With the h3 kernel off (SNK_H3S=0), conv_x6s accumulates the six part
+    products in x6m16's order: the Q values of a 2050-sample forward are
+    identical with SNK_X6S=1 and 0. The default (h3s) forward agrees with
+    them to 1e-5 * max(1, |q|)."""
     import os
     import subprocess
     import sys
     repo = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
     out = {}
-    for v in ("1", "0"):
-        f = str(tmp_path / f"q{v}.npy")
-        env = dict(os.environ, SNK_X6S=v)
+    for tag, envs in (("x6s", {"SNK_H3S": "0", "SNK_X6S": "1"}), ("m16", {"SNK_H3S": "0", "SNK_X6S": "0"}),
+                      ("h3s", {})):
+        f = str(tmp_path / f"q{tag}.npy")
+        env = dict(os.environ, **envs)
         subprocess.run([sys.executable, "-c", _X6S_SCRIPT, repo, f], env=env, check=True, timeout=300)
-        out[v] = np.load(f)
-    assert np.array_equal(out["1"], out["0"])
+        out[tag] = np.load(f)
+    assert np.array_equal(out["x6s"], out["m16"])
+    assert _qclose(out["h3s"], out["x6s"])
