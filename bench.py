@@ -30,7 +30,26 @@ sys.path.insert(0, REPO)
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
 PEAK_BF16_TFLOPS = 2516.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak (2.5 PF, no sparsity)
 X6_PRODUCTS = 6            # bf16 MFMA products per fp32 product in the exact-split forward
+H3_PRODUCTS = 3            # fp16 MFMA products per fp32 product in the h3 conv3 (snk_conv_h3.hpp)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def _latest_traffic(h3: bool):
+    """HBM bytes per conv3 act-forward launch from the newest committed PMC pass
+    (profiles/*_conv3_traffic.json, written by tools/traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 --pmc runs; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md's gfx950 note), for the kernel this run uses."""
+    import glob
+    kern = "conv_h3s_kernel" if h3 else "conv_x6"
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_conv3_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel", "").startswith(kern):
+            d["source"] = os.path.relpath(f, REPO) + ": " + d.get("how", "")
+            return d
+    return None
 
 
 def parse():
@@ -216,8 +235,9 @@ def main():
                    "n_envs_per_gpu": n, "board_size": bs, "n_frames": C, "replay_capacity": args.capacity,
                    "batch_size": 64, "epsilon": args.epsilon, "parallelism": f"dp{world}" if world > 1 else "none",
                    "hipgraph": graph,
-                   "gemm_arithmetic": ("f32 operands split exactly into 3 bf16 parts, 6 bf16 MFMA products, "
-                                       "f32 accumulation (fp32 error class)" if os.environ.get("SNK_CONV", "") != "fp32"
+                   "gemm_arithmetic": ("act-forward conv3: f32 operands as fp16 hi/lo parts of power-of-two-scaled "
+                                       "values, 3 f16 MFMA products; other GEMMs: 3-way bf16 split, 6 bf16 MFMA "
+                                       "products; f32 accumulation throughout" if os.environ.get("SNK_CONV", "") != "fp32"
                                        else "native f32 MFMA")},
         "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
                         "food_faults": faults},
@@ -237,14 +257,22 @@ def main():
         # bf16 MFMA (SNK_CONV=fp32: native f32 MFMA): the fp32-equivalent peak is
         # the bf16 dense peak / 6
         x6 = os.environ.get("SNK_CONV", "") != "fp32"
-        peak = PEAK_BF16_TFLOPS / X6_PRODUCTS if x6 else PEAK_FP32_TFLOPS
+        # >= 1024 samples at bs 8..13: conv_h3s_kernel (3 fp16 products per fp32 product)
+        h3 = x6 and os.environ.get("SNK_H3S", "1") != "0" and n >= 1024 and 8 <= bs <= 13
+        nprod = H3_PRODUCTS if h3 else X6_PRODUCTS
+        peak = PEAK_BF16_TFLOPS / nprod if x6 else PEAK_FP32_TFLOPS
+        kname = ("conv_h3s_kernel: fp16 h3 split on v_mfma_f32_16x16x32_f16" if h3 else
+                 "bf16x6 split on v_mfma_f32_16x16x32_bf16" if x6 else "v_mfma_f32_32x32x2_f32")
         out["roofline"] = {"bound": "mfma",
-                           "kernel": "conv3 implicit GEMM, act forward (" +
-                                     ("bf16x6 split on v_mfma_f32_16x16x32_bf16" if x6 else "v_mfma_f32_32x32x2_f32") + ")",
+                           "kernel": "conv3 implicit GEMM, act forward (" + kname + ")",
                            "achieved": tf, "peak": peak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / peak,
                            "traffic": None, "avg_launch_ms": ms[2], "flop_per_launch": flop_conv3,
-                           "bf16_mfma_tflops_executed": tf * X6_PRODUCTS if x6 else None,
+                           "half_mfma_tflops_executed": tf * nprod if x6 else None,
                            "fp32_mfma_peak": PEAK_FP32_TFLOPS}
+        tr_file = _latest_traffic(h3)
+        if tr_file:
+            out["roofline"]["traffic"] = tr_file["bytes_per_launch"]
+            out["roofline"]["traffic_source"] = tr_file["source"]
         out["act_forward_ms"] = {"conv1": ms[0], "conv2": ms[1], "conv3": ms[2], "dense1": ms[3], "head": ms[4],
                                  "total": float(ms.sum()),
                                  "tflops_total": flop_total / (ms.sum() * 1e-3) / 1e12}

@@ -89,7 +89,9 @@ __global__ __launch_bounds__(256) void wmax_scan_kernel(const float *__restrict_
 // conv3 (CK = 32 -> CN = 64, pad 0, EPI_BIAS_RELU) on the h3 split; ConvArgs:
 // x = fp32 input [S][HIN^2][32], w = fp32 weight image [kk][64][32],
 // wmax/nwmax = partial max |w| of that image; out (fp32) and/or outb (x6 planes)
-template <int KS, int EPI>
+// HIN (= board side) is a template constant: the index arithmetic of the
+// staging and of the epilogue then has no integer division.
+template <int KS, int EPI, int HIN>
 __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     constexpr int CN = 64, CK = 32, NSG = 4, NB = 2 * CN * CK / 8;   // 512 16-byte chunks per offset
     constexpr int NKK = KS * KS, NLA = 11;   // A float4 loads per thread: 4 samples of <= 13 x 13 x 32
@@ -102,12 +104,14 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     u32x4 *As = h3s_lds + 2 * NB;   // A image, conv_x6s_kernel's slot map with two planes per group
     u32x2 *Bs2 = reinterpret_cast<u32x2 *>(Bs);
     u32x2 *As2 = reinterpret_cast<u32x2 *>(As);
-    const int hin = a.HIN, ho = a.HOUT, ho2 = ho * ho, hin2 = hin * hin;
-    const int XW = ho + 8, PL = (hin * XW + 3) & ~3, GG = 2 * PL, XS = 4 * GG + 4;
+    constexpr int hin = HIN, ho = HIN - KS + 1, ho2 = ho * ho, hin2 = hin * hin;
+    constexpr int XW = ho + 8, PL = (hin * XW + 3) & ~3, GG = 2 * PL, XS = 4 * GG + 4;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
     const int s0 = blockIdx.x * NSG;
     const int ns = min(NSG, S - s0);
+    uint64_t ts[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0;   // SNK_H3S_DBG phase stamps
+    if (a.dbg) { ts[0] = clock64(); rt0 = wall_clock64(); }
 
     // B register sets: set kk & 1 carries B(kk) (fp32, unsplit) from global to LDS
     f32x4 bst[2];
@@ -125,7 +129,8 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     b_load(1, 1);
 
     // A: the group's fp32 inputs, then one max per sample and the weight max
-    const int per = hin2 * 8, n4 = ns * per;
+    constexpr int per = hin2 * 8;
+    const int n4 = ns * per;
     const f32x4 *src = reinterpret_cast<const f32x4 *>(a.x) + (int64_t)s0 * per;
     f32x4 av[NLA];
 #pragma unroll
@@ -149,10 +154,12 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     sm2 = wave_max(sm2);
     sm3 = wave_max(sm3);
     wm = wave_max(wm);
+    if (a.dbg) ts[1] = clock64();
     if (lane == 0) {
         red[wave][0] = sm0; red[wave][1] = sm1; red[wave][2] = sm2; red[wave][3] = sm3; red[wave][4] = wm;
     }
     __syncthreads();
+    if (a.dbg) ts[2] = clock64();
     int ea[NSG];
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
@@ -180,11 +187,12 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     b_store(0, 0);
     b_store(1, 1);
 
-    const int T = (NSG * ho2 + 15) / 16;
+    constexpr int T = (NSG * ho2 + 15) / 16;
     const int rg = wave >> 1, cg = wave & 1;
     const int nt = __builtin_amdgcn_readfirstlane(T > rg ? (T - rg + 3) / 4 : 0);
     const int bslot = (cg * 32 + r) * 4 + (g ^ ((4 - ((r >> 2) & 3)) & 3));
     __syncthreads();
+    if (a.dbg) ts[3] = clock64();
 
     // conv_x6s_kernel's pipeline (see there): offset kk's MFMAs on fragments
     // read during kk-1, B(kk+2) split into LDS while B(kk+3) is in flight
@@ -247,14 +255,46 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
         Frag f0, f1;
         frag_read(0, f0);
         b_load(2, 0);
-        __syncthreads();
+        __syncthreads();   // every wave has B(0) in registers before step 0 overwrites Bs[0]
         static_assert(NKK % 2 == 0, "offsets come in pairs");
         for (int kk = 0; kk < NKK; kk += 2) {
             step(kk, f0, f1, 0);
             step(kk + 1, f1, f0, 1);
         }
+        if (a.dbg) ts[4] = clock64();
 
         // acc[k][ct][e]: tile row 4g + e = position 4t + g of sample e; column 16ct + r
+        if (!a.outb) {
+            // through LDS (the A image is dead after the last offset's barrier): rows of
+            // CS floats (CS = 80: the two 32-lane halves of a ds_write_b32 land 16 banks
+            // apart), then the group's contiguous [ns*ho2][64] block as float4 stores
+            constexpr int CS = 80;
+            static_assert(NSG * ho2 * CS * 4 <= 4 * XS * 16, "output staging fits the A image");
+            float *Cs = reinterpret_cast<float *>(As);
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+                const int p = 4 * (rg + 4 * k) + g;
+                if (p >= ho2) continue;
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    const int col = cg * 32 + ct * 16 + r;
+                    const float bv = EPI == EPI_BIAS_RELU ? a.bias[col] : 0.0f;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float v = __builtin_ldexpf(acc[k][ct][e], -(ea[e] + ew)) + bv;
+                        Cs[(e * ho2 + p) * CS + col] = v > 0.0f ? v : 0.0f;
+                    }
+                }
+            }
+            __syncthreads();
+            if (a.out) {
+                const int n4o = ns * ho2 * 16;
+                f32x4 *o4 = reinterpret_cast<f32x4 *>(a.out + (int64_t)s0 * ho2 * CN);
+                const f32x4 *c4 = reinterpret_cast<const f32x4 *>(Cs);
+                for (int q = tid; q < n4o; q += 512) o4[q] = c4[(q >> 4) * (CS / 4) + (q & 15)];
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < NT; ++k) {
             const int p = 4 * (rg + 4 * k) + g;
@@ -270,11 +310,9 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
                     float v = __builtin_ldexpf(acc[k][ct][e], -(ea[e] + ew)) + bv;
                     v = v > 0.0f ? v : 0.0f;
                     if (a.out) a.out[row * CN + col] = v;
-                    if (a.outb) {
-                        uint16_t *pb = a.outb + row * 3 * CN + col;
+                    uint16_t *pb = a.outb + row * 3 * CN + col;
 #pragma unroll
-                        for (int pl = 0; pl < 3; ++pl) pb[pl * CN] = split_part(v, pl);
-                    }
+                    for (int pl = 0; pl < 3; ++pl) pb[pl * CN] = split_part(v, pl);
                 }
             }
         }
@@ -283,6 +321,13 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     else if (nt == 3) run(std::integral_constant<int, 3>{});
     else if (nt == 2) run(std::integral_constant<int, 2>{});
     else run(std::integral_constant<int, 1>{});
+    if (a.dbg && lane == 0) {
+        ts[5] = clock64();
+        uint64_t *d = a.dbg + ((int64_t)blockIdx.x * 8 + wave) * 8;
+        for (int q = 0; q < 6; ++q) d[q] = ts[q];
+        d[6] = rt0;
+        d[7] = wall_clock64();
+    }
 }
 
 // dynamic LDS bytes of conv_h3s_kernel for an HIN x HIN input (0: does not fit)

@@ -9,6 +9,7 @@
 // weight-gradient loaders; RMSProp (Optimisers.jl, utils.jl:429,466) is
 // element-wise over the packed parameter vector.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -392,6 +393,54 @@ static ConvPair make_conv_pair(const ConvArgs *ga, int ng, int &splits, const ui
     return pr;
 }
 
+// conv3 on the h3 kernel (snk_conv_h3.hpp) for an HIN x HIN input
+template <int KS, int EPI, int HIN>
+static void h3s_launch(const ConvPair &pr, int ng, int splits, hipStream_t s) {
+    const ConvArgs &a = pr.g[0];
+    const int ho2 = a.HOUT * a.HOUT;
+    const int S = a.M / ho2;
+    const size_t lds = conv_h3s_lds(a.HIN);
+    SNK_CHECK(splits == 1 && lds && S * ho2 == a.M && a.HOUT == HIN - KS + 1 && !a.xb && a.x && a.w &&
+                  (ng == 1 || pr.g[1].wmax),
+              SNK_ERR_INTERNAL, "h3s conv3 geometry");
+    static size_t attr = 0;   // dynamic bytes only: the kernel's static LDS counts against the 160 KB
+    if (lds > attr) {
+        SNK_HIP(hipFuncSetAttribute((const void *)conv_h3s_kernel<KS, EPI, HIN>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = lds;
+    }
+    const dim3 g3((unsigned)ceil_div(S, 4), 1, (unsigned)ng);
+    static const bool dbg = getenv("SNK_H3S_DBG") != nullptr;
+    if (dbg && ng == 1) {   // experiment: per-workgroup phase timestamps to stderr
+        const size_t nd = (size_t)g3.x * 64;
+        uint64_t *d = dalloc<uint64_t>(nd);
+        ConvPair p2 = pr;
+        p2.g[0].dbg = d;
+        conv_h3s_kernel<KS, EPI, HIN><<<g3, 512, lds, s>>>(p2, S);
+        launch_check("conv_h3s_kernel");
+        std::vector<uint64_t> hbuf(nd);
+        SNK_HIP(hipMemcpyAsync(hbuf.data(), d, nd * 8, hipMemcpyDeviceToHost, s));
+        SNK_HIP(hipStreamSynchronize(s));
+        dfree(d);
+        double ph[5] = {0, 0, 0, 0, 0};
+        uint64_t rmin = ~0ull, rmax = 0;
+        int n = 0;
+        for (size_t b = 0; b < g3.x; ++b)
+            for (int w = 0; w < 8; ++w) {
+                const uint64_t *q = &hbuf[(b * 8 + w) * 8];
+                for (int k = 0; k < 5; ++k) ph[k] += (double)(q[k + 1] - q[k]);
+                rmin = std::min(rmin, q[6]); rmax = std::max(rmax, q[7]);
+                ++n;
+            }
+        fprintf(stderr, "h3s dbg: %u WGs, per-wave cycles: A loads %.0f | reduce+barrier %.0f | split+write "
+                "%.0f | loop %.0f | epilogue %.0f; wall %.1f us\n", g3.x, ph[0] / n, ph[1] / n, ph[2] / n,
+                ph[3] / n, ph[4] / n, (double)(rmax - rmin) / 100.0);
+        return;
+    }
+    conv_h3s_kernel<KS, EPI, HIN><<<g3, 512, lds, s>>>(pr, S);
+    launch_check("conv_h3s_kernel");
+}
+
 template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
 static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, const uint16_t *const *wb = nullptr) {
     const ConvPair pr = make_conv_pair(ga, ng, splits, wb);
@@ -399,22 +448,15 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
     dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)splits, (unsigned)ng);
     if constexpr (MODE == MODE_FWD && CN == 64 && CK == 32 && KS == 6 && PAD == 0 && EPI == EPI_BIAS_RELU) {
         if (a.wmax) {   // fp16 h3 split, four samples resident in LDS (forward_layers chose it: h3s_ok)
-            const int ho2 = a.HOUT * a.HOUT;
-            const int S = a.M / ho2;
-            const size_t lds = conv_h3s_lds(a.HIN);
-            SNK_CHECK(splits == 1 && lds && S * ho2 == a.M && a.HOUT == a.HIN - 5 && !a.xb && a.x && a.w &&
-                          (ng == 1 || pr.g[1].wmax),
-                      SNK_ERR_INTERNAL, "h3s conv3 geometry");
-            static bool attr = false;
-            if (!attr) {
-                SNK_HIP(hipFuncSetAttribute((const void *)conv_h3s_kernel<KS, EPI>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-                attr = true;
+            switch (a.HIN) {
+                case 8: h3s_launch<KS, EPI, 8>(pr, ng, splits, s); return;
+                case 9: h3s_launch<KS, EPI, 9>(pr, ng, splits, s); return;
+                case 10: h3s_launch<KS, EPI, 10>(pr, ng, splits, s); return;
+                case 11: h3s_launch<KS, EPI, 11>(pr, ng, splits, s); return;
+                case 12: h3s_launch<KS, EPI, 12>(pr, ng, splits, s); return;
+                case 13: h3s_launch<KS, EPI, 13>(pr, ng, splits, s); return;
+                default: SNK_CHECK(false, SNK_ERR_INTERNAL, "h3s conv3: board side outside 8..13");
             }
-            const dim3 g3((unsigned)ceil_div(S, 4), 1, (unsigned)ng);
-            conv_h3s_kernel<KS, EPI><<<g3, 512, lds, s>>>(pr, S);
-            launch_check("conv_h3s_kernel");
-            return;
         }
     }
     if constexpr (MODE != MODE_DX) {
@@ -1129,7 +1171,7 @@ static bool h3s_ok(const QLayout &L, const FwdNet *net, int ng, int64_t S) {
     for (int g = 0; g < ng; ++g)
         if (!net[g].wtb) return false;
     if (getenv("SNK_CONV12")) return false;   // the fused conv1+conv2 kernel writes a2 as x6 planes only
-    return on && S >= smin && conv_h3s_lds(L.bs) && L.Wo == L.bs - 5 &&
+    return on && S >= smin && L.bs >= 8 && L.bs <= 13 && conv_h3s_lds(L.bs) && L.Wo == L.bs - 5 &&
            conv_splits(S * L.Wo * L.Wo * ng, 36) == 1;
 }
 
