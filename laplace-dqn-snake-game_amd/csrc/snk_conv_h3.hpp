@@ -80,7 +80,7 @@ __device__ __forceinline__ void wmax_block(const float *__restrict__ w, int64_t 
     if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
 }
 
-__global__ __launch_bounds__(256) void wmax_scan_kernel(const float *__restrict__ w, int64_t n,
+static __global__ __launch_bounds__(256) void wmax_scan_kernel(const float *__restrict__ w, int64_t n,
                                                         float *__restrict__ part) {
     __shared__ float red4[4];
     wmax_block(w, n, part, red4);

@@ -161,19 +161,24 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s) {
     SNK_CHECK(a.K % 4 == 0 && a.ld % 4 == 0 && a.kchunk % 4 == 0, SNK_ERR_INTERNAL, "syrk: K/ld not multiples of 4");
     SNK_CHECK(a.ntiles < (int64_t)1 << 31 && z <= 65535, SNK_ERR_INVALID, "syrk: problem too large");
     dim3 grid((unsigned)a.ntiles, (unsigned)z);
-    // bf16 x6 split MFMA by default; SNK_SYRK=fp32: the exact-f32 32x32x2 MFMA
-    static const bool f32 = getenv("SNK_SYRK") && strcmp(getenv("SNK_SYRK"), "fp32") == 0;
+    // SNK_SYRK=fp32: the exact-f32 32x32x2 MFMA everywhere; =x6: the bf16 x6 split also
+    // for pre-split (h3) callers; default: x6, and h3 where the caller pre-split x
+    static const char *env = getenv("SNK_SYRK");
+    static const bool f32 = env && strcmp(env, "fp32") == 0, nox3 = env && strcmp(env, "x6") == 0;
     if (f32) {
         switch (out) {
-            case SYRK_F32: syrk_kernel<SYRK_F32, false><<<grid, 256, 0, s>>>(a); break;
-            case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, false><<<grid, 256, 0, s>>>(a); break;
-            default: syrk_kernel<SYRK_DENSE_ADD, false><<<grid, 256, 0, s>>>(a); break;
+            case SYRK_F32: syrk_kernel<SYRK_F32, SY_F32><<<grid, 256, 0, s>>>(a); break;
+            case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, SY_F32><<<grid, 256, 0, s>>>(a); break;
+            default: syrk_kernel<SYRK_DENSE_ADD, SY_F32><<<grid, 256, 0, s>>>(a); break;
         }
+    } else if (a.xh && !nox3) {
+        SNK_CHECK(out == SYRK_F32 && z == 1 && a.ldh % SY_KS == 0 && a.xl && a.xe, SNK_ERR_INTERNAL, "syrk h3 arguments");
+        syrk_kernel<SYRK_F32, SY_H3><<<grid, 256, 0, s>>>(a);
     } else {
         switch (out) {
-            case SYRK_F32: syrk_kernel<SYRK_F32, true><<<grid, 256, 0, s>>>(a); break;
-            case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, true><<<grid, 256, 0, s>>>(a); break;
-            default: syrk_kernel<SYRK_DENSE_ADD, true><<<grid, 256, 0, s>>>(a); break;
+            case SYRK_F32: syrk_kernel<SYRK_F32, SY_X6><<<grid, 256, 0, s>>>(a); break;
+            case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, SY_X6><<<grid, 256, 0, s>>>(a); break;
+            default: syrk_kernel<SYRK_DENSE_ADD, SY_X6><<<grid, 256, 0, s>>>(a); break;
         }
     }
     launch_check("syrk_kernel");
@@ -382,6 +387,26 @@ extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_d
         if (ms_out) SNK_HIP(hipEventRecord(ev[2], s));
         SyrkArgs a{};
         a.x = m->jbuf; a.ld = Kc; a.K = Kc; a.kchunk = Kc; a.N = (int)n; a.g32 = G_dev; a.ldg = n;
+        static const char *senv = getenv("SNK_SYRK");
+        if (!senv || strcmp(senv, "h3") == 0) {
+            // h3 Gram: rows pre-split once into scaled fp16 planes (snk_syrk.hpp h3_rows_kernel)
+            const int64_t ldh = (Kc + SY_KS - 1) / SY_KS * SY_KS;
+            if (2 * n * ldh > m->jplanes_halves) {
+                (void)hipStreamSynchronize(s);
+                dfree(m->jplanes);
+                m->jplanes = dalloc<uint16_t>(2 * n * ldh);
+                m->jplanes_halves = 2 * n * ldh;
+            }
+            if (n > m->jexp_cap) {
+                (void)hipStreamSynchronize(s);
+                dfree(m->jexp);
+                m->jexp = dalloc<int32_t>(n);
+                m->jexp_cap = n;
+            }
+            h3_rows_kernel<<<(unsigned)n, 256, 0, s>>>(m->jbuf, Kc, Kc, m->jplanes, m->jplanes + n * ldh, m->jexp, ldh);
+            launch_check("h3_rows_kernel");
+            a.xh = m->jplanes; a.xl = m->jplanes + n * ldh; a.xe = m->jexp; a.ldh = ldh;
+        }
         syrk_launch(SYRK_F32, a, 1, s);
         if (ms_out) SNK_HIP(hipEventRecord(ev[3], s));
         SyrkArgs d{};

@@ -20,7 +20,7 @@
 // (1024 k), so the error is that of 1024-long fp32 dot products summed in
 // fp64, independent of K (K is ~79k for the Jacobian Gram).
 #pragma once
-#include "snk_conv_x6.hpp"
+#include "snk_conv_h3.hpp"
 
 namespace snk {
 
@@ -330,13 +330,170 @@ struct SyrkArgs {
     const float *z, *hh;
     const uint8_t *act;
     int64_t ldz;
+    // SY_H3: x pre-split by h3_rows_kernel: fp16 planes xh / xl [N][ldh] (ldh a multiple
+    // of SY_KS, zero tail), row i scaled by 2^xe[i]
+    const uint16_t *xh, *xl;
+    const int32_t *xe;
+    int64_t ldh;
 };
+
+// h3 operands for the Gram (snk_conv_h3.hpp's split, one scale per ROW):
+// row i of x [N][ld] -> fp16 planes h, l of x * 2^e_i with e_i = h3_exp(max_k |x_ik|),
+// zero-padded to ldh. One workgroup per row: the max pass, then the split pass
+// (the row is L2-resident by then). G_ij = 2^-(e_i + e_j) (Xs Xs')_ij exactly.
+static __global__ __launch_bounds__(256) void h3_rows_kernel(const float *__restrict__ x, int64_t ld, int64_t K,
+                                                      uint16_t *__restrict__ xh, uint16_t *__restrict__ xl,
+                                                      int32_t *__restrict__ xe, int64_t ldh) {
+    __shared__ float red4[4];
+    const int64_t row = blockIdx.x;
+    const f32x4 *src = reinterpret_cast<const f32x4 *>(x + row * ld);
+    const int64_t n4 = K / 4, nh4 = ldh / 4;
+    float m = 0.0f;
+    for (int64_t i = threadIdx.x; i < n4; i += 256) {
+        const f32x4 v = src[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+    __syncthreads();
+    const int e = h3_exp(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
+    if (threadIdx.x == 0) xe[row] = e;
+    u32x2 *oh = reinterpret_cast<u32x2 *>(xh + row * ldh), *ol = reinterpret_cast<u32x2 *>(xl + row * ldh);
+    for (int64_t i = threadIdx.x; i < nh4; i += 256) {
+        const f32x4 v = i < n4 ? src[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        u32x2 h, l;
+        h3_split4(v, e, h, l);
+        oh[i] = h;
+        ol[i] = l;
+    }
+}
+
+// The Gram tile on pre-split h3 planes: each 32-k stage of both 128-row blocks
+// is loaded as fp16 h / l pieces (16 B = 8 k per plane), parked in LDS
+// ([op][plane][row][40 halves], as the x6 loop) with no conversion work, and
+// each wave runs 2 k-steps x 2 x 2 tiles x 3 part products of
+// v_mfma_f32_32x32x16_f16: 768 MFMA cycles per stage (x6: 1536). Rows past N
+// read row N-1 (their results are never stored); the zero tail of ldh covers
+// the k range. Accumulators and fp64 flushing as syrk_loop; the 2^-(e_i+e_j)
+// scale is applied in the kernel epilogue.
+template <bool FLUSH>
+__device__ __forceinline__ void syrk_loop_h3(const SyrkArgs &a, int bi, int bj, SyrkX6Lds &s, f32x16 (&acc)[2][2],
+                                             double (&accd)[2][2][16]) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+    const int N = a.N;
+    const int c8 = 8 * (tid & 3);
+    const uint16_t *ph[2][2], *pl[2][2];   // [op][q]
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int ra = bi * SY_T + (tid >> 2) + 64 * q, rb = bj * SY_T + (tid >> 2) + 64 * q;
+        const int64_t oa = (int64_t)(ra < N ? ra : N - 1) * a.ldh + c8, ob = (int64_t)(rb < N ? rb : N - 1) * a.ldh + c8;
+        ph[0][q] = a.xh + oa; pl[0][q] = a.xl + oa;
+        ph[1][q] = a.xh + ob; pl[1][q] = a.xl + ob;
+    }
+    const int nst = (int)(a.ldh / SY_KS);
+    struct Stage {
+        u32x4 v[2][2][2];   // [op][q][plane]
+    };
+    Stage rs[3];
+    auto issue = [&](int st, Stage &g) {
+        const int64_t k = (int64_t)st * SY_KS;
+#pragma unroll
+        for (int op = 0; op < 2; ++op)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                g.v[op][q][0] = *reinterpret_cast<const u32x4 *>(ph[op][q] + k);
+                g.v[op][q][1] = *reinterpret_cast<const u32x4 *>(pl[op][q] + k);
+            }
+    };
+    auto park_piece = [&](int buf, const Stage &g, int op, int q) {
+        const int off = ((tid >> 2) + 64 * q) * SX_LD + c8;
+        *reinterpret_cast<u32x4 *>(&s.p[buf][op][0][off]) = g.v[op][q][0];
+        *reinterpret_cast<u32x4 *>(&s.p[buf][op][1][off]) = g.v[op][q][1];
+    };
+    auto compute_park = [&](int buf, bool pk, const Stage &nx) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            f16x8 fa[2][2], fb[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int pn = 0; pn < 2; ++pn) {
+                    fa[i][pn] = as_h(*reinterpret_cast<const u32x4 *>(
+                        &s.p[buf][0][pn][(wr + 32 * i + r) * SX_LD + 16 * ks + 8 * h]));
+                    fb[i][pn] = as_h(*reinterpret_cast<const u32x4 *>(
+                        &s.p[buf][1][pn][(wc + 32 * i + r) * SX_LD + 16 * ks + 8 * h]));
+                }
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    f32x16 c = acc[mi][ni];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[mi][1], fb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[mi][0], fb[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[mi][0], fb[ni][0], c, 0, 0, 0);
+                    acc[mi][ni] = c;
+                    if (ks == 1 && pk) park_piece(buf ^ 1, nx, mi, ni);
+                }
+        }
+    };
+    auto flush = [&]() {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    accd[mi][ni][g] += (double)acc[mi][ni][g];
+                    acc[mi][ni][g] = 0.0f;
+                }
+    };
+    // syrk_loop_x6's rotation: stage st+3 loads into set st % 3, stage st+1 is
+    // parked after this stage's MFMAs (park_piece(op = mi, q = ni) covers the
+    // four pieces of a stage)
+    auto step = [&](int st, auto bufc, Stage &ld3, Stage &nx) {
+        constexpr int BUF = decltype(bufc)::value;
+        const bool more = st + 1 < nst;
+        issue(st + 3 < nst ? st + 3 : nst - 1, ld3);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_park(BUF, more, nx);
+        if (FLUSH && (st % SY_FLUSH == SY_FLUSH - 1 || !more)) flush();
+        __syncthreads();
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    issue(0, rs[0]);
+    if (nst > 1) issue(1, rs[1]);
+    if (nst > 2) issue(2, rs[2]);
+#pragma unroll
+    for (int op = 0; op < 2; ++op)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) park_piece(0, rs[0], op, q);
+    __syncthreads();
+    int st = 0;
+    for (; st + 6 <= nst; st += 6) {
+        step(st, B0{}, rs[0], rs[1]);
+        step(st + 1, B1{}, rs[1], rs[2]);
+        step(st + 2, B0{}, rs[2], rs[0]);
+        step(st + 3, B1{}, rs[0], rs[1]);
+        step(st + 4, B0{}, rs[1], rs[2]);
+        step(st + 5, B1{}, rs[2], rs[0]);
+    }
+    if (st < nst) step(st, B0{}, rs[0], rs[1]);
+    if (st + 1 < nst) step(st + 1, B1{}, rs[1], rs[2]);
+    if (st + 2 < nst) step(st + 2, B0{}, rs[2], rs[0]);
+    if (st + 3 < nst) step(st + 3, B1{}, rs[0], rs[1]);
+    if (st + 4 < nst) step(st + 4, B0{}, rs[1], rs[2]);
+}
 
 union SyrkSmem {
     SyrkLds f32;
     SyrkX6Lds x6;
 };
-template <int OUT, bool X6>
+enum SyrkMode { SY_F32 = 0, SY_X6 = 1, SY_H3 = 2 };
+
+template <int OUT, int MODE>
 __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
     __shared__ __attribute__((aligned(16))) SyrkSmem sm;
     SyrkLds &s = sm.f32;
@@ -362,8 +519,10 @@ __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
             for (int g = 0; g < 16; ++g) accd[mi][ni][g] = 0.0;
     const int64_t k0 = (int64_t)blockIdx.y * a.kchunk;
     const int64_t k1 = k0 + a.kchunk < a.K ? k0 + a.kchunk : a.K;
-    if (k0 < k1) {
-        if (X6)
+    if (MODE == SY_H3) {
+        syrk_loop_h3<true>(a, bi, bj, sm.x6, acc, accd);
+    } else if (k0 < k1) {
+        if (MODE == SY_X6)
             syrk_loop_x6<true>(a.x, a.ld, a.N, k0, k1, bi, bj, sm.x6, acc, accd);
         else
             syrk_loop<true>(a.x, a.ld, a.N, k0, k1, bi, bj, s, acc, accd);
@@ -394,6 +553,7 @@ __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
             for (int g = 0; g < 16; ++g) {
                 const int row = bi * SY_T + wr + mi * 32 + acc_row(g, lane);
                 if (row >= a.N) continue;
+                if (MODE == SY_H3) accd[mi][ni][g] = __builtin_ldexp(accd[mi][ni][g], -(a.xe[row] + a.xe[col]));
                 if (OUT == SYRK_F32) {
                     a.g32[(int64_t)row * a.ldg + col] = (float)accd[mi][ni][g];
                 } else if (OUT == SYRK_SLAB64) {
