@@ -132,20 +132,26 @@ def d_build(args, snk, tr) -> dict:
     flop_gram = float(n) * (n + 1) * Kc                          # lower triangle incl. diagonal, 2 flop / MAC
     tf = flop_gram / (ms[2] * 1e-3) / 1e12
     P = tr.model.P
-    # syrk_kernel runs the fp32 products as 6 exact bf16 split products (SNK_SYRK=fp32: native f32 MFMA)
-    x6 = os.environ.get("SNK_SYRK", "") != "fp32"
-    speak = PEAK_BF16_TFLOPS / X6_PRODUCTS if x6 else PEAK_FP32_TFLOPS
+    # default: syrk_h3_kernel, the fp32 products as 3 fp16 products of per-row-scaled
+    # parts (SNK_SYRK=x6: 6 bf16 split products; =fp32: native f32 MFMA)
+    mode = os.environ.get("SNK_SYRK", "h3")
+    nprod = {"h3": H3_PRODUCTS, "x6": X6_PRODUCTS}.get(mode)
+    speak = PEAK_BF16_TFLOPS / nprod if nprod else PEAK_FP32_TFLOPS
+    kname = {"h3": "h3_rows_kernel + syrk_h3_kernel (fp16 h3 split, LDS-DMA staged)",
+             "x6": "syrk_kernel (bf16 x6 split)"}.get(mode, "syrk_kernel (f32 MFMA)")
     res = {"d_build_sec": wall,
            "d_build": {"kind": "per-sample Jacobian Gram G = J J' (n x n, fp32-accurate "
-                               + ("bf16x6 split MFMA" if x6 else "f32 MFMA") + ", fp64 accumulation)",
+                               + {"h3": "fp16 h3 split MFMA", "x6": "bf16x6 split MFMA"}.get(mode, "f32 MFMA")
+                               + ", fp64 accumulation)",
                        "n_samples": n, "n_params": P, "conv_columns": Kc,
                        "phase_ms": {"forward_and_data_grads": ms[0], "per_sample_conv_jacobians": ms[1],
                                     "conv_gram": ms[2], "dense_terms_and_mirror": ms[3]},
                        "naive_flop": 2.0 * n * n * P, "executed_gram_flop": flop_gram,
-                       "roofline": {"bound": "mfma", "kernel": "syrk_kernel (conv-column Gram)", "achieved": tf,
+                       "roofline": {"bound": "mfma", "kernel": kname + ", conv-column Gram", "achieved": tf,
                                     "peak": speak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / speak,
                                     "avg_launch_ms": ms[2], "flop_per_launch": flop_gram, "traffic": None,
-                                    "bf16_mfma_tflops_executed": tf * X6_PRODUCTS if x6 else None,
+                                    "half_mfma_tflops_executed": tf * nprod if nprod else None,
+                                    "mfma_utilization": tf * nprod / PEAK_BF16_TFLOPS if nprod else tf / PEAK_FP32_TFLOPS,
                                     "fp32_mfma_peak": PEAK_FP32_TFLOPS}}}
     del G
     K = args.d_snapshots

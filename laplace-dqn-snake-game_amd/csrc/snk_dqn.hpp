@@ -19,7 +19,7 @@ struct snk_dqn_s {
     snk::QWork jw;
     float *jbuf = nullptr;
     int64_t jbuf_floats = 0, jn_cap = 0;
-    uint16_t *jplanes = nullptr;    // h3 Gram: fp16 hi/lo planes of jbuf's rows [2][n][ldh]
+    uint16_t *jplanes = nullptr;    // h3 Gram: jbuf rows as scaled fp16 parts [n][ldh/32][h 32 | l 32]
     int32_t *jexp = nullptr;        //   and their per-row power-of-two exponents
     int64_t jplanes_halves = 0, jexp_cap = 0;
     int64_t *jidx = nullptr;

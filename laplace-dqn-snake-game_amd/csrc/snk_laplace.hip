@@ -172,8 +172,12 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s) {
             default: syrk_kernel<SYRK_DENSE_ADD, SY_F32><<<grid, 256, 0, s>>>(a); break;
         }
     } else if (a.xh && !nox3) {
-        SNK_CHECK(out == SYRK_F32 && z == 1 && a.ldh % SY_KS == 0 && a.xl && a.xe, SNK_ERR_INTERNAL, "syrk h3 arguments");
-        syrk_kernel<SYRK_F32, SY_H3><<<grid, 256, 0, s>>>(a);
+        SNK_CHECK(out == SYRK_F32 && z == 1 && a.ldh % SY_KS == 0 && a.xe, SNK_ERR_INTERNAL, "syrk h3 arguments");
+        static const bool w4 = getenv("SNK_SYRK_W4") != nullptr;   // 4 waves of 64 x 64 (one per SIMD)
+        if (w4)
+            syrk_h3_kernel<4><<<grid, 256, 0, s>>>(a);
+        else
+            syrk_h3_kernel<8><<<grid, 512, 0, s>>>(a);
     } else {
         switch (out) {
             case SYRK_F32: syrk_kernel<SYRK_F32, SY_X6><<<grid, 256, 0, s>>>(a); break;
@@ -403,9 +407,10 @@ extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_d
                 m->jexp = dalloc<int32_t>(n);
                 m->jexp_cap = n;
             }
-            h3_rows_kernel<<<(unsigned)n, 256, 0, s>>>(m->jbuf, Kc, Kc, m->jplanes, m->jplanes + n * ldh, m->jexp, ldh);
+            h3_rows_kernel<<<(unsigned)n, 256, 0, s>>>(m->jbuf, Kc, Kc, m->jplanes, m->jexp, ldh);
             launch_check("h3_rows_kernel");
-            a.xh = m->jplanes; a.xl = m->jplanes + n * ldh; a.xe = m->jexp; a.ldh = ldh;
+            a.xh = m->jplanes; a.xe = m->jexp; a.ldh = ldh;
+            if (getenv("SNK_SYRK_EXP_NOLOAD")) a.kchunk = -4;   // experiment: every stage re-reads k = 0
         }
         syrk_launch(SYRK_F32, a, 1, s);
         if (ms_out) SNK_HIP(hipEventRecord(ev[3], s));

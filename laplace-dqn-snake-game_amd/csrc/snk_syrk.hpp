@@ -330,20 +330,23 @@ struct SyrkArgs {
     const float *z, *hh;
     const uint8_t *act;
     int64_t ldz;
-    // SY_H3: x pre-split by h3_rows_kernel: fp16 planes xh / xl [N][ldh] (ldh a multiple
-    // of SY_KS, zero tail), row i scaled by 2^xe[i]
+    // syrk_h3_kernel: x pre-split by h3_rows_kernel into xh [N][ldh/32][2][32] fp16
+    // (per row and 32-k stage: the h part, then the l part: one 128-byte line;
+    // ldh a multiple of SY_KS, zero tail), row i scaled by 2^xe[i]
     const uint16_t *xh, *xl;
     const int32_t *xe;
     int64_t ldh;
 };
 
 // h3 operands for the Gram (snk_conv_h3.hpp's split, one scale per ROW):
-// row i of x [N][ld] -> fp16 planes h, l of x * 2^e_i with e_i = h3_exp(max_k |x_ik|),
-// zero-padded to ldh. One workgroup per row: the max pass, then the split pass
-// (the row is L2-resident by then). G_ij = 2^-(e_i + e_j) (Xs Xs')_ij exactly.
+// row i of x [N][ld] -> fp16 parts h, l of x * 2^e_i with e_i = h3_exp(max_k |x_ik|),
+// zero-padded to ldh, stored per 32-k stage as [h 32][l 32] (one 128-byte line,
+// so a stage fetch uses whole lines). One workgroup per row: the max pass,
+// then the split pass (the row is L2-resident by then).
+// G_ij = 2^-(e_i + e_j) (Xs Xs')_ij exactly.
 static __global__ __launch_bounds__(256) void h3_rows_kernel(const float *__restrict__ x, int64_t ld, int64_t K,
-                                                      uint16_t *__restrict__ xh, uint16_t *__restrict__ xl,
-                                                      int32_t *__restrict__ xe, int64_t ldh) {
+                                                      uint16_t *__restrict__ xhl, int32_t *__restrict__ xe,
+                                                      int64_t ldh) {
     __shared__ float red4[4];
     const int64_t row = blockIdx.x;
     const f32x4 *src = reinterpret_cast<const f32x4 *>(x + row * ld);
@@ -358,140 +361,208 @@ static __global__ __launch_bounds__(256) void h3_rows_kernel(const float *__rest
     __syncthreads();
     const int e = h3_exp(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
     if (threadIdx.x == 0) xe[row] = e;
-    u32x2 *oh = reinterpret_cast<u32x2 *>(xh + row * ldh), *ol = reinterpret_cast<u32x2 *>(xl + row * ldh);
+    u32x2 *o = reinterpret_cast<u32x2 *>(xhl + row * 2 * ldh);   // 4 halves per u32x2
     for (int64_t i = threadIdx.x; i < nh4; i += 256) {
         const f32x4 v = i < n4 ? src[i] : f32x4{0.f, 0.f, 0.f, 0.f};
         u32x2 h, l;
         h3_split4(v, e, h, l);
-        oh[i] = h;
-        ol[i] = l;
+        const int64_t q = (i >> 3) * 16 + (i & 7);   // stage i / 8, 4-half piece i % 8
+        o[q] = h;
+        o[q + 8] = l;
     }
 }
 
-// The Gram tile on pre-split h3 planes: each 32-k stage of both 128-row blocks
-// is loaded as fp16 h / l pieces (16 B = 8 k per plane), parked in LDS
-// ([op][plane][row][40 halves], as the x6 loop) with no conversion work, and
-// each wave runs 2 k-steps x 2 x 2 tiles x 3 part products of
-// v_mfma_f32_32x32x16_f16: 768 MFMA cycles per stage (x6: 1536). Rows past N
-// read row N-1 (their results are never stored); the zero tail of ldh covers
-// the k range. Accumulators and fp64 flushing as syrk_loop; the 2^-(e_i+e_j)
-// scale is applied in the kernel epilogue.
-template <bool FLUSH>
-__device__ __forceinline__ void syrk_loop_h3(const SyrkArgs &a, int bi, int bj, SyrkX6Lds &s, f32x16 (&acc)[2][2],
-                                             double (&accd)[2][2][16]) {
+// The production h3 Gram kernel: 8 waves (two per SIMD) on a 128 x 128
+// lower-triangle tile, each wave a 64 x 32 quarter-half (2 x 1 tiles of
+// 32 x 32; fp64 flush accumulators 32 doubles, so two waves fit a SIMD), the
+// stages moved global -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR
+// staging, no ds_write), four stage buffers [op][plane][128][32 halves]
+// (128 KB) with the 16-byte chunk of row r stored at slot chunk ^ ((r>>2)&3)
+// (the swizzle is applied on the global source address: the DMA destination
+// is lane-linear; the fragment ds_read_b128 lane groups then hit 16 distinct
+// bank quads). Per step: DMA of stage st+3, k-step-1 fragments of st, the
+// k-step-0 MFMAs, a counted vmcnt (stage st+1 landed; st+2, st+3 stay in
+// flight) and a raw s_barrier, k-step-0 fragments of st+1, the k-step-1
+// MFMAs. Rows past N read row N-1 (never stored); the zero tail of ldh
+// covers the k range.
+constexpr int SH_BUF = 4, SH_ROW = 32;   // halves per LDS row (one 32-k stage)
+__device__ __forceinline__ constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+
+// NW waves: 8 (two per SIMD, 64 x 32 per wave) or 4 (one per SIMD, 64 x 64 per wave:
+// half the fragment reads per MFMA)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
+    constexpr int NC = NW == 4 ? 2 : 1, NJ = 32 / NW;   // column tiles per wave, DMA jobs per wave and stage
+    __shared__ __attribute__((aligned(16))) uint16_t lds[SH_BUF * 2 * 2 * SY_T * SH_ROW];   // 128 KB
+    int bi, bj;
+    {
+        const int64_t t = syrk_xcd_remap(blockIdx.x, a.ntiles);
+        if (a.tiles) {
+            const int2 tb = a.tiles[t];
+            bi = tb.x;
+            bj = tb.y;
+        } else {
+            syrk_tile(t, bi, bj);
+        }
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
+    const int wr = (wave / (NW / 2)) * 64, wc = (wave % (NW / 2)) * 32 * NC;
     const int N = a.N;
-    const int c8 = 8 * (tid & 3);
-    const uint16_t *ph[2][2], *pl[2][2];   // [op][q]
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int ra = bi * SY_T + (tid >> 2) + 64 * q, rb = bj * SY_T + (tid >> 2) + 64 * q;
-        const int64_t oa = (int64_t)(ra < N ? ra : N - 1) * a.ldh + c8, ob = (int64_t)(rb < N ? rb : N - 1) * a.ldh + c8;
-        ph[0][q] = a.xh + oa; pl[0][q] = a.xl + oa;
-        ph[1][q] = a.xh + ob; pl[1][q] = a.xl + ob;
-    }
     const int nst = (int)(a.ldh / SY_KS);
-    struct Stage {
-        u32x4 v[2][2][2];   // [op][q][plane]
+
+    // this wave's NJ DMA jobs per stage: j = NJ * wave + q -> op = j >> 4, plane = (j >> 3) & 1, row block j & 7
+    const uint16_t *dsrc[NJ];
+    int ddst[NJ];   // LDS offset (halves) inside a stage buffer
+#pragma unroll
+    for (int q = 0; q < NJ; ++q) {
+        const int j = NJ * wave + q, op = j >> 4, pl = (j >> 3) & 1, rb = j & 7;
+        const int row = rb * 16 + (lane >> 2);
+        const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+        const int grow = (op ? bj : bi) * SY_T + row;
+        dsrc[q] = a.xh + (int64_t)(grow < N ? grow : N - 1) * 2 * a.ldh + pl * SY_KS + chunk * 8;
+        ddst[q] = ((op * 2 + pl) * SY_T + rb * 16) * SH_ROW;
+    }
+    auto dma = [&](int st, int buf) {
+        const int64_t k = a.kchunk < 0 ? 0 : (int64_t)min(st, nst - 1) * 2 * SY_KS;   // past the end: harmless reloads
+#pragma unroll
+        for (int q = 0; q < NJ; ++q)
+            __builtin_amdgcn_global_load_lds((const void *)(dsrc[q] + k),
+                                             (__attribute__((address_space(3))) void *)(lds + buf * (4 * SY_T * SH_ROW) + ddst[q]),
+                                             16, 0, 0);
     };
-    Stage rs[3];
-    auto issue = [&](int st, Stage &g) {
-        const int64_t k = (int64_t)st * SY_KS;
+    struct Frag {
+        f16x8 a[2][2], b[NC][2];   // [tile][plane]
+    };
+    auto frag = [&](int buf, int ks, Frag &f) {
+        const uint16_t *base = lds + buf * (4 * SY_T * SH_ROW);
+        const int c = 2 * ks + h;
 #pragma unroll
-        for (int op = 0; op < 2; ++op)
+        for (int pn = 0; pn < 2; ++pn) {
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                g.v[op][q][0] = *reinterpret_cast<const u32x4 *>(ph[op][q] + k);
-                g.v[op][q][1] = *reinterpret_cast<const u32x4 *>(pl[op][q] + k);
+            for (int i = 0; i < 2; ++i) {
+                const int row = wr + 32 * i + r;
+                f.a[i][pn] = as_h(*reinterpret_cast<const u32x4 *>(
+                    base + ((0 * 2 + pn) * SY_T + row) * SH_ROW + 8 * (c ^ ((row >> 2) & 3))));
             }
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                const int row = wc + 32 * j + r;
+                f.b[j][pn] = as_h(*reinterpret_cast<const u32x4 *>(
+                    base + ((1 * 2 + pn) * SY_T + row) * SH_ROW + 8 * (c ^ ((row >> 2) & 3))));
+            }
+        }
     };
-    auto park_piece = [&](int buf, const Stage &g, int op, int q) {
-        const int off = ((tid >> 2) + 64 * q) * SX_LD + c8;
-        *reinterpret_cast<u32x4 *>(&s.p[buf][op][0][off]) = g.v[op][q][0];
-        *reinterpret_cast<u32x4 *>(&s.p[buf][op][1][off]) = g.v[op][q][1];
+    f32x16 acc[2][NC];
+    double accd[2][NC][16];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                acc[i][j][g] = 0.0f;
+                accd[i][j][g] = 0.0;
+            }
+    // the six MFMAs of one k-step, split after the first: the next fragments'
+    // ds_reads go out between the two parts (see step)
+    auto mfma_first = [&](const Frag &f) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[0][1], f.b[0][0], acc[0][0], 0, 0, 0);
     };
-    auto compute_park = [&](int buf, bool pk, const Stage &nx) {
+    auto mfma_rest = [&](const Frag &f) {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            f16x8 fa[2][2], fb[2][2];
+        for (int j = 0; j < NC; ++j)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int mi = 0; mi < 2; ++mi) {
+                if (mi == 0 && j == 0) continue;
+                acc[mi][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[mi][1], f.b[j][0], acc[mi][j], 0, 0, 0);
+            }
 #pragma unroll
-                for (int pn = 0; pn < 2; ++pn) {
-                    fa[i][pn] = as_h(*reinterpret_cast<const u32x4 *>(
-                        &s.p[buf][0][pn][(wr + 32 * i + r) * SX_LD + 16 * ks + 8 * h]));
-                    fb[i][pn] = as_h(*reinterpret_cast<const u32x4 *>(
-                        &s.p[buf][1][pn][(wc + 32 * i + r) * SX_LD + 16 * ks + 8 * h]));
-                }
+        for (int j = 0; j < NC; ++j)
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi)
+                acc[mi][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[mi][0], f.b[j][1], acc[mi][j], 0, 0, 0);
 #pragma unroll
-                for (int ni = 0; ni < 2; ++ni) {
-                    f32x16 c = acc[mi][ni];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[mi][1], fb[ni][0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[mi][0], fb[ni][1], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[mi][0], fb[ni][0], c, 0, 0, 0);
-                    acc[mi][ni] = c;
-                    if (ks == 1 && pk) park_piece(buf ^ 1, nx, mi, ni);
-                }
-        }
+        for (int j = 0; j < NC; ++j)
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+                acc[mi][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[mi][0], f.b[j][0], acc[mi][j], 0, 0, 0);
     };
     auto flush = [&]() {
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
+            for (int j = 0; j < NC; ++j)
 #pragma unroll
                 for (int g = 0; g < 16; ++g) {
-                    accd[mi][ni][g] += (double)acc[mi][ni][g];
-                    acc[mi][ni][g] = 0.0f;
+                    accd[mi][j][g] += (double)acc[mi][j][g];
+                    acc[mi][j][g] = 0.0f;
                 }
     };
-    // syrk_loop_x6's rotation: stage st+3 loads into set st % 3, stage st+1 is
-    // parked after this stage's MFMAs (park_piece(op = mi, q = ni) covers the
-    // four pieces of a stage)
-    auto step = [&](int st, auto bufc, Stage &ld3, Stage &nx) {
-        constexpr int BUF = decltype(bufc)::value;
-        const bool more = st + 1 < nst;
-        issue(st + 3 < nst ? st + 3 : nst - 1, ld3);
+    // prologue: stages 0, 1, 2 in flight; stage 0 landed everywhere
+    dma(0, 0);
+    dma(1, 1);
+    dma(2, 2);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * NJ));
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) (vmcnt 63, expcnt 7)
+    __builtin_amdgcn_s_barrier();
+    Frag f0, f1;
+    frag(0, 0, f0);
+    // ROCm 7.2's waitcnt pass drains lgkmcnt to 0 before the first MFMA of a
+    // k-step whatever is in flight, so the next fragments are read AFTER that
+    // first MFMA (they then overlap the remaining five and the other wave's)
+    auto step = [&](int st, auto bc) {
+        constexpr int B = decltype(bc)::value;   // st % 4
+        mfma_first(f0);
         __builtin_amdgcn_sched_barrier(0);
-        compute_park(BUF, more, nx);
-        if (FLUSH && (st % SY_FLUSH == SY_FLUSH - 1 || !more)) flush();
-        __syncthreads();
+        frag(B, 1, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_rest(f0);
+        __builtin_amdgcn_sched_barrier(0);
+        dma(st + 3, (B + 3) & 3);
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * NJ));   // my part of stage st+1 landed
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        mfma_first(f1);
+        __builtin_amdgcn_sched_barrier(0);
+        frag((B + 1) & 3, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_rest(f1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st % SY_FLUSH == SY_FLUSH - 1) flush();
     };
-    using B0 = std::integral_constant<int, 0>;
-    using B1 = std::integral_constant<int, 1>;
-    issue(0, rs[0]);
-    if (nst > 1) issue(1, rs[1]);
-    if (nst > 2) issue(2, rs[2]);
-#pragma unroll
-    for (int op = 0; op < 2; ++op)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) park_piece(0, rs[0], op, q);
-    __syncthreads();
     int st = 0;
-    for (; st + 6 <= nst; st += 6) {
-        step(st, B0{}, rs[0], rs[1]);
-        step(st + 1, B1{}, rs[1], rs[2]);
-        step(st + 2, B0{}, rs[2], rs[0]);
-        step(st + 3, B1{}, rs[0], rs[1]);
-        step(st + 4, B0{}, rs[1], rs[2]);
-        step(st + 5, B1{}, rs[2], rs[0]);
+    for (; st + 4 <= nst; st += 4) {
+        step(st, std::integral_constant<int, 0>{});
+        step(st + 1, std::integral_constant<int, 1>{});
+        step(st + 2, std::integral_constant<int, 2>{});
+        step(st + 3, std::integral_constant<int, 3>{});
     }
-    if (st < nst) step(st, B0{}, rs[0], rs[1]);
-    if (st + 1 < nst) step(st + 1, B1{}, rs[1], rs[2]);
-    if (st + 2 < nst) step(st + 2, B0{}, rs[2], rs[0]);
-    if (st + 3 < nst) step(st + 3, B1{}, rs[0], rs[1]);
-    if (st + 4 < nst) step(st + 4, B0{}, rs[1], rs[2]);
+    if (st < nst) step(st, std::integral_constant<int, 0>{});
+    if (st + 1 < nst) step(st + 1, std::integral_constant<int, 1>{});
+    if (st + 2 < nst) step(st + 2, std::integral_constant<int, 2>{});
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // drain the clamped tail DMAs before the workgroup ends
+    flush();
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const int col = bj * SY_T + wc + 32 * j + r;
+            if (col >= N) continue;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int row = bi * SY_T + wr + mi * 32 + acc_row(g, lane);
+                if (row >= N) continue;
+                a.g32[(int64_t)row * a.ldg + col] = (float)__builtin_ldexp(accd[mi][j][g], -(a.xe[row] + a.xe[col]));
+            }
+        }
 }
 
 union SyrkSmem {
     SyrkLds f32;
     SyrkX6Lds x6;
 };
-enum SyrkMode { SY_F32 = 0, SY_X6 = 1, SY_H3 = 2 };
+enum SyrkMode { SY_F32 = 0, SY_X6 = 1 };
 
 template <int OUT, int MODE>
 __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
@@ -519,9 +590,7 @@ __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
             for (int g = 0; g < 16; ++g) accd[mi][ni][g] = 0.0;
     const int64_t k0 = (int64_t)blockIdx.y * a.kchunk;
     const int64_t k1 = k0 + a.kchunk < a.K ? k0 + a.kchunk : a.K;
-    if (MODE == SY_H3) {
-        syrk_loop_h3<true>(a, bi, bj, sm.x6, acc, accd);
-    } else if (k0 < k1) {
+    if (k0 < k1) {
         if (MODE == SY_X6)
             syrk_loop_x6<true>(a.x, a.ld, a.N, k0, k1, bi, bj, sm.x6, acc, accd);
         else
@@ -553,7 +622,6 @@ __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
             for (int g = 0; g < 16; ++g) {
                 const int row = bi * SY_T + wr + mi * 32 + acc_row(g, lane);
                 if (row >= a.N) continue;
-                if (MODE == SY_H3) accd[mi][ni][g] = __builtin_ldexp(accd[mi][ni][g], -(a.xe[row] + a.xe[col]));
                 if (OUT == SYRK_F32) {
                     a.g32[(int64_t)row * a.ldg + col] = (float)accd[mi][ni][g];
                 } else if (OUT == SYRK_SLAB64) {
