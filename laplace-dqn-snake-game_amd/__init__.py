@@ -16,5 +16,6 @@ from .qnet import DQNModel, nparams, update_target_net_  # noqa: F401
 from .dist import Comm, aggregate_throughput, dist_attach  # noqa: F401
 from .trainer import Trainer, epsilon_greedy, fill_buffer_, play_episode, train_  # noqa: F401
 from .laplace import LaplaceD, compute_D, jacobian, jacobian_gram  # noqa: F401
+from .bsonio import load_trainer, read_trainer  # noqa: F401
 
 __version__ = "1.0.0"

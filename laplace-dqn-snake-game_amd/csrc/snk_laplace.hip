@@ -176,6 +176,8 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s) {
         static const bool w4 = getenv("SNK_SYRK_W4") != nullptr;   // 4 waves of 64 x 64 (one per SIMD)
         if (w4)
             syrk_h3_kernel<4><<<grid, 256, 0, s>>>(a);
+        else if (getenv("SNK_SYRK_PRIO"))
+            syrk_h3_kernel<8, true><<<grid, 512, 0, s>>>(a);
         else
             syrk_h3_kernel<8><<<grid, 512, 0, s>>>(a);
     } else {

@@ -5,9 +5,10 @@ The batched trainer keeps the reference's per-update schedule — epsilon
 decays by `decay` per update, update_target_net! when nb % rate == 0
 (nb = 0 included), n_batches + 1 updates in all — but feeds the replay from
 `n_envs` games stepped in lockstep (`updates_per_iter` updates per lockstep
-step) instead of one full episode per update. With n_envs = 1 and
-`schedule="episode"`, train_ plays one whole episode per update exactly as
-utils.jl:434-482 does.
+step) instead of one full episode per update. `train_(tr,
+schedule="episode")` runs the reference's own loop instead (one whole
+epsilon-greedy episode, stored, then one 64-sample update, utils.jl:434-482),
+host-driven over the same device primitives.
 """
 from __future__ import annotations
 
@@ -20,7 +21,7 @@ from . import _lib
 from ._lib import DeviceArray, call, vp
 from .env import SnakeGame, step_indices_dev
 from .qnet import DQNModel
-from .replay import ReplayBuffer, stack_exp
+from .replay import ReplayBuffer, sample, stack_exp
 
 
 def epsilon_greedy(game: SnakeGame, model: DQNModel, epsilon: float, *, seed: int = 0,
@@ -51,6 +52,9 @@ class Trainer:
         self.save, self.gamma, self.seed = bool(save), float(gamma), int(seed)
         self.updates_per_iter = int(updates_per_iter)
         self.loss_log_capacity = int(loss_log_capacity)
+        # schedule="episode" history (tr.episode_rewards / tr.losses of utils.jl:477-478)
+        self.episode_rewards: list[float] = []
+        self.episode_losses: list[float] = []
         cfg = _lib.TrainerCfg(self.epsilon, self.epsilon_end, self.decay, self.updates_per_iter,
                               self.target_update_rate, self.gamma, self.seed, self.loss_log_capacity)
         h = vp()
@@ -96,8 +100,60 @@ def fill_buffer_(tr: Trainer, graph: bool = True) -> None:
         tr.run(math.ceil(need / tr.game.n_envs), learn=False, graph=graph)
 
 
-def train_(tr: Trainer, trainer_name: str | None = None, graph: bool = True) -> dict:
-    """utils.jl:420-494: fill the buffer, then n_batches + 1 DQN updates."""
+def _episode_into(tr: "Trainer", game: SnakeGame, act: DeviceArray, epsilon: float, seed: int,
+                  max_steps: int = 100000) -> tuple[int, float]:
+    """play_episode (utils.jl:198-259) with the live q_net, every transition
+    stored into tr.buffer as it happens (store!, utils.jl:267-277).
+    Returns (steps, episode reward summed in Float32 as utils.jl:247)."""
+    L, ep = 0, np.float32(0)
+    while L < max_steps:
+        call("snk_dqn_act", tr.model.handle, game.handle, float(epsilon), int(seed), act.ptr)
+        step_indices_dev(game, act.ptr, replay=tr.buffer)
+        o = game.last("reward", "done")
+        ep = np.float32(ep + np.float32(o["reward"][0]))
+        L += 1
+        if o["done"][0]:
+            break
+    return L, float(ep)
+
+
+def _train_episodes(tr: "Trainer") -> dict:
+    """utils.jl:389-402 (fill_buffer!) and 420-482 (train!'s loop), one env:
+    fill until more than `capacity` experiences were played; then for
+    nb = 0..n_batches: one epsilon-greedy episode into the buffer, one
+    B-sample DQN update (sample -> t_net target -> Huber -> backward ->
+    RMSProp), update_target_net! when nb % rate == 0, epsilon decay."""
+    bs, nf = tr.game.board_size, tr.game.n_frames
+    game = SnakeGame(bs, nf, n_envs=1, autoreset=True)
+    act = DeviceArray(1, np.uint8)
+    seed = tr.seed
+    played = 0
+    while played <= tr.buffer.capacity:                       # utils.jl:392
+        L, _ = _episode_into(tr, game, act, tr.epsilon, seed)
+        played += L
+    eps = np.float32(tr.epsilon)
+    for nb in range(tr.n_batches + 1):                        # utils.jl:435 (nb <= n_batches)
+        _, ep_reward = _episode_into(tr, game, act, float(eps), seed)
+        idx, B = sample(tr.buffer, seed=seed, draw=nb)
+        loss = tr.model.update(tr.buffer, idx, B, tr.gamma)
+        if nb % tr.target_update_rate == 0:                   # utils.jl:469-472
+            call("snk_dqn_sync_target", tr.model.handle)
+        tr.episode_rewards.append(ep_reward)
+        tr.episode_losses.append(loss)
+        eps = max(np.float32(eps - np.float32(tr.decay)), np.float32(tr.epsilon_end))   # utils.jl:480
+    tr.epsilon = float(eps)
+    return {"updates": tr.n_batches + 1, "episodes": len(tr.episode_rewards), "epsilon": float(eps),
+            "buffer_length": len(tr.buffer)}
+
+
+def train_(tr: Trainer, trainer_name: str | None = None, graph: bool = True, schedule: str = "batched") -> dict:
+    """utils.jl:420-494: fill the buffer, then n_batches + 1 DQN updates.
+    schedule="batched": the lockstep device loop (snk_trainer_run);
+    schedule="episode": the reference's one-episode-per-update loop."""
+    if schedule == "episode":
+        return _train_episodes(tr)
+    if schedule != "batched":
+        raise ValueError(f"unknown schedule {schedule!r}")
     fill_buffer_(tr, graph=graph)
     if tr.updates_per_iter > 0:
         total = tr.n_batches + 1 - tr.stats()["updates"]

@@ -264,3 +264,29 @@ def test_x6s_bitexact_with_x6m16_and_h3s_close(tmp_path):
         out[tag] = np.load(f)
     assert np.array_equal(out["x6s"], out["m16"])
     assert _qclose(out["h3s"], out["x6s"])
+
+
+def test_train_episode_schedule(snk):
+    """train_(tr, schedule="episode") runs utils.jl:389-482 literally: fill
+    until more than `capacity` transitions were played, then n_batches + 1
+    rounds of (one epsilon-greedy episode stored, one B=64 update), the
+    target synced when nb % rate == 0 (rate 1: after every update, so t_net
+    ends equal to q_net), epsilon decayed per update in Float32 and clamped
+    at epsilon_end. Deterministic for a fixed seed."""
+    outs = []
+    for _ in range(2):
+        tr = snk.Trainer(n_envs=1, board_size=10, n_frames=2, capacity=300, n_batches=12, target_update_rate=1,
+                         epsilon=1.0, epsilon_end=0.6, decay=0.05, seed=3)
+        st = snk.train_(tr, schedule="episode")
+        outs.append((tr.model.get_params(), tr.model.get_params(snk.SNK_NET_TARGET), list(tr.episode_losses),
+                     list(tr.episode_rewards), st))
+    (p0, t0, l0, r0, s0), (p1, t1, l1, r1, s1) = outs
+    assert np.array_equal(p0, t0), "rate 1: t_net synced after the last update"
+    assert np.array_equal(p0, p1) and l0 == l1 and r0 == r1
+    assert s0["updates"] == 13 and len(l0) == 13 and len(r0) == 13
+    assert np.all(np.isfinite(l0)) and all(r <= 60 for r in r0)
+    eps = np.float32(1.0)
+    for _ in range(13):
+        eps = max(np.float32(eps - np.float32(0.05)), np.float32(0.6))
+    assert np.float32(s0["epsilon"]) == eps
+    assert s0["buffer_length"] == 300
