@@ -169,6 +169,29 @@ def d_build(args, snk, tr) -> dict:
         _, gms = lap.gram()
         t_gram = time.perf_counter() - t0
         fl = float(K) * (K + 1) * ((P + 3) // 4 * 4)
+        # la_utils.jl:97-118 at the reference's scale: K = 58 snapshots, 5000 sampled models,
+        # every model one greedy episode (lockstep, per-env weights)
+        lap58 = snk.LaplaceD(P, 58)
+        for pos in range(58):
+            tr.run(1, learn=True, graph=not args.no_graph)
+            lap58.snapshot(tr.model, pos)
+        lap58.fit_center()
+        ls = snk.laplace_sampling_(tr, lap58, n_models=64, seed=1)          # warm-up
+        _lib.call("snk_synchronize")
+        t0 = time.perf_counter()
+        ls = snk.laplace_sampling_(tr, lap58, n_models=5000, seed=2)
+        t_ls = time.perf_counter() - t0
+        msteps = int(ls["lengths"].sum())
+        wbytes = 4.0 * ((P + 3) // 4 * 4)
+        res["laplace_sampling"] = {"kind": "laplace_sampling! (la_utils.jl:97-118): sample_model x 5000 (K = 58) + "
+                                           "one greedy episode each, lockstep on the device",
+                                   "n_models": 5000, "K": 58, "seconds": t_ls, "models_per_s": 5000 / t_ls,
+                                   "model_steps": msteps, "model_steps_per_s": msteps / t_ls,
+                                   "mean_episode_length": float(ls["lengths"].mean()),
+                                   "n_better_models": ls["n_better_models"],
+                                   "weight_stream_GBs": msteps * wbytes / t_ls / 1e9,
+                                   "weight_stream_frac_hbm": msteps * wbytes / t_ls / 1e9 / PEAK_HBM_GBS}
+        del lap58
         res["snapshot_gram"] = {"kind": "compute_D.jl D (P x K Float64 snapshots) -> Welford, centre, G = D'D",
                                 "K": K, "n_params": P, "welford_center_ms": 1e3 * t_fit,
                                 "welford_center_GBs": 28.0 * K * P / t_fit / 1e9,

@@ -262,6 +262,26 @@ int snk_jacobian(snk_dqn m, snk_replay rb, const int64_t *slots_dev, int64_t n, 
  * gradients, per-sample conv Jacobians, conv Gram, dense terms + mirror. */
 int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_dev, float *ms_out);
 
+/* ---------------------------------------------------------------- Laplace sampling
+ * la_utils.jl:83-118. D, mean and var are the handle's (after
+ * snk_laplace_fit_center: the centred deviation matrix and its Welford
+ * statistics, la_utils.jl:161-167). Model n's weights:
+ *   w = mean + 1/sqrt(2) * sqrt(|var|) .* z1 + 1/sqrt(2(K-1)) * D * z2   (fp64, term by term)
+ * with z1 (P, Flux index) and z2 (K) from the counter-based normal stream
+ * z(seed, n, stream 1|2, i) (the reference draws from the unseeded global RNG).
+ */
+/* the stream itself (tests): out_host[q] = z(seed, model, which, i0 + q) */
+int snk_laplace_normals(uint64_t seed, int64_t model, int32_t which, int64_t i0, int64_t n, double *out_host);
+/* sample_model (la_utils.jl:83-95): model n's weights in Flux.destructure order (Float32) */
+int snk_laplace_sample_params(snk_laplace h, snk_dqn m, uint64_t seed, int64_t model, float *flux_host);
+/* laplace_sampling! (la_utils.jl:97-118) with epsilon 0: tr_reward = greedy episode
+ * reward of m's q_net; models 0..n_models-1 each play one greedy episode (lockstep,
+ * `chunk` models at a time, 0 = up to 4096); the transitions of every model with
+ * reward > tr_reward are appended to rb in (model, step) order.
+ * rewards_host / lengths_host (optional, n_models): each model's episode. */
+int snk_laplace_sampling(snk_laplace h, snk_dqn m, snk_replay rb, int64_t n_models, uint64_t seed, int64_t chunk,
+                         float *tr_reward_out, int64_t *n_better_out, float *rewards_host, int32_t *lengths_host);
+
 #ifdef __cplusplus
 }
 #endif

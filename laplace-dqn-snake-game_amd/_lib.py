@@ -123,6 +123,9 @@ _PROTOS = {
     "snk_laplace_gram": [vp, P(f32)],
     "snk_jacobian": [vp, vp, vp, i64, vp],
     "snk_jacobian_gram": [vp, vp, i64, vp, P(f32)],
+    "snk_laplace_normals": [u64, i64, i32, i64, i64, vp],
+    "snk_laplace_sample_params": [vp, vp, u64, i64, vp],
+    "snk_laplace_sampling": [vp, vp, vp, i64, u64, i64, P(f32), P(i64), vp, vp],
 }
 
 SNK_NET_Q = 0

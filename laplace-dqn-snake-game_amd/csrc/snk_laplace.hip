@@ -433,3 +433,454 @@ extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_d
         }
     });
 }
+
+// =========================================================================
+// Laplace sampling (la_utils.jl:83-118)
+//
+// sample_model (:83-95): w = mean + 1/sqrt(2) * sqrt.(Gamma) * z1
+//                              + 1/sqrt(2(K-1)) * D * z2,   Gamma = Diagonal(|var|)
+// with z1 ~ N(0, I_P), z2 ~ N(0, I_K); restructure(w) -> Float32 model.
+// laplace_sampling! (:97-118): the greedy (epsilon 0) episode reward of the
+// current model, then n_models x (sample_model, greedy play_episode); the
+// transitions of every model that beats it are stored into the buffer, in
+// model order.
+//
+// Here the n_models episodes run in LOCKSTEP, one env per sampled model:
+//  * lap_sample_kernel builds the models' weights in the packed layout (the
+//    Julia expression above in fp64, term by term; z from a counter-based
+//    Box-Muller stream indexed by (seed, model, stream, Flux index), so a
+//    model's weights do not depend on the chunking);
+//  * lap_act_kernel is one workgroup per env running ITS model's whole
+//    forward (conv1, conv2 in LDS, conv3 / Dense1 streaming that model's
+//    weights, Dense2 + first-max argmax) — the weights differ per env, so
+//    the shared-weight MFMA kernels of the training path do not apply; the
+//    launch is HBM-bound on ~1.1 MB of weights per live env and step;
+//  * the fused env step stores every transition into a scratch ring (slot
+//    t * G + g); lap_track_kernel records each env's first episode end
+//    (length, Float32 episode reward);
+//  * the better models' transitions are appended to the trainer's buffer in
+//    (model, step) order by lap_copy_kernel.
+// =========================================================================
+namespace snk {
+
+__host__ __device__ inline double lap_u01(uint64_t x) { return ((double)(x >> 11) + 0.5) * 0x1.0p-53; }
+
+// z(seed, model, stream, i) ~ N(0, 1): Box-Muller on two splitmix64 draws
+__device__ inline double lap_normal(uint64_t seed, uint64_t model, uint32_t stream, uint64_t i) {
+    const uint64_t b = rng_hash(seed ^ ((uint64_t)stream << 56), model, i);
+    const double u1 = lap_u01(splitmix64(b)), u2 = lap_u01(splitmix64(b ^ 0x9E3779B97F4A7C15ULL));
+    return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+__global__ void lap_normals_kernel(uint64_t seed, uint64_t model, uint32_t stream, int64_t i0, int64_t n,
+                                   double *__restrict__ out) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) out[q] = lap_normal(seed, model, stream, (uint64_t)(i0 + q));
+}
+
+// W[g][j] (packed index j, Flux index fi = perm[j]) for models n0 .. n0+G-1:
+//   w = (mean[fi] + (c1 * sqrt|var[fi]|) * z1(fi)) + sum_k (c2 * D[k][fi]) * z2(k)   (k ascending)
+// 8 models per pass keep their gemv sums in registers; z2 of the G models in LDS
+constexpr int LAP_GM = 8;
+__global__ __launch_bounds__(256) void lap_sample_kernel(const double *__restrict__ mean, const double *__restrict__ var,
+                                                         const double *__restrict__ D, int K, int64_t P,
+                                                         const int32_t *__restrict__ perm, uint64_t seed, int64_t n0,
+                                                         int G, double c1, double c2, float *__restrict__ W,
+                                                         int64_t ldw) {
+    extern __shared__ double z2s[];   // [G][K]
+    for (int q = threadIdx.x; q < G * K; q += blockDim.x) z2s[q] = lap_normal(seed, (uint64_t)(n0 + q / K), 2, q % K);
+    __syncthreads();
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < P; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t fi = perm[j];
+        const double a = c1 * sqrt(fabs(var[fi]));
+        const double m = mean[fi];
+        for (int g0 = 0; g0 < G; g0 += LAP_GM) {
+            double d[LAP_GM];
+#pragma unroll
+            for (int u = 0; u < LAP_GM; ++u) d[u] = 0.0;
+            for (int k = 0; k < K; ++k) {
+                const double dk = c2 * D[(int64_t)k * P + fi];
+#pragma unroll
+                for (int u = 0; u < LAP_GM; ++u)
+                    if (g0 + u < G) d[u] = d[u] + dk * z2s[(g0 + u) * K + k];
+            }
+#pragma unroll
+            for (int u = 0; u < LAP_GM; ++u)
+                if (g0 + u < G) {
+                    const double w = (m + a * lap_normal(seed, (uint64_t)(n0 + g0 + u), 1, (uint64_t)fi)) + d[u];
+                    W[(int64_t)(g0 + u) * ldw + j] = (float)w;
+                }
+        }
+    }
+}
+
+// dynamic LDS floats of lap_act_kernel
+static inline int64_t lap_act_lds_floats(const QLayout &L) {
+    const int bp = L.bs + 2, r4 = (L.C * bp * bp + 3) & ~3, a4 = (16 * bp * bp + 3) & ~3;
+    return (int64_t)r4 + a4 + 9 * 16 * 32 + (int64_t)L.ncell * 32 + L.K1 + 16 * 64 + 64 + 8;
+}
+
+// one workgroup (256 threads) per env g: the greedy action of model g on the env's state
+__global__ __launch_bounds__(256) void lap_act_kernel(QLayout L, const float *__restrict__ W, int64_t ldw, BoardSrc src,
+                                                      const uint8_t *__restrict__ fin, uint8_t *__restrict__ act,
+                                                      float *__restrict__ qout) {
+    const int64_t g = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (fin && fin[g]) {
+        if (tid == 0) act[g] = 0;
+        return;
+    }
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    const int bs = L.bs, bp = bs + 2, C = L.C, nc = L.ncell, Wo = L.Wo;
+    float *xin = lsm;                       // [C][bp*bp] bordered input planes
+    float *a1 = xin + ((C * bp * bp + 3) & ~3);   // [16][bp*bp] bordered conv1 output (16-B aligned sections)
+    float *w2s = a1 + ((16 * bp * bp + 3) & ~3);  // conv2 weights [(kk*16+ci)*32+co]
+    float *a2 = w2s + 9 * 16 * 32;          // [ncell][32]
+    float *a3 = a2 + nc * 32;               // [Wo*Wo][64]
+    float *red = a3 + L.K1;                 // [16][64] Dense1 partial sums
+    float *h1 = red + 4 * 64;               // [64]
+    const float *th = W + g * ldw;
+    for (int q = tid; q < (int)(w2s - xin); q += 256) xin[q] = 0.0f;
+    for (int q = tid; q < 9 * 16 * 32; q += 256) w2s[q] = th[L.off_w2 + q];
+    __syncthreads();
+    for (int q = tid; q < C * nc; q += 256) {
+        const int c = q / nc, cell = q - c * nc;
+        const int jj = cell / bs, ii = cell - jj * bs;
+        xin[c * bp * bp + (ii + 1) + (jj + 1) * bp] = src.load(g, c, cell);
+    }
+    __syncthreads();
+    // conv1 (3x3, pad 1): thread -> co = tid & 15, positions (tid >> 4) + 16 r
+    {
+        const int co = tid & 15;
+        const float *w1 = th + L.off_w1;
+        const float b = th[L.off_b1 + co];
+        for (int p = tid >> 4; p < nc; p += 16) {
+            const int j = p / bs, i = p - j * bs;
+            float acc = b;
+            for (int kk = 0; kk < 9; ++kk) {
+                const int du = kk % 3, dv = kk / 3;
+                for (int c = 0; c < C; ++c)
+                    acc = __builtin_fmaf(xin[c * bp * bp + (i + du) + (j + dv) * bp], w1[(kk * C + c) * 16 + co], acc);
+            }
+            a1[co * bp * bp + (i + 1) + (j + 1) * bp] = fmaxf(acc, 0.0f);
+        }
+    }
+    __syncthreads();
+    // conv2 (3x3, 16 -> 32, pad 1): co = tid & 31, positions (tid >> 5) + 8 r
+    {
+        const int co = tid & 31;
+        const float b = th[L.off_b2 + co];
+        for (int p = tid >> 5; p < nc; p += 8) {
+            const int j = p / bs, i = p - j * bs;
+            float acc = b;
+            for (int kk = 0; kk < 9; ++kk) {
+                const int du = kk % 3, dv = kk / 3;
+                const float *ap = a1 + (i + du) + (j + dv) * bp;
+#pragma unroll 4
+                for (int ci = 0; ci < 16; ++ci) acc = __builtin_fmaf(ap[ci * bp * bp], w2s[(kk * 16 + ci) * 32 + co], acc);
+            }
+            a2[p * 32 + co] = fmaxf(acc, 0.0f);
+        }
+    }
+    __syncthreads();
+    // conv3 (6x6, 32 -> 64, pad 0), weights streamed from HBM: thread -> 4 output
+    // channels 4*(tid & 15) .. +3 at positions (tid >> 4) + 16 r, r < 4 (Wo^2 <= 64);
+    // per 4 input channels: 4 ds_read_b128 of a2, 4 float4 weight loads, 64 FMAs
+    {
+        const int cq = tid & 15, pg = tid >> 4;
+        const int np = Wo * Wo;
+        float acc[4][4];
+        int base[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int p = pg + 16 * r;
+            const int pj = p < np ? p / Wo : 0, pi = p < np ? p - pj * Wo : 0;
+            base[r] = (pi + pj * bs) * 32;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[r][j] = th[L.off_b3 + 4 * cq + j];
+        }
+        const f32x4 *w3 = reinterpret_cast<const f32x4 *>(th + L.off_w3) + cq;   // [(kk*32+ci)*16 + cq]
+        for (int kk = 0; kk < 36; ++kk) {
+            const int du = kk % 6, dv = kk / 6;
+            const int off = (du + dv * bs) * 32;
+#pragma unroll 2
+            for (int ci = 0; ci < 32; ci += 4) {
+                f32x4 w[4], av[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) w[c] = w3[(kk * 32 + ci + c) * 16];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) av[r] = *reinterpret_cast<const f32x4 *>(a2 + base[r] + off + ci);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[r][j] = __builtin_fmaf(av[r][c], w[c][j], acc[r][j]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int p = pg + 16 * r;
+            if (p < np)
+                *reinterpret_cast<f32x4 *>(a3 + p * 64 + 4 * cq) =
+                    f32x4{fmaxf(acc[r][0], 0.f), fmaxf(acc[r][1], 0.f), fmaxf(acc[r][2], 0.f), fmaxf(acc[r][3], 0.f)};
+        }
+    }
+    __syncthreads();
+    // Dense1: thread -> 4 outputs 4*(tid & 15) .. +3 over the 16th (tid >> 4) of the
+    // K1 inputs (4 at a time: one ds_read_b128, 4 float4 weight loads, 16 FMAs), then
+    // a 16-way reduction in LDS
+    {
+        const int oq = tid & 15, part = tid >> 4;
+        const int kq = (L.K1 / 4 + 15) / 16 * 4, k0 = part * kq, k1 = min(L.K1, k0 + kq);
+        const f32x4 *wd = reinterpret_cast<const f32x4 *>(th + L.off_d1w) + oq;   // [k*16 + oq]
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+        for (int k = k0; k < k1; k += 4) {
+            const f32x4 a = *reinterpret_cast<const f32x4 *>(a3 + k);
+            f32x4 w[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) w[c] = wd[(int64_t)(k + c) * 16];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] = __builtin_fmaf(a[c], w[c][j], acc[j]);
+        }
+        *reinterpret_cast<f32x4 *>(red + part * 64 + 4 * oq) = acc;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        float h = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) h += red[q * 64 + tid];
+        h1[tid] = fmaxf(th[L.off_d1b + tid] + h, 0.0f);
+    }
+    __syncthreads();
+    if (tid < 64) {   // Dense2 + first-max argmax (utils.jl:165-169)
+        float q[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float v = h1[tid] * th[L.off_d2w + a * 64 + tid];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            q[a] = v + th[L.off_d2b + a];
+        }
+        if (tid == 0) {
+            int best = 0;
+            if (q[1] > q[best]) best = 1;
+            if (q[2] > q[best]) best = 2;
+            act[g] = (uint8_t)best;
+            if (qout) {
+                qout[g * 3] = q[0]; qout[g * 3 + 1] = q[1]; qout[g * 3 + 2] = q[2];
+            }
+        }
+    }
+}
+
+// after the step of iteration t: the first episode end of each env
+__global__ void lap_track_kernel(const uint8_t *__restrict__ done, const float *__restrict__ ep, int64_t G, int t,
+                                 uint8_t *__restrict__ fin, int32_t *__restrict__ len, float *__restrict__ rew,
+                                 int32_t *__restrict__ nfin) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G || fin[g] || !done[g]) return;
+    fin[g] = 1;
+    len[g] = t + 1;
+    rew[g] = ep[g];
+    atomicAdd(nfin, 1);
+}
+
+// append the listed scratch slots to the destination ring, in list order (store!)
+__global__ void lap_copy_kernel(ReplayDev src, ReplayDev dst, const int64_t *__restrict__ slots, int64_t n,
+                                int64_t dcount) {
+    const int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const int64_t s = slots[i], d = (dcount + i) % dst.cap;
+    const int nb = (src.C + 1) * src.pitch;
+    for (int q = threadIdx.x; q < nb; q += blockDim.x) dst.frames[d * nb + q] = src.frames[s * nb + q];
+    if (threadIdx.x == 0) {
+        dst.reward[d] = src.reward[s];
+        dst.act[d] = src.act[s];
+        dst.done[d] = src.done[s];
+        dst.mask[d] = src.mask[s];
+        dst.dirs[d] = src.dirs[s];
+    }
+}
+
+__global__ void lap_count_add_kernel(int64_t *count, int64_t n) { *count += n; }
+
+}  // namespace snk
+
+// greedy lockstep episodes of G models whose packed weights are W [G][ldw];
+// per-model length / Float32 reward; scratch ring (slot t*G + g) left in *scratch
+static void lap_rollout(snk_dqn m, const float *W, int64_t ldw, int64_t G, float *rew_dev, int32_t *len_dev,
+                        snk_env *env_out, snk_replay *scratch_out) {
+    const QLayout &L = m->L;
+    hipStream_t s = stream();
+    const int T = 501;   // the first episode is over by step 500 (utils.jl:88 truncation)
+    snk_env env = nullptr;
+    snk_replay sc = nullptr;
+    if (snk_env_create(&env, G, L.bs, L.C, 42, 500, 1) != SNK_OK) throw Error{SNK_ERR_HIP};
+    if (snk_replay_create(&sc, G * T, L.bs, L.C, 1) != SNK_OK) {
+        snk_env_destroy(env);
+        throw Error{SNK_ERR_HIP};
+    }
+    *env_out = env;
+    *scratch_out = sc;
+    const EnvDev &E = env_dev(env);
+    const ReplayDev &R = replay_dev(sc);
+    uint8_t *fin = dalloc<uint8_t>(G), *act = dalloc<uint8_t>(G);
+    int32_t *nfin = dalloc<int32_t>(1);
+    SNK_HIP(hipMemsetAsync(fin, 0, G, s));
+    SNK_HIP(hipMemsetAsync(nfin, 0, sizeof(int32_t), s));
+    SNK_HIP(hipMemsetAsync(len_dev, 0, G * sizeof(int32_t), s));
+    const size_t lds = (size_t)lap_act_lds_floats(L) * sizeof(float);
+    SNK_CHECK(lds <= 160 * 1024 && L.Wo * L.Wo <= 64 && L.K1 % 4 == 0 && L.off_w3 % 4 == 0 && L.off_d1w % 4 == 0 &&
+                  ldw % 4 == 0,
+              SNK_ERR_INVALID,
+              "Laplace sampling: board side %d too large", L.bs);
+    static size_t attr = 0;
+    if (lds > attr) {
+        SNK_HIP(hipFuncSetAttribute((const void *)lap_act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = lds;
+    }
+    const BoardSrc src = src_env(E);
+    for (int t = 0; t < T; ++t) {
+        lap_act_kernel<<<(unsigned)G, 256, lds, s>>>(L, W, ldw, src, fin, act, nullptr);
+        launch_check("lap_act_kernel");
+        env_launch_step(E, act, SNK_ACT_INDEX, &R, s);
+        env_launch_advance(E, &R, s);
+        lap_track_kernel<<<(unsigned)ceil_div(G, 256), 256, 0, s>>>(E.out_done, E.out_ep_reward, G, t, fin, len_dev,
+                                                                    rew_dev, nfin);
+        launch_check("lap_track_kernel");
+        if ((t & 7) == 7) {
+            int32_t h = 0;
+            SNK_HIP(hipMemcpyAsync(&h, nfin, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            SNK_HIP(hipStreamSynchronize(s));
+            if (h == G) break;
+        }
+    }
+    SNK_HIP(hipStreamSynchronize(s));
+    dfree(fin);
+    dfree(act);
+    dfree(nfin);
+}
+
+extern "C" int snk_laplace_normals(uint64_t seed, int64_t model, int32_t which, int64_t i0, int64_t n, double *out_host) {
+    return guard([&] {
+        SNK_CHECK(out_host && n >= 0 && (which == 1 || which == 2), SNK_ERR_INVALID, "bad laplace_normals arguments");
+        if (n == 0) return;
+        hipStream_t s = stream();
+        double *d = dalloc<double>(n);
+        lap_normals_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, s>>>(seed, (uint64_t)model, (uint32_t)which, i0, n, d);
+        launch_check("lap_normals_kernel");
+        SNK_HIP(hipMemcpyAsync(out_host, d, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        SNK_HIP(hipStreamSynchronize(s));
+        dfree(d);
+    });
+}
+
+static void lap_build(snk_laplace h, snk_dqn m, uint64_t seed, int64_t n0, int64_t G, float *W, int64_t ldw) {
+    SNK_CHECK(h->K >= 2, SNK_ERR_INVALID, "sample_model needs K >= 2 columns of D (la_utils.jl:93)");
+    SNK_CHECK(h->P == m->L.P, SNK_ERR_INVALID, "D has %lld parameters, the model %lld", (long long)h->P,
+              (long long)m->L.P);
+    const double c1 = 1.0 / sqrt(2.0), c2 = 1.0 / sqrt(2.0 * (double)(h->K - 1));
+    const int GS = (int)std::max<int64_t>(1, std::min<int64_t>(64, 16384 / h->K));   // z2 of GS models in LDS
+    hipStream_t s = stream();
+    for (int64_t g0 = 0; g0 < G; g0 += GS) {
+        const int gn = (int)std::min<int64_t>(GS, G - g0);
+        lap_sample_kernel<<<(unsigned)std::min<int64_t>(ceil_div(h->P, 256), 4096), 256, (size_t)gn * h->K * sizeof(double),
+                            s>>>(h->mean, h->var, h->D, h->K, h->P, m->perm, seed, n0 + g0, gn, c1, c2, W + g0 * ldw, ldw);
+        launch_check("lap_sample_kernel");
+    }
+}
+
+extern "C" int snk_laplace_sample_params(snk_laplace h, snk_dqn m, uint64_t seed, int64_t model, float *flux_host) {
+    return guard([&] {
+        SNK_CHECK(h && m && flux_host && model >= 0, SNK_ERR_INVALID, "bad sample_params arguments");
+        const int64_t P = m->L.P;
+        float *W = dalloc<float>(P);
+        lap_build(h, m, seed, model, 1, W, P);
+        std::vector<float> packed(P);
+        std::vector<int32_t> perm(P);
+        SNK_HIP(hipMemcpyAsync(packed.data(), W, P * sizeof(float), hipMemcpyDeviceToHost, stream()));
+        SNK_HIP(hipMemcpyAsync(perm.data(), m->perm, P * sizeof(int32_t), hipMemcpyDeviceToHost, stream()));
+        SNK_HIP(hipStreamSynchronize(stream()));
+        dfree(W);
+        for (int64_t j = 0; j < P; ++j) flux_host[perm[j]] = packed[j];
+    });
+}
+
+extern "C" int snk_laplace_sampling(snk_laplace h, snk_dqn m, snk_replay rb, int64_t n_models, uint64_t seed,
+                                    int64_t chunk, float *tr_reward_out, int64_t *n_better_out, float *rewards_host,
+                                    int32_t *lengths_host) {
+    return guard([&] {
+        SNK_CHECK(h && m && rb && n_models >= 0 && tr_reward_out && n_better_out, SNK_ERR_INVALID, "NULL argument");
+        const QLayout &L = m->L;
+        const ReplayDev &D = replay_dev(rb);
+        SNK_CHECK(D.bs == L.bs && D.C == L.C, SNK_ERR_INVALID, "replay geometry differs from the model");
+        hipStream_t s = stream();
+        const int64_t P = L.P;
+        const int64_t G0 = chunk > 0 ? chunk : std::max<int64_t>(1, std::min<int64_t>(n_models, 4096));
+        const int64_t ldw = (P + 3) & ~int64_t(3);   // 16-byte aligned model rows (float4 weight loads)
+        float *W = dalloc<float>((size_t)std::max<int64_t>(G0, 1) * ldw);
+        float *rew = dalloc<float>(std::max<int64_t>(G0, 1));
+        int32_t *len = dalloc<int32_t>(std::max<int64_t>(G0, 1));
+        auto cleanup = [&](snk_env e, snk_replay r) {
+            if (e) snk_env_destroy(e);
+            if (r) snk_replay_destroy(r);
+        };
+        // play_episode(tr.model, 0f0): the current q_net (packed theta) as a one-model batch
+        float tr_reward = 0.0f;
+        {
+            snk_env e = nullptr;
+            snk_replay r = nullptr;
+            lap_rollout(m, m->theta_q, P, 1, rew, len, &e, &r);
+            SNK_HIP(hipMemcpy(&tr_reward, rew, sizeof(float), hipMemcpyDeviceToHost));
+            cleanup(e, r);
+        }
+        int64_t n_better = 0;
+        std::vector<float> hr;
+        std::vector<int32_t> hl;
+        for (int64_t n0 = 0; n0 < n_models; n0 += G0) {
+            const int64_t G = std::min(G0, n_models - n0);
+            lap_build(h, m, seed, n0, G, W, ldw);
+            snk_env e = nullptr;
+            snk_replay r = nullptr;
+            lap_rollout(m, W, ldw, G, rew, len, &e, &r);
+            hr.resize(G);
+            hl.resize(G);
+            SNK_HIP(hipMemcpy(hr.data(), rew, G * sizeof(float), hipMemcpyDeviceToHost));
+            SNK_HIP(hipMemcpy(hl.data(), len, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+            std::vector<int64_t> slots;
+            for (int64_t g = 0; g < G; ++g) {
+                SNK_CHECK(hl[g] > 0, SNK_ERR_INTERNAL, "model %lld: episode did not end", (long long)(n0 + g));
+                if (rewards_host) rewards_host[n0 + g] = hr[g];
+                if (lengths_host) lengths_host[n0 + g] = hl[g];
+                if (hr[g] > tr_reward) {   // la_utils.jl:108
+                    ++n_better;
+                    for (int t = 0; t < hl[g]; ++t) slots.push_back((int64_t)t * G + g);
+                }
+            }
+            if (!slots.empty()) {
+                const int64_t ns = (int64_t)slots.size();
+                int64_t *sd = dalloc<int64_t>(ns);
+                int64_t dcount = 0;
+                SNK_HIP(hipMemcpyAsync(sd, slots.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice, s));
+                SNK_HIP(hipMemcpyAsync(&dcount, D.count, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+                SNK_HIP(hipStreamSynchronize(s));
+                lap_copy_kernel<<<(unsigned)ns, 256, 0, s>>>(replay_dev(r), D, sd, ns, dcount);
+                launch_check("lap_copy_kernel");
+                lap_count_add_kernel<<<1, 1, 0, s>>>(D.count, ns);
+                launch_check("lap_count_add_kernel");
+                SNK_HIP(hipStreamSynchronize(s));
+                dfree(sd);
+            }
+            cleanup(e, r);
+        }
+        dfree(W);
+        dfree(rew);
+        dfree(len);
+        *tr_reward_out = tr_reward;
+        *n_better_out = n_better;
+    });
+}

@@ -181,3 +181,49 @@ def jacobian_gram(model: DQNModel, buf: ReplayBuffer, n: int | None = None, *, o
 def d_build_seconds(ms) -> float:
     """Wall time of one Jacobian-Gram D build from its phase times."""
     return sum(ms) / 1e3 if ms else math.nan
+
+
+# ---------------------------------------------------------------- Laplace sampling
+def laplace_normals(seed: int, model: int, which: int, i0: int, n: int) -> np.ndarray:
+    """The counter-based N(0, 1) stream behind sample_model: z1 (which=1,
+    indexed by Flux parameter index) or z2 (which=2, indexed by column k)
+    of model `model`."""
+    out = np.empty(int(n), np.float64)
+    call("snk_laplace_normals", int(seed), int(model), int(which), int(i0), int(n), _lib.ptr(out))
+    return out
+
+
+def sample_model(lap: LaplaceD, model: DQNModel, n: int = 0, seed: int = 0) -> np.ndarray:
+    """la_utils.jl:83-95 `sample_model(mean, var, D, re)` for sample n:
+    w = mean + 1/sqrt(2) * sqrt.(Diagonal(|var|)) * z1 + 1/sqrt(2(K-1)) * D * z2,
+    computed on the device in Float64 term by term, returned as Float32 in
+    Flux.destructure order (what `re(w)` holds). `lap` must be fitted
+    (mean, var and the centred D, la_utils.jl:161-167)."""
+    if not lap.fitted:
+        raise RuntimeError("LaplaceD.fit_center() first: sample_model needs mean, var and the centred D")
+    out = np.empty(model.P, np.float32)
+    call("snk_laplace_sample_params", lap.handle, model.handle, int(seed), int(n), _lib.ptr(out))
+    return out
+
+
+def laplace_sampling_(tr, lap: LaplaceD, n_models: int = 5000, epsilon: float = 0.0, *, seed: int = 0,
+                      chunk: int = 0) -> dict:
+    """la_utils.jl:97-118 `laplace_sampling!(tr, mean, var, D; n_models=5000)`:
+    the greedy episode reward of tr.model, then n_models sampled models each
+    play one greedy episode (all in lockstep on the device); the transitions
+    of every model whose episode reward beats tr.model's are stored into
+    tr.buffer in model order. `epsilon` is accepted for the reference's
+    signature; like the reference (`play_episode(model, 0.0f0)`, :105) the
+    sampled models play greedily. Returns n_better_models, the reference
+    reward and every model's (reward, length)."""
+    del epsilon
+    if not lap.fitted:
+        raise RuntimeError("LaplaceD.fit_center() first")
+    n_models = int(n_models)
+    rew = np.zeros(max(n_models, 1), np.float32)
+    length = np.zeros(max(n_models, 1), np.int32)
+    trr, nb = C.c_float(0), C.c_int64(0)
+    call("snk_laplace_sampling", lap.handle, tr.model.handle, tr.buffer.handle, n_models, int(seed), int(chunk),
+         C.byref(trr), C.byref(nb), _lib.ptr(rew), _lib.ptr(length))
+    return {"n_better_models": nb.value, "tr_reward": float(trr.value), "rewards": rew[:n_models],
+            "lengths": length[:n_models]}

@@ -162,3 +162,107 @@ def test_spectrum_ncols_and_trajectory_match_svd(snk):
     for i in range(2):
         sgn = np.sign(np.dot(Y[i], Yref[i]))
         assert np.allclose(sgn * Y[i], Yref[i], rtol=1e-4, atol=1e-6 * np.abs(Yref[i]).max())
+
+
+# ---------------------------------------------------------------- Laplace sampling (la_utils.jl:83-118)
+def _fitted_lap(snk, m, K, seed=0):
+    """K q_net snapshots spread around m's weights, Welford-fitted and centred."""
+    rng = np.random.default_rng(seed)
+    p0 = m.get_params()
+    lap = snk.LaplaceD(m.P, K)
+    for k in range(K):
+        m.set_params((p0 + rng.standard_normal(p0.size).astype(np.float32) * np.float32(0.02)).astype(np.float32))
+        lap.snapshot(m, k)
+    m.set_params(p0)
+    lap.fit_center()
+    return lap
+
+
+def test_laplace_normals_stream(snk):
+    """The z stream of sample_model: N(0, 1) moments (5-sigma bounds on
+    200k draws), streams 1 and 2 and different models independent, and
+    index-addressable (a sub-range equals the same indices of a longer draw)."""
+    z = snk.laplace_normals(5, 3, 1, 0, 200_000)
+    assert abs(z.mean()) < 5 / np.sqrt(z.size) and abs(z.var() - 1) < 5 * np.sqrt(2 / z.size)
+    assert abs(np.mean(z ** 4) - 3) < 0.1 and np.all(np.isfinite(z))
+    z2 = snk.laplace_normals(5, 3, 2, 0, 200_000)
+    z_other = snk.laplace_normals(5, 4, 1, 0, 200_000)
+    assert abs(np.corrcoef(z, z2)[0, 1]) < 0.02 and abs(np.corrcoef(z, z_other)[0, 1]) < 0.02
+    assert np.array_equal(snk.laplace_normals(5, 3, 1, 1000, 500), z[1000:1500])
+
+
+def test_sample_model_bitexact_vs_restatement(snk):
+    """sample_model (la_utils.jl:83-95) given the device z: the numpy
+    restatement of w = mean + 1/sqrt(2) sqrt|var| z1 + 1/sqrt(2(K-1)) D z2
+    (Float64, term by term, the D*z2 sum k-ascending) rounds to the same
+    Float32 weights bit for bit (Flux order)."""
+    bs, C, K = 10, 2, 7
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=3)
+    lap = _fitted_lap(snk, m, K)
+    D, mean, var = lap.D(), lap.mean(), lap.var()       # D: [K][P] (Julia's P x K)
+    for n in (0, 11):
+        w = snk.sample_model(lap, m, n=n, seed=9)
+        z1 = snk.laplace_normals(9, n, 1, 0, m.P)
+        z2 = snk.laplace_normals(9, n, 2, 0, K)
+        c1, c2 = 1.0 / np.sqrt(2.0), 1.0 / np.sqrt(2.0 * (K - 1))
+        d = np.zeros(m.P)
+        for k in range(K):
+            d = d + (c2 * D[k]) * z2[k]
+        ref = ((mean + (c1 * np.sqrt(np.abs(var))) * z1) + d).astype(np.float32)
+        assert np.array_equal(w, ref), np.abs(w - ref).max()
+
+
+def _oracle_greedy_episode(bs, C, params):
+    """play_episode(model, 0f0) on the CPU oracle: fp64 forward, first-max
+    argmax, oracle step!; returns (Float32 reward, length, min top-2 margin)."""
+    ob = oracle.OracleBatch(1, bs, C)
+    ep, L, margin = np.float32(0), 0, np.inf
+    while True:
+        q = oracle.qnet_forward(bs, C, params, ob.states().astype(np.float32))[0]
+        srt = np.sort(q)
+        margin = min(margin, float(srt[-1] - srt[-2]) / max(1.0, abs(float(srt[-1]))))
+        r = ob.step(np.array([int(np.argmax(q))], np.uint8), want_frames=False)
+        ep = np.float32(ep + np.float32(r["reward"][0]))
+        L += 1
+        if r["done"][0]:
+            return float(ep), L, margin
+
+
+def test_laplace_sampling_lockstep_episodes(snk):
+    """laplace_sampling! (la_utils.jl:97-118) with 6 models in chunks of 4:
+    every model's lockstep greedy episode (per-env-weights forward) has the
+    reward and length of play_episode(re(w), 0f0) on the CPU oracle (fp64
+    forward + step!) whenever no step's top-2 Q margin is below 1e-4
+    (relative); tr_reward is tr.model's greedy episode on the oracle; the
+    buffer grows by exactly the better models' transitions, appended in
+    (model, step) order (their rewards sum to the models' episode rewards)."""
+    bs, C, K = 10, 2, 5
+    tr = snk.Trainer(n_envs=1, board_size=bs, n_frames=C, capacity=20000, seed=5)
+    lap = _fitted_lap(snk, tr.model, K, seed=1)
+    before = len(tr.buffer)
+    res = snk.laplace_sampling_(tr, lap, n_models=6, seed=13, chunk=4)
+    ref_r, ref_l, ref_m = _oracle_greedy_episode(bs, C, tr.model.get_params())
+    if ref_m > 1e-4:
+        assert res["tr_reward"] == np.float32(ref_r)
+    checked = 0
+    for n in range(6):
+        w = snk.sample_model(lap, tr.model, n=n, seed=13)
+        r, L, margin = _oracle_greedy_episode(bs, C, w)
+        if margin > 1e-4:
+            assert res["rewards"][n] == np.float32(r) and res["lengths"][n] == L, (n, res["rewards"][n], r)
+            checked += 1
+    assert checked >= 3
+    better = [n for n in range(6) if res["rewards"][n] > res["tr_reward"]]
+    assert res["n_better_models"] == len(better)
+    grown = int(sum(res["lengths"][n] for n in better))
+    assert len(tr.buffer) == before + grown
+    if grown:
+        got = snk.stack_exp(tr.buffer, np.arange(before, before + grown, dtype=np.int64))
+        o = 0
+        for n in better:
+            L = int(res["lengths"][n])
+            s = np.float32(0)
+            for v in got["rewards"][o:o + L]:
+                s = np.float32(s + np.float32(v))
+            assert s == res["rewards"][n] and got["dones"][o + L - 1]
+            o += L
