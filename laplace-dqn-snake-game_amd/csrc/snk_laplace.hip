@@ -735,7 +735,7 @@ static void lap_rollout(snk_dqn m, const float *W, int64_t ldw, int64_t G, float
     SNK_HIP(hipMemsetAsync(len_dev, 0, G * sizeof(int32_t), s));
     const size_t lds = (size_t)lap_act_lds_floats(L) * sizeof(float);
     SNK_CHECK(lds <= 160 * 1024 && L.Wo * L.Wo <= 64 && L.K1 % 4 == 0 && L.off_w3 % 4 == 0 && L.off_d1w % 4 == 0 &&
-                  ldw % 4 == 0,
+                  (G == 1 || ldw % 4 == 0),
               SNK_ERR_INVALID,
               "Laplace sampling: board side %d too large", L.bs);
     static size_t attr = 0;
