@@ -1,0 +1,54 @@
+"""Per-kernel counter summary of the counter-only passes tools/pmc_h3.sh /
+tools/pmc_syrk.sh write (p1: SQ cycles, p2: FETCH_SIZE + GRBM_GUI_ACTIVE,
+p3: WRITE_SIZE + TCC hit/miss, p4: instruction counts).
+
+usage: python tools/pmc_summary.py <pmc dir> <out.json> [kernel substrings...]
+
+mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), kernel
+cycles = GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs);
+hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB; FETCH_SIZE doubled per
+MI355X_MICROARCH.md's gfx950 note); all per launch (mean over launches).
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def load(d):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for p in ("p1", "p2", "p3", "p4"):
+        f = os.path.join(d, p, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+
+
+def main():
+    d, out = sys.argv[1], sys.argv[2]
+    keys = sys.argv[3:]
+    res = {}
+    for k, c in load(d).items():
+        if keys and not any(s in k for s in keys):
+            continue
+        row = {"counters": c}
+        cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8.0
+        if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+            row["mfma_busy"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc)
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            row["hbm_bytes"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+        if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c and c["SQ_LDS_IDX_ACTIVE"]:
+            row["lds_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+        if "TCC_HIT" in c and "TCC_MISS" in c and (c["TCC_HIT"] + c["TCC_MISS"]):
+            row["l2_hit"] = c["TCC_HIT"] / (c["TCC_HIT"] + c["TCC_MISS"])
+        res[k.replace("void snk::", "").replace("snk::", "")[:90]] = row
+    json.dump(res, open(out, "w"), indent=1)
+    for k, r in res.items():
+        print(k[:60], {x: round(y, 3) for x, y in r.items() if x != "counters" and isinstance(y, float)})
+
+
+if __name__ == "__main__":
+    main()
