@@ -4,8 +4,9 @@ p3: WRITE_SIZE + TCC hit/miss, p4: instruction counts).
 
 usage: python tools/pmc_summary.py <pmc dir> <out.json> [kernel substrings...]
 
-mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), kernel
-cycles = GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs);
+mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x 2.4 GHz x the dispatch's
+duration in the same pass (End - Start timestamps)): the fraction of the
+nominal dense MFMA peak;
 hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB; FETCH_SIZE doubled per
 MI355X_MICROARCH.md's gfx950 note); all per launch (mean over launches).
 """
@@ -22,8 +23,12 @@ def load(d):
         f = os.path.join(d, p, "run_counter_collection.csv")
         if not os.path.exists(f):
             continue
+        seen = set()
         for r in csv.DictReader(open(f)):
             agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if p == "p1" and r["Dispatch_Id"] not in seen:   # one duration per dispatch
+                seen.add(r["Dispatch_Id"])
+                agg[r["Kernel_Name"]]["duration_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
 
 
@@ -35,7 +40,7 @@ def main():
         if keys and not any(s in k for s in keys):
             continue
         row = {"counters": c}
-        cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8.0
+        cyc = c.get("duration_ns", 0) * 2.4
         if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
             row["mfma_busy"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc)
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
