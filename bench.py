@@ -244,6 +244,12 @@ def main():
         elapsed = float(t.item())
     st = tr.stats()
     faults = tr.game.check_faults()
+    if comm is not None:
+        # every rank leaves the RCCL group together: rank 0's extras below keep
+        # training locally (snapshots) and must not wait on ranks that have exited
+        _lib.call("snk_synchronize")
+        dist.barrier()
+        snk.dist_detach(tr)
 
     out = {
         "metric": "env-steps/sec/GPU @4096 envs + D(50k) build sec, 1/2/4/8 MI355X",
@@ -336,7 +342,7 @@ def main():
             del gl, rl, al
         except Exception as e:   # report, do not fail the headline line
             out["step_kernel_large"] = {"error": str(e)}
-    if rank == 0 and not args.no_dbuild:
+    if rank == 0 and world == 1 and not args.no_dbuild:   # single-GPU measurements (configs[4])
         out.update(d_build(args, snk, tr))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)

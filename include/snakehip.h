@@ -218,7 +218,8 @@ int snk_comm_destroy(snk_comm c);
 int snk_comm_allreduce_mean(snk_comm c, float *buf_dev, int64_t n);
 int snk_comm_broadcast(snk_comm c, float *buf_dev, int64_t n, int32_t root);
 /* the trainer all-reduces (mean) the gradient of every update across the
- * communicator; broadcasts rank 0's q_net first */
+ * communicator; broadcasts rank 0's q_net first. c = NULL detaches (updates
+ * are local again; nothing is broadcast) */
 int snk_trainer_set_comm(snk_trainer t, snk_comm c);
 
 /* ---------------------------------------------------------------- Laplace D

@@ -13,7 +13,7 @@ from .replay import (ReplayBuffer, empty_buffer_, isfull, isready, sample, stack
                      store_)
 from ._lib import SNK_NET_GRAD, SNK_NET_OPT_STATE, SNK_NET_Q, SNK_NET_TARGET  # noqa: F401
 from .qnet import DQNModel, nparams, update_target_net_  # noqa: F401
-from .dist import Comm, aggregate_throughput, dist_attach  # noqa: F401
+from .dist import Comm, aggregate_throughput, dist_attach, dist_detach  # noqa: F401
 from .trainer import Trainer, epsilon_greedy, fill_buffer_, play_episode, train_  # noqa: F401
 from .laplace import (LaplaceD, compute_D, jacobian, jacobian_gram, laplace_normals,  # noqa: F401
                       laplace_sampling_, sample_model)

@@ -290,16 +290,18 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
 
 extern "C" int snk_trainer_set_comm(snk_trainer h, snk_comm comm) {
     return guard([&] {
-        SNK_CHECK(h && comm, SNK_ERR_INVALID, "NULL argument");
+        SNK_CHECK(h, SNK_ERR_INVALID, "NULL argument");
         hipStream_t s = stream();
         snk_dqn_s *q = h->dqn;
-        // replicas start from rank 0's q_net; t_net = q_net; fresh RMSProp state
-        comm_broadcast(comm, q->theta_q, q->L.P, 0, s);
-        dqn_q_changed(q, s);
-        dqn_sync_target_launch(q, nullptr, 1, s);
-        SNK_HIP(hipMemsetAsync(q->acc, 0, q->L.P * sizeof(float), s));
+        if (comm) {
+            // replicas start from rank 0's q_net; t_net = q_net; fresh RMSProp state
+            comm_broadcast(comm, q->theta_q, q->L.P, 0, s);
+            dqn_q_changed(q, s);
+            dqn_sync_target_launch(q, nullptr, 1, s);
+            SNK_HIP(hipMemsetAsync(q->acc, 0, q->L.P * sizeof(float), s));
+        }
         SNK_HIP(hipStreamSynchronize(s));
-        h->comm = comm;
+        h->comm = comm;   // NULL: detach (updates local again)
         for (int i = 0; i < 2; ++i) {   // captured graphs predate the collective
             if (h->exec[i]) (void)hipGraphExecDestroy(h->exec[i]);
             if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);

@@ -76,3 +76,11 @@ def dist_attach(trainer, dist, rank: int, world: int) -> Comm:
     call("snk_trainer_set_comm", trainer.handle, comm.handle)
     trainer._comm = comm
     return comm
+
+
+def dist_detach(trainer) -> None:
+    """Leave the data-parallel group: later updates stay local (no collective),
+    so one rank can keep training (e.g. rank 0's D builds after a timed
+    multi-GPU run) while the others exit."""
+    call("snk_trainer_set_comm", trainer.handle, None)
+    trainer._comm = None

@@ -37,3 +37,26 @@ def test_comm_allreduce_and_broadcast(snk):
     snk._lib.call("snk_comm_broadcast", comm.handle, d.ptr, 1000, 0)
     snk._lib.call("snk_synchronize")
     assert np.array_equal(d.numpy(), x)
+
+
+def test_detach_then_train_locally(snk):
+    """dist_detach (bench.py before rank 0's single-GPU extras): a trainer that
+    leaves its communicator keeps training with local updates and its
+    recaptured graphs; a 1-rank run detached half way matches the plain run."""
+    def run(detach):
+        tr = snk.Trainer(n_batches=20, target_update_rate=8, n_envs=96, board_size=12, n_frames=2, capacity=600,
+                         decay=1e-3, seed=5)
+        if detach:
+            comm = snk.Comm(1, 0, snk.Comm.unique_id())
+            snk._lib.call("snk_trainer_set_comm", tr.handle, comm.handle)
+            tr._comm = comm
+        snk.fill_buffer_(tr)
+        tr.run(10, learn=True, graph=True)
+        if detach:
+            snk.dist_detach(tr)
+            assert tr._comm is None
+        tr.run(10, learn=True, graph=True)
+        return tr.model.get_params(), tr.losses
+    p0, l0 = run(False)
+    p1, l1 = run(True)
+    assert np.array_equal(p0, p1) and np.array_equal(l0, l1)
