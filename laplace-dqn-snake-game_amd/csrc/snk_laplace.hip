@@ -173,8 +173,8 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s) {
         }
     } else if (a.xh && !nox3) {
         SNK_CHECK(out == SYRK_F32 && z == 1 && a.ldh % SY_KS == 0 && a.xe, SNK_ERR_INTERNAL, "syrk h3 arguments");
-        static const bool w4 = getenv("SNK_SYRK_W4") != nullptr;   // 4 waves of 64 x 64 (one per SIMD)
-        if (w4)
+        static const char *hk = getenv("SNK_SYRK_H3K");   // "4": 4 waves of 64 x 64 (one per SIMD)
+        if (hk && strcmp(hk, "4") == 0)
             syrk_h3_kernel<4><<<grid, 256, 0, s>>>(a);
         else if (getenv("SNK_SYRK_PRIO"))
             syrk_h3_kernel<8, true><<<grid, 512, 0, s>>>(a);
@@ -397,12 +397,15 @@ extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_d
         if (!senv || strcmp(senv, "h3") == 0) {
             // h3 Gram: rows pre-split once into scaled fp16 planes (snk_syrk.hpp h3_rows_kernel)
             const int64_t ldh = (Kc + SY_KS - 1) / SY_KS * SY_KS;
-            if (2 * n * ldh > m->jplanes_halves) {
+            const int64_t npad = (n + SW_ROWS_B - 1) / SW_ROWS_B * SW_ROWS_B;   // zero rows past n (whole row blocks)
+            if (2 * npad * ldh > m->jplanes_halves) {
                 (void)hipStreamSynchronize(s);
                 dfree(m->jplanes);
-                m->jplanes = dalloc<uint16_t>(2 * n * ldh);
-                m->jplanes_halves = 2 * n * ldh;
+                m->jplanes = dalloc<uint16_t>(2 * npad * ldh);
+                m->jplanes_halves = 2 * npad * ldh;
             }
+            if (npad > n)
+                SNK_HIP(hipMemsetAsync(m->jplanes + 2 * n * ldh, 0, (size_t)(npad - n) * 2 * ldh * sizeof(uint16_t), s));
             if (n > m->jexp_cap) {
                 (void)hipStreamSynchronize(s);
                 dfree(m->jexp);

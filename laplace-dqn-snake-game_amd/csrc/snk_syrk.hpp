@@ -562,6 +562,8 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
         }
 }
 
+constexpr int SW_ROWS_B = 256;   // Jacobian-plane rows are padded to a multiple of this
+
 union SyrkSmem {
     SyrkLds f32;
     SyrkX6Lds x6;

@@ -1,5 +1,3 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 120 python tools/dbuild.py 16384 2 2>&1 | tail -1
-SNK_SYRK_PRIO=1 timeout -k 10 120 python tools/dbuild.py 16384 2 2>&1 | tail -1
-SNK_SYRK_EXP_NOLOAD=1 timeout -k 10 120 python tools/dbuild.py 16384 2 2>&1 | tail -1
-SNK_SYRK_ORDER=rows timeout -k 10 120 python tools/dbuild.py 16384 2 2>&1 | tail -1
+timeout -k 10 300 python -u -m pytest tests/test_laplace_gpu.py -q --timeout 200 --timeout-method thread -k "gram" 2>&1 | tail -2
+timeout -k 10 200 python tools/dbuild.py 50000 2 2>&1 | tail -1
