@@ -330,6 +330,147 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     }
 }
 
+// conv2 (3x3, 16 -> 32, pad 1, EPI_BIAS_RELU) of a large batch on the h3 split.
+// A workgroup (4 waves) owns two whole samples: their fp32 conv1 outputs are
+// staged with a per-sample power-of-two scale as fp16 h/l parts into LDS inside
+// a zero border ([sample][part][(BS+2)^2 positions][24 halves]: 48-byte
+// position rows, conflict-free for 16 consecutive positions), and the whole
+// weight tensor goes to LDS once (scale from its own max, split, paired
+// offsets: k = 16 * (kk - 2p) + ci for offset pair p, the 10th offset zero).
+// Each wave then runs its 16-row tiles over the 5 offset pairs on
+// v_mfma_f32_16x16x32_f16 with every B fragment held in registers: no barrier
+// after the staging. Output: fp32 a2 (the h3s conv3 consumes it).
+template <int BS>
+__global__ __launch_bounds__(256) void conv_h3c2_kernel(const float *__restrict__ x, const float *__restrict__ wimg,
+                                                        const float *__restrict__ bias, float *__restrict__ out, int S) {
+    constexpr int BP = BS + 2, NPB = BP * BP, NC = BS * BS, NSG = 2, XR = 24, BR = 40;
+    constexpr int ROWS = NSG * NC, T = (ROWS + 15) / 16;
+    constexpr int A_H = NSG * 2 * NPB * XR;          // halves of the A image
+    constexpr int B_H = 5 * 2 * 32 * BR;             // halves of the B image
+    extern __shared__ __attribute__((aligned(16))) uint16_t c2l[];
+    uint16_t *As = c2l, *Bs = c2l + A_H;
+    __shared__ float red[4][3];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int s0 = blockIdx.x * NSG, ns = min(NSG, S - s0);
+    // zero the A image (borders) and the pad offset of B
+    for (int q = tid; q < A_H / 8; q += 256) reinterpret_cast<u32x4 *>(As)[q] = u32x4{0, 0, 0, 0};
+    for (int q = tid; q < B_H / 8; q += 256) reinterpret_cast<u32x4 *>(Bs)[q] = u32x4{0, 0, 0, 0};
+    // loads: weights (9 x 32 x 16 fp32 = 1152 float4) and the two samples' a1 (2 x NC x 16 = 8*NC float4)
+    constexpr int NW4 = 9 * 32 * 16 / 4, NA4 = NSG * NC * 4, LW = (NW4 + 255) / 256, LA = (NA4 + 255) / 256;
+    f32x4 wv[LW], av[LA];
+    const f32x4 *w4 = reinterpret_cast<const f32x4 *>(wimg);
+    const f32x4 *x4 = reinterpret_cast<const f32x4 *>(x) + (int64_t)s0 * NC * 4;
+    const int na4 = ns * NC * 4;
+#pragma unroll
+    for (int u = 0; u < LW; ++u) wv[u] = w4[min(u * 256 + tid, NW4 - 1)];
+#pragma unroll
+    for (int u = 0; u < LA; ++u) av[u] = x4[min(u * 256 + tid, na4 - 1)];
+    float mw = 0.0f, m0 = 0.0f, m1 = 0.0f;
+#pragma unroll
+    for (int u = 0; u < LW; ++u) {
+        const f32x4 v = wv[u];
+        if (u * 256 + tid < NW4)
+            mw = fmaxf(mw, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+        const int e = u * 256 + tid;
+        const f32x4 v = av[u];
+        const float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+        if (e < na4) {
+            if (e < NC * 4) m0 = fmaxf(m0, m);
+            else m1 = fmaxf(m1, m);
+        }
+    }
+    mw = wave_max(mw);
+    m0 = wave_max(m0);
+    m1 = wave_max(m1);
+    if (lane == 0) {
+        red[wave][0] = mw; red[wave][1] = m0; red[wave][2] = m1;
+    }
+    __syncthreads();   // also: the zero fill is done
+    const int ew = h3_exp(fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0])));
+    const int ea0 = h3_exp(fmaxf(fmaxf(red[0][1], red[1][1]), fmaxf(red[2][1], red[3][1])));
+    const int ea1 = h3_exp(fmaxf(fmaxf(red[0][2], red[1][2]), fmaxf(red[2][2], red[3][2])));
+    u32x2 *As2 = reinterpret_cast<u32x2 *>(As), *Bs2 = reinterpret_cast<u32x2 *>(Bs);
+#pragma unroll
+    for (int u = 0; u < LW; ++u) {   // image [kk][co][ci]: float4 e -> kk, co, ci0 = 4 * (e & 3)
+        const int e = u * 256 + tid;
+        if (e < NW4) {
+            const int kk = e >> 7, co = (e >> 2) & 31, ci0 = 4 * (e & 3);
+            const int p = kk >> 1, k0 = 16 * (kk & 1) + ci0;
+            u32x2 hh, ll;
+            h3_split4(wv[u], ew, hh, ll);
+            Bs2[(((p * 2 + 0) * 32 + co) * BR + k0) / 4] = hh;
+            Bs2[(((p * 2 + 1) * 32 + co) * BR + k0) / 4] = ll;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {   // a1 [s][pos][16]: float4 e -> sample, position, channels 4*(e & 3)
+        const int e = u * 256 + tid;
+        if (e < na4) {
+            const int sr = e / (NC * 4), loc = e - sr * NC * 4;
+            const int pos = loc >> 2, c0 = 4 * (loc & 3);
+            const int j = pos / BS, i = pos - j * BS;
+            const int pb = (i + 1) + (j + 1) * BP;
+            u32x2 hh, ll;
+            h3_split4(av[u], sr ? ea1 : ea0, hh, ll);
+            As2[(((sr * 2 + 0) * NPB + pb) * XR + c0) / 4] = hh;
+            As2[(((sr * 2 + 1) * NPB + pb) * XR + c0) / 4] = ll;
+        }
+    }
+    __syncthreads();
+    const int r = lane & 15, g = lane >> 4;
+    // every B fragment of the layer in registers: [pair][col tile][part]
+    u32x4 bf[5][2][2];
+#pragma unroll
+    for (int p = 0; p < 5; ++p)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+                bf[p][ct][pl] = *reinterpret_cast<const u32x4 *>(Bs + ((p * 2 + pl) * 32 + ct * 16 + r) * BR + 8 * g);
+    for (int t = wave; t < T; t += 4) {
+        const int q = min(t * 16 + r, ROWS - 1);
+        const int sr = q >= NC ? 1 : 0, pos = q - sr * NC;
+        const int j = pos / BS, i = pos - j * BS;
+        f32x4v acc[2] = {f32x4v{0.f, 0.f, 0.f, 0.f}, f32x4v{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int p = 0; p < 5; ++p) {
+            const int kk = min(2 * p + (g >> 1), 8), du = kk % 3, dv = kk / 3;
+            const int pb = (i + du) + (j + dv) * BP;
+            const uint16_t *pa = As + ((sr * 2) * NPB + pb) * XR + 8 * (g & 1);
+            const f16x8 ah = as_h(*reinterpret_cast<const u32x4 *>(pa));
+            const f16x8 al = as_h(*reinterpret_cast<const u32x4 *>(pa + NPB * XR));
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                f32x4v c = acc[ct];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, as_h(bf[p][ct][0]), c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, as_h(bf[p][ct][1]), c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, as_h(bf[p][ct][0]), c, 0, 0, 0);
+                acc[ct] = c;
+            }
+        }
+        // acc[ct][e]: row 4g + e of the tile, column 16 ct + r
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int row = t * 16 + 4 * g + e;
+            if (row >= ns * NC) continue;
+            const int es = (row >= NC ? ea1 : ea0) + ew;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int col = ct * 16 + r;
+                const float v = __builtin_ldexpf(acc[ct][e], -es) + bias[col];
+                out[((int64_t)s0 * NC + row) * 32 + col] = v > 0.0f ? v : 0.0f;
+            }
+        }
+    }
+}
+template <int BS>
+static inline size_t conv_h3c2_lds() {
+    return (size_t)(2 * 2 * (BS + 2) * (BS + 2) * 24 + 5 * 2 * 32 * 40) * sizeof(uint16_t);
+}
+
 // dynamic LDS bytes of conv_h3s_kernel for an HIN x HIN input (0: does not fit)
 static inline size_t conv_h3s_lds(int hin) {
     const int ho = hin - 5, XW = ho + 8, PL = (hin * XW + 3) & ~3, XS = 8 * PL + 4;

@@ -1175,9 +1175,40 @@ static bool h3s_ok(const QLayout &L, const FwdNet *net, int ng, int64_t S) {
            conv_splits(S * L.Wo * L.Wo * ng, 36) == 1;
 }
 
+template <int BS>
+static void h3c2_launch_bs(const float *a1, const float *wimg, const float *b2, float *a2, int64_t S, hipStream_t s) {
+    const size_t lds = conv_h3c2_lds<BS>();
+    static size_t attr = 0;
+    if (lds > attr) {
+        SNK_HIP(hipFuncSetAttribute((const void *)conv_h3c2_kernel<BS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+        attr = lds;
+    }
+    conv_h3c2_kernel<BS><<<(unsigned)ceil_div(S, 2), 256, lds, s>>>(a1, wimg, b2, a2, (int)S);
+    launch_check("conv_h3c2_kernel");
+}
+
+static void conv_h3c2_launch(const QLayout &L, const FwdNet &n, int64_t S, hipStream_t s) {
+    const float *a1 = n.w->a1, *wimg = n.wt + L.off_t2, *b2 = n.th + L.off_b2;
+    float *a2 = n.w->a2;
+    SNK_CHECK(S <= n.w->cap && S <= INT32_MAX, SNK_ERR_INTERNAL, "h3 conv2 batch");
+    switch (L.bs) {
+        case 8: h3c2_launch_bs<8>(a1, wimg, b2, a2, S, s); return;
+        case 9: h3c2_launch_bs<9>(a1, wimg, b2, a2, S, s); return;
+        case 10: h3c2_launch_bs<10>(a1, wimg, b2, a2, S, s); return;
+        case 11: h3c2_launch_bs<11>(a1, wimg, b2, a2, S, s); return;
+        case 12: h3c2_launch_bs<12>(a1, wimg, b2, a2, S, s); return;
+        case 13: h3c2_launch_bs<13>(a1, wimg, b2, a2, S, s); return;
+        default: SNK_CHECK(false, SNK_ERR_INTERNAL, "h3 conv2: board side outside 8..13");
+    }
+}
+
 static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi) {
     const int bs = L.bs, nc = L.ncell;
     const bool h3 = h3s_ok(L, net, ng, S);
+    // h3 also for conv2 (conv_h3c2_kernel): conv1 then writes fp32 a1 only. SNK_H3C2=0: x6 conv2.
+    static const bool c2on = !getenv("SNK_H3C2") || atoi(getenv("SNK_H3C2")) != 0;
+    const bool h3c2 = h3 && c2on;
     const int64_t n3 = 36LL * 32 * 64;   // conv3 weight image floats
     // x6: conv1 + conv2 fused into one kernel (layer 0; layer 1 is then empty)
     // measured slower than conv1 + conv2 (per-workgroup staging dominates): opt-in
@@ -1221,8 +1252,9 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         for (int g = 0; g < 2; ++g) {
             const FwdNet &n = net[g < ng ? g : 0];
             // x6: a1 also (acting: only) as bf16 planes for conv2
-            cp.g[g] = Conv1Args{n.src, n.th + L.off_w1, n.th + L.off_b1, (n.wtb && !n.w->has_train) ? nullptr : n.w->a1,
-                                n.wtb ? n.w->a1b : nullptr, n.w->has_train ? n.w->x0 : nullptr,
+            cp.g[g] = Conv1Args{n.src, n.th + L.off_w1, n.th + L.off_b1,
+                                (n.wtb && !n.w->has_train && !h3c2) ? nullptr : n.w->a1,
+                                (n.wtb && !h3c2) ? n.w->a1b : nullptr, n.w->has_train ? n.w->x0 : nullptr,
                                 h3 ? n.wt + L.off_t3 : nullptr, n3, h3 ? n.w->wmax_part : nullptr};
         }
         if (L.C == 1)
@@ -1237,7 +1269,9 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         }
     }
     FwdIO io[2];
-    if (lo <= 1 && hi >= 1) {   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
+    if (lo <= 1 && hi >= 1 && h3c2) {   // conv2 on the h3 kernel: fp32 a1 -> fp32 a2
+        for (int g = 0; g < ng; ++g) conv_h3c2_launch(L, net[g], S, s);
+    } else if (lo <= 1 && hi >= 1) {   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
         // x6: a2 also (acting: only) as bf16 planes for conv3; training keeps fp32 a2 for the backward
         for (int g = 0; g < ng; ++g) {
             const FwdNet &n = net[g];

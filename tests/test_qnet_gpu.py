@@ -201,6 +201,21 @@ def test_large_batch_forward_h3s_vs_oracle(snk):
     assert _qclose(q, qref), np.abs(q - qref).max()
 
 
+@pytest.mark.parametrize("bs,C", [(8, 1), (10, 2), (13, 2)])
+def test_large_batch_forward_h3_board_sizes(snk, bs, C):
+    """conv2 (conv_h3c2_kernel, two samples per workgroup) and conv3 on the h3
+    split at the other board sides: at 10 and 13 a 16-row tile straddles the
+    two samples (per-row exponents), 1027 samples leave a one-sample last
+    workgroup. Tolerance as the 12x12 case."""
+    rng = np.random.default_rng(bs)
+    B = 1027
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=bs + 1)
+    x = rng.integers(-1, 3, size=(B, C, bs * bs)).astype(np.float32)
+    q = m(x)
+    qref = oracle.qnet_forward(bs, C, m.get_params(), x)
+    assert _qclose(q, qref), np.abs(q - qref).max()
+
+
 @pytest.mark.parametrize("scale", [1.0, 3.0, 1e-3, 40.0])
 def test_h3s_error_class_vs_fp32(snk, scale, monkeypatch):
     """The h3 conv3 (fp16 parts of power-of-two-scaled operands, 3 MFMAs per
@@ -249,21 +264,22 @@ np.save(sys.argv[2], m(x))
 def test_x6s_bitexact_with_x6m16_and_h3s_close(tmp_path):
     """With the h3 kernel off (SNK_H3S=0), conv_x6s accumulates the six part
     products in x6m16's order: the Q values of a 2050-sample forward are
-    identical with SNK_X6S=1 and 0. The default (h3s) forward agrees with
-    them to 1e-5 * max(1, |q|)."""
+    identical with SNK_X6S=1 and 0. The default forward (conv2 and conv3 on
+    h3) and the h3-conv3-only one (SNK_H3C2=0) agree with them to
+    1e-5 * max(1, |q|)."""
     import os
     import subprocess
     import sys
     repo = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
     out = {}
     for tag, envs in (("x6s", {"SNK_H3S": "0", "SNK_X6S": "1"}), ("m16", {"SNK_H3S": "0", "SNK_X6S": "0"}),
-                      ("h3s", {})):
+                      ("h3c3", {"SNK_H3C2": "0"}), ("h3s", {})):
         f = str(tmp_path / f"q{tag}.npy")
         env = dict(os.environ, **envs)
         subprocess.run([sys.executable, "-c", _X6S_SCRIPT, repo, f], env=env, check=True, timeout=300)
         out[tag] = np.load(f)
     assert np.array_equal(out["x6s"], out["m16"])
-    assert _qclose(out["h3s"], out["x6s"])
+    assert _qclose(out["h3s"], out["x6s"]) and _qclose(out["h3c3"], out["x6s"])
 
 
 def test_train_episode_schedule(snk):
