@@ -1,0 +1,256 @@
+// snk_bwd3.hpp — conv3's backward for the small-batch DQN update (B = 64).
+//
+// The generic path ran conv3's weight gradient as a split-K GEMM whose lanes
+// gathered im2col elements one float at a time (two divisions per element:
+// VALU-bound, 19 us) and its data gradient as an implicit GEMM over the
+// HOUT^2 = bs^2 input positions, 4/5 of whose 36 kernel offsets fall outside
+// the Wo x Wo gradient (1.36 GFLOP of MFMA work for 0.34 useful, plus a
+// partial-slab reduce). Both are reorganised around LDS-staged samples, in
+// one launch (blocks [0, nW) weight gradient, the rest data gradient), on the
+// exact-fp32 v_mfma_f32_32x32x2_f32:
+//
+//  * dW (grid: Z chunks of 2 samples x 9 groups of four kernel offsets):
+//    the chunk's a2 [2][bs^2][32] and dz3 [2][Wo^2][64] go to LDS once;
+//    wave w owns offset kk = 4*group + w, a 32 (ci) x 64 (co) tile. MFMA k-step
+//    t = output position (io, jo), its two k lanes = the two samples:
+//    A[ci][s] = a2[s][(io + du, jo + dv)][ci], B[s][co] = dz3[s][(io, jo)][co],
+//    lane-consecutive LDS reads at wave-uniform offsets. The chunk's partial
+//    goes to slab z (the bias row: column sums of dz3, group 0) and
+//    grad_update_kernel sums the Z slabs.
+//  * dX (grid: S samples x 32/CG channel groups): T[pout][(kk, ci)] =
+//    sum_co dz3[s][pout][co] * W[kk][ci][co] (a dense GEMM, K = 64) into LDS,
+//    (v_mfma_f32_16x16x4_f32 tiles), then col2im: dz2[s][pin][ci] = sum over the offsets with
+//    pout = pin - (du, dv) inside the Wo x Wo grid of T[pout][(kk, ci)],
+//    kk ascending, relu-masked by a2. No wasted products, no slab, no reduce.
+#pragma once
+#include "snk_conv.hpp"
+
+namespace snk {
+
+struct Conv3BwdArgs {
+    const float *a2;    // [S][bs*bs][32]  conv2 output (relu'd)
+    const float *dz3;   // [S][wo*wo][64]  gradient at conv3's pre-activation
+    const float *w;     // conv3 weights, parameter layout [36 kk][32 ci][64 co]
+    float *slab;        // dW partials [Z][1153][64] (row 1152: bias)
+    float *dz2;         // [S][bs*bs][32]
+    int S, bs, wo, nsc, Z, nW;
+    int boff;           // first block index of this launch (the halves as separate launches: profiling)
+    uint64_t *dbg;      // SNK_C3_DBG: per-block [clock at start, staged, computed, end, wall start, wall end]
+};
+#define C3_TS(k)                                                                  \
+    do {                                                                          \
+        if (a.dbg && threadIdx.x == 0) a.dbg[(blockIdx.x + a.boff) * 8 + (k)] = clock64(); \
+    } while (0)
+
+constexpr int C3_CG = 4;          // dX input channels per workgroup
+constexpr int C3_DLD = 68;        // LDS row stride of dz3 / weights in dX (16x16x4 reads conflict-free)
+constexpr int C3_TLD = 36 * C3_CG + 1;
+
+__host__ __device__ inline int c3_dw_lds_floats(int bs, int wo, int nsc) {
+    return nsc * bs * bs * 32 + nsc * wo * wo * 64;
+}
+__host__ __device__ inline int c3_dx_lds_floats(int wo) {   // T overlays the staged operands
+    const int op = wo * wo * C3_DLD + 36 * C3_CG * C3_DLD, t = wo * wo * C3_TLD;
+    return op > t ? op : t;
+}
+
+// global -> LDS copies with U loads in flight per thread (a plain strided loop
+// waits for each load before the next: ~20 serialised round trips per block)
+template <int U>
+__device__ __forceinline__ void c3_copy(f32x4 *__restrict__ dst, const f32x4 *__restrict__ src, int n) {
+    for (int b = 0; b < n; b += U * 256) {
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * 256 + (int)threadIdx.x;
+            v[u] = src[e < n ? e : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * 256 + (int)threadIdx.x;
+            if (e < n) dst[e] = v[u];
+        }
+    }
+}
+// rows of 64 floats -> LDS rows of C3_DLD floats; row e>>4 of the source at src + srow(e>>4)*64
+template <int U, class F>
+__device__ __forceinline__ void c3_copy_rows(float *__restrict__ dst, const float *__restrict__ src, int rows, F srow) {
+    const int n = rows * 16;
+    for (int b = 0; b < n; b += U * 256) {
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * 256 + (int)threadIdx.x;
+            const int ee = e < n ? e : 0;
+            v[u] = *reinterpret_cast<const f32x4 *>(src + (int64_t)srow(ee >> 4) * 64 + (ee & 15) * 4);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = b + u * 256 + (int)threadIdx.x;
+            if (e < n) *reinterpret_cast<f32x4 *>(dst + (e >> 4) * C3_DLD + (e & 15) * 4) = v[u];
+        }
+    }
+}
+
+template <int WO>
+__device__ __forceinline__ void c3_dw_block(const Conv3BwdArgs &a, int z, int grp, float *sm) {
+    // lane half h takes sample s0 + h of the chunk (NSC = 2), the k-step t its position t:
+    // every lane's im2col address follows from the wave-uniform (io, jo) of t
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int bs2 = a.bs * a.bs, wo2 = WO * WO;
+    const int s0 = z * 2, ns = min(2, a.S - s0);
+    float *A = sm, *D = sm + 2 * bs2 * 32;
+    c3_copy<12>(reinterpret_cast<f32x4 *>(A), reinterpret_cast<const f32x4 *>(a.a2 + (int64_t)s0 * bs2 * 32),
+                ns * bs2 * 8);
+    c3_copy<8>(reinterpret_cast<f32x4 *>(D), reinterpret_cast<const f32x4 *>(a.dz3 + (int64_t)s0 * wo2 * 64),
+               ns * wo2 * 16);
+    __syncthreads();
+    C3_TS(1);
+    const int r = lane & 31, h = lane >> 5;
+    const int kk = grp * 4 + wave;
+    const int dv = kk / 6, du = kk - dv * 6;
+    const bool hv = h < ns;
+    const float *pa = A + ((hv ? h : 0) * bs2 + du + dv * a.bs) * 32 + r;
+    const float *pd = D + (hv ? h : 0) * wo2 * 64 + r;
+    f32x16 acc[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[nt][g] = 0.0f;
+    for (int jo = 0; jo < WO; ++jo) {
+        const float *ra = pa + jo * a.bs * 32;
+        const float *rd = pd + jo * WO * 64;
+#pragma unroll
+        for (int io = 0; io < WO; ++io) {
+            const float x = ra[io * 32], y0 = rd[io * 64], y1 = rd[io * 64 + 32];
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv ? x : 0.0f, y0, acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv ? x : 0.0f, y1, acc[1], 0, 0, 0);
+        }
+    }
+    C3_TS(2);
+    float *out = a.slab + (int64_t)z * 1153 * 64;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) out[(kk * 32 + acc_row(g, lane)) * 64 + nt * 32 + r] = acc[nt][g];
+    if (grp == 0) {   // bias row: column sums of the chunk's dz3 (four partial runs, then in order)
+        __shared__ float bpart[4][64];
+        const int K = ns * wo2, co = tid & 63, q = tid >> 6, len = (K + 3) / 4;
+        const int k0 = q * len, k1 = min(K, k0 + len);
+        float b = 0.0f;
+        int k = k0;
+        for (; k + 8 <= k1; k += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = D[(k + u) * 64 + co];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) b += v[u];
+        }
+        for (; k < k1; ++k) b += D[k * 64 + co];
+        bpart[q][co] = b;
+        __syncthreads();
+        if (tid < 64) out[1152 * 64 + tid] = ((bpart[0][tid] + bpart[1][tid]) + bpart[2][tid]) + bpart[3][tid];
+    }
+}
+
+typedef float f32x4m __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg, float *sm) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int bs2 = a.bs * a.bs, wo2 = a.wo * a.wo;
+    constexpr int NN = 36 * C3_CG;   // T columns (kk, ci)
+    float *Dz = sm, *Wl = sm + wo2 * C3_DLD, *Tl = sm;
+    // relu-mask values of this block's outputs, loaded now (used by the col2im)
+    constexpr int NMK = 3;   // (pin, ci) per thread: bs^2 * CG <= 3 * 256 for bs <= 13
+    float mk[NMK];
+#pragma unroll
+    for (int u = 0; u < NMK; ++u) {
+        const int e = u * 256 + tid, ee = e < bs2 * C3_CG ? e : 0;
+        mk[u] = a.a2[((int64_t)s * bs2 + ee / C3_CG) * 32 + cg * C3_CG + ee % C3_CG];
+    }
+    // dz3[s] and W[kk][cg*CG + ci][co] (row n = kk*CG + ci)
+    c3_copy_rows<4>(Dz, a.dz3 + (int64_t)s * wo2 * 64, wo2, [](int row) { return row; });
+    c3_copy_rows<9>(Wl, a.w, NN, [cg](int n) { return (n / C3_CG) * 32 + cg * C3_CG + n % C3_CG; });
+    __syncthreads();
+    C3_TS(1);
+    // T in 16x16 tiles (v_mfma_f32_16x16x4_f32: lane l holds A[l&15][k + (l>>4)],
+    // B[k + (l>>4)][l&15]; C rows 4*(l>>4) + e, column l&15), round robin over the waves
+    // (all tiles kept in registers, then written over the operands after a barrier)
+    const int r = lane & 15, g = lane >> 4;
+    const int rt = (wo2 + 15) / 16, ct = NN / 16;
+    constexpr int MT = 9;   // tiles per wave: rt <= 4 (Wo <= 8), ct = 9
+    f32x4m acc[MT];
+#pragma unroll
+    for (int u = 0; u < MT; ++u) {
+        const int t = wave + 4 * u;
+        acc[u] = f32x4m{0.0f, 0.0f, 0.0f, 0.0f};
+        if (t < rt * ct) {
+            const int tr = t / ct, tc = t - tr * ct;
+            const float *pa = Dz + min(tr * 16 + r, wo2 - 1) * C3_DLD + g;
+            const float *pb = Wl + (tc * 16 + r) * C3_DLD + g;
+#pragma unroll
+            for (int k = 0; k < 64; k += 4) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[k], pb[k], acc[u], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < MT; ++u) {
+        const int t = wave + 4 * u;
+        if (t < rt * ct) {
+            const int tr = t / ct, tc = t - tr * ct;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int rr = tr * 16 + 4 * g + e;
+                if (rr < wo2) Tl[rr * C3_TLD + tc * 16 + r] = acc[u][e];
+            }
+        }
+    }
+    __syncthreads();
+    C3_TS(2);
+    // col2im + relu mask, (pin, ci) per thread: the 36 terms load together (out-of-grid
+    // terms read a valid slot and add 0), summed kk ascending
+#pragma unroll
+    for (int u = 0; u < NMK; ++u) {
+        const int e = u * 256 + tid;
+        if (e >= bs2 * C3_CG) break;
+        const int pin = e / C3_CG, ci = e - pin * C3_CG;
+        const int j = pin / a.bs, i = pin - j * a.bs;
+        float t[36];
+#pragma unroll
+        for (int kk = 0; kk < 36; ++kk) {
+            const int dv = kk / 6, du = kk - dv * 6;
+            const int io = i - du, jo = j - dv;
+            const bool v = io >= 0 && io < a.wo && jo >= 0 && jo < a.wo;
+            const float x = Tl[(v ? io + jo * a.wo : 0) * C3_TLD + kk * C3_CG + ci];
+            t[kk] = v ? x : 0.0f;
+        }
+        float v = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < 36; ++kk) v += t[kk];
+        const int64_t o = ((int64_t)s * bs2 + pin) * 32 + cg * C3_CG + ci;
+        a.dz2[o] = mk[u] > 0.0f ? v : 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float c3sm[];
+    const int b = blockIdx.x + a.boff;
+    C3_TS(0);
+    if (a.dbg && threadIdx.x == 0) a.dbg[b * 8 + 4] = wall_clock64();
+    if (b < a.nW) {
+        switch (a.wo) {
+            case 3: c3_dw_block<3>(a, b / 9, b % 9, c3sm); break;
+            case 4: c3_dw_block<4>(a, b / 9, b % 9, c3sm); break;
+            case 5: c3_dw_block<5>(a, b / 9, b % 9, c3sm); break;
+            case 6: c3_dw_block<6>(a, b / 9, b % 9, c3sm); break;
+            case 7: c3_dw_block<7>(a, b / 9, b % 9, c3sm); break;
+            default: c3_dw_block<8>(a, b / 9, b % 9, c3sm); break;
+        }
+    } else
+        c3_dx_block(a, (b - a.nW) / (32 / C3_CG), (b - a.nW) % (32 / C3_CG), c3sm);
+    __syncthreads();
+    C3_TS(3);
+    if (a.dbg && threadIdx.x == 0) a.dbg[b * 8 + 5] = wall_clock64();
+}
+
+}  // namespace snk

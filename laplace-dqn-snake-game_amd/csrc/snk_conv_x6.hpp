@@ -75,22 +75,26 @@ __device__ __forceinline__ uint16_t split_part(float x, int p) {
 }
 
 // PRE: A comes pre-split (a.xb, written by the producing layer's epilogue),
-// so the main loop does no conversion work at all
-template <int CK, int CN, int KS, int PAD, int MODE, int EPI, bool PRE>
-__global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
-    const ConvArgs &a = pr.g[blockIdx.z];
-    const uint16_t *__restrict__ wb = pr.wb[blockIdx.z];
+// so the main loop does no conversion work at all.
+// BSPLIT: the weights come as the fp32 image a.w ([kk][n][c]) and are split
+// while staged (one 8-channel piece per thread and offset at CN x CK = 2048:
+// the B = 64 conv3 data gradient, whose weights change every update).
+// MODE_DX: A = dz[s][p - (du,dv) + PAD][c] with the bounds check (HIN < HOUT).
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI, bool PRE, bool BSPLIT = false>
+__device__ __forceinline__ void conv_x6_body(const ConvPair &pr, dim3 bid) {
+    const ConvArgs &a = pr.g[bid.z];
+    const uint16_t *__restrict__ wb = pr.wb[bid.z];
     constexpr int NT = CN / 32;
     constexpr int KC = CK / 16;                  // 16-channel MFMA chunks per offset
     constexpr int LDB = CK + 8;                  // bf16 per LDS row
     constexpr int PLANE = CN * LDB;              // bf16 per LDS plane
-    constexpr int NE = 3 * CN * CK / 8;          // 16-byte pieces per staged block
-    constexpr int NV = (NE + 255) / 256;
+    constexpr int NE = BSPLIT ? CN * CK / 8 : 3 * CN * CK / 8;   // staged units per block: 8-channel
+    constexpr int NV = (NE + 255) / 256;                          //   pieces (BSPLIT) or 16-byte plane pieces
     __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * PLANE + 8];   // + pad piece for idle stagers
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int m = blockIdx.x * 128 + wave * 32 + r;
+    const int m = bid.x * 128 + wave * 32 + r;
     const bool ok = m < a.M;
     const int mm = ok ? m : 0;
     int s, i = 0, j = 0;
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
     }
     const float *xs = a.x + (int64_t)s * a.HIN * a.HIN * CK + 8 * h;
     const uint16_t *xsb = PRE ? a.xb + (int64_t)s * a.HIN * a.HIN * 3 * CK + 8 * h : nullptr;
-    const int kk0 = blockIdx.y * a.kk_per_split;
+    const int kk0 = bid.y * a.kk_per_split;
     const int kk1 = min(a.nkk, kk0 + a.kk_per_split);
 
     f32x16 acc[NT];
@@ -120,7 +124,7 @@ __global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
         const int e = tid + q * 256;
         const bool in = (NE % 256 == 0) || e < NE;
         const int ee = in ? e : 0;
-        const int pl = ee / (CN * CK / 8), rem = ee - pl * (CN * CK / 8);
+        const int pl = BSPLIT ? 0 : ee / (CN * CK / 8), rem = ee - pl * (CN * CK / 8);
         const int n = rem / (CK / 8), c8 = rem - n * (CK / 8);
         s_src[q] = ee;
         s_dst[q] = in ? pl * PLANE + n * LDB + c8 * 8 : 3 * PLANE;
@@ -130,8 +134,9 @@ __global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
     auto a_pos = [&](int kk) -> int {
         if (MODE == MODE_DENSE) return ok ? kk : -1;
         const int dv = kk / KS, du = kk - dv * KS;
-        const int xi = i + du - PAD, xj = j + dv - PAD;
-        if (PAD == 0) return xi + xj * a.HIN;   // always inside; rows past M are never stored
+        const int xi = MODE == MODE_DX ? i - du + PAD : i + du - PAD;
+        const int xj = MODE == MODE_DX ? j - dv + PAD : j + dv - PAD;
+        if (PAD == 0 && MODE == MODE_FWD) return xi + xj * a.HIN;   // always inside; rows past M are never stored
         const bool v = ok && xi >= 0 && xi < a.HIN && xj >= 0 && xj < a.HIN;
         return v ? xi + xj * a.HIN : -1;
     };
@@ -167,19 +172,44 @@ __global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
             const float msk = v ? 1.0f : 0.0f;
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc)
-                cur[kc] = (PAD == 0 && MODE != MODE_DENSE) ? split3(araw[2 * kc], araw[2 * kc + 1])
+                cur[kc] = (PAD == 0 && MODE == MODE_FWD) ? split3(araw[2 * kc], araw[2 * kc + 1])
                                                            : split3(araw[2 * kc] * msk, araw[2 * kc + 1] * msk);
         }
     };
 
-    u32x4 bst[NV];
+    u32x4 bst[NV][BSPLIT ? 2 : 1];
+    const u32x4 *wsrc32 = reinterpret_cast<const u32x4 *>(a.w);
+    auto b_load = [&](int kk) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            if (BSPLIT) {
+                bst[q][0] = wsrc32[((int64_t)kk * NE + s_src[q]) * 2];
+                bst[q][1] = wsrc32[((int64_t)kk * NE + s_src[q]) * 2 + 1];
+            } else {
+                bst[q][0] = wsrc[(int64_t)kk * NE + s_src[q]];
+            }
+        }
+    };
+    auto b_store = [&](uint16_t *B) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            if (BSPLIT) {
+                const Split3 sp = split3(__builtin_bit_cast(f32x4, bst[q][0]), __builtin_bit_cast(f32x4, bst[q][1]));
+                if (s_dst[q] < 3 * PLANE) {
+                    *reinterpret_cast<u32x4 *>(&B[s_dst[q]]) = sp.h;
+                    *reinterpret_cast<u32x4 *>(&B[s_dst[q] + PLANE]) = sp.m;
+                    *reinterpret_cast<u32x4 *>(&B[s_dst[q] + 2 * PLANE]) = sp.l;
+                }
+            } else {
+                *reinterpret_cast<u32x4 *>(&B[s_dst[q]]) = bst[q][0];
+            }
+        }
+    };
     Split3 acur[KC];
     {
-#pragma unroll
-        for (int q = 0; q < NV; ++q) bst[q] = wsrc[(int64_t)kk0 * NE + s_src[q]];
+        b_load(kk0);
         const bool v0 = a_load(kk0);
-#pragma unroll
-        for (int q = 0; q < NV; ++q) *reinterpret_cast<u32x4 *>(&Bs[0][s_dst[q]]) = bst[q];
+        b_store(Bs[0]);
         a_finish(v0, acur);
     }
     __syncthreads();
@@ -187,8 +217,7 @@ __global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
         const int buf = (kk - kk0) & 1;
         const bool more = kk + 1 < kk1;
         const int kn = more ? kk + 1 : kk;
-#pragma unroll
-        for (int q = 0; q < NV; ++q) bst[q] = wsrc[(int64_t)kn * NE + s_src[q]];
+        b_load(kn);
         const bool v_n = a_load(kn);
         __builtin_amdgcn_sched_barrier(0);
         const uint16_t *bb = &Bs[buf][r * LDB + 8 * h];
@@ -218,13 +247,12 @@ __global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
             for (int nt = 0; nt < NT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[nt], acc[nt], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < NV; ++q) *reinterpret_cast<u32x4 *>(&Bs[buf ^ 1][s_dst[q]]) = bst[q];
+        b_store(Bs[buf ^ 1]);
         __syncthreads();
         a_finish(v_n, acur);
     }
 
-    const int mrow0 = blockIdx.x * 128 + wave * 32;
+    const int mrow0 = bid.x * 128 + wave * 32;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         const int col = nt * 32 + r;
@@ -244,12 +272,21 @@ __global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
                     for (int pl = 0; pl < 3; ++pl) pb[pl * CN] = split_part(v, pl);
                 }
             } else if (EPI == EPI_SLAB) {
-                a.out[(int64_t)blockIdx.y * a.M * CN + o] = acc[nt][g];
+                a.out[(int64_t)bid.y * a.M * CN + o] = acc[nt][g];
             } else {
                 a.out[o] = a.act[o] > 0.0f ? acc[nt][g] : 0.0f;
             }
         }
     }
+}
+
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI, bool PRE>
+__global__ __launch_bounds__(256) void conv_x6_kernel(ConvPair pr) {
+    conv_x6_body<CK, CN, KS, PAD, MODE, EPI, PRE>(pr, blockIdx);
+}
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI>
+__global__ __launch_bounds__(256) void conv_x6_split_kernel(ConvPair pr) {
+    conv_x6_body<CK, CN, KS, PAD, MODE, EPI, false, true>(pr, blockIdx);
 }
 
 }  // namespace snk

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "snk_conv_h3.hpp"
+#include "snk_bwd3.hpp"
 #include "snk_conv_x6.hpp"
 #include "snk_qnet.hpp"
 
@@ -319,6 +320,13 @@ struct ConvJob {
     dim3 grid;
     __device__ void operator()(dim3 bid) const { conv_mfma_body<CK, CN, KS, PAD, MODE, EPI>(pr, bid); }
 };
+// the bf16x6 conv (snk_conv_x6.hpp) as a paired job; BSPLIT: weights split while staged
+template <int CK, int CN, int KS, int PAD, int MODE, int EPI, bool PRE, bool BSPLIT>
+struct ConvX6Job {
+    ConvPair pr;
+    dim3 grid;
+    __device__ void operator()(dim3 bid) const { conv_x6_body<CK, CN, KS, PAD, MODE, EPI, PRE, BSPLIT>(pr, bid); }
+};
 template <int NTH, class J1, class J2>
 __global__ __launch_bounds__(NTH) void pair_kernel(J1 j1, J2 j2) {
     const unsigned n1 = j1.grid.x * j1.grid.y * j1.grid.z;
@@ -366,6 +374,13 @@ static int conv_splits(int64_t M, int nkk) {
     static const int min_kk = getenv("SNK_SPLIT_MIN_KK") ? atoi(getenv("SNK_SPLIT_MIN_KK")) : 0;
     if (wgs >= 512 || nkk <= min_kk) return 1;
     return (int)std::min<int64_t>(std::min(nkk, 16), ceil_div(512, wgs));
+}
+
+// conv3 data gradients on the bf16x6 split (dz3 and the fp32 weights split in the
+// kernel: 2.7x the exact-fp32 MFMA rate, same error class); SNK_DX_X6=0: fp32 MFMA
+static bool dx_x6() {
+    static const bool on = !getenv("SNK_DX_X6") || atoi(getenv("SNK_DX_X6")) != 0;
+    return on;
 }
 
 // kk splits of the conv3 data gradient (36 offsets): SNK_DX_SPLITS overrides (tuning)
@@ -457,6 +472,13 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
                 case 13: h3s_launch<KS, EPI, 13>(pr, ng, splits, s); return;
                 default: SNK_CHECK(false, SNK_ERR_INTERNAL, "h3s conv3: board side outside 8..13");
             }
+        }
+    }
+    if constexpr (MODE == MODE_DX) {
+        if (dx_x6()) {   // bf16x6, dz and the fp32 weights split in the kernel
+            conv_x6_split_kernel<CK, CN, KS, PAD, MODE, EPI><<<grid, 256, 0, s>>>(pr);
+            launch_check("conv_x6_split_kernel");
+            return;
         }
     }
     if constexpr (MODE != MODE_DX) {
@@ -1365,10 +1387,25 @@ struct BwdPlan {
 };
 // waves per tile fixed so that the layer pairs (d1 wgrad | d1x: 2, c3 wgrad |
 // conv3 data grad: 4 = the conv kernel's 256 threads, c2 wgrad | c2x: 8) launch together
+// conv3's backward on conv3_bwd_kernel (snk_bwd3.hpp): both halves' LDS within a CU's
+// 160 KB (boards up to 13x13 at two samples per weight-gradient chunk). SNK_C3BWD=0: the
+// generic pair (gemm_body weight gradient | implicit-GEMM data gradient + reduce).
+constexpr int C3_NSC = 2;
+static bool c3bwd_ok(const QLayout &L, int64_t S) {
+    static const bool on = !getenv("SNK_C3BWD") || atoi(getenv("SNK_C3BWD")) != 0;
+    const size_t lim = 160 * 1024 / sizeof(float);
+    return on && S <= (1 << 24) && L.Wo >= 3 && L.Wo <= 8 && (size_t)c3_dw_lds_floats(L.bs, L.Wo, C3_NSC) <= lim &&
+           (size_t)c3_dx_lds_floats(L.Wo) <= lim;
+}
+
 static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
     BwdPlan p;
     p.d1 = plan_gemm_kw(L.K1 + 1, 64, 2, S, true, 2);
     p.c3 = plan_gemm_kw(1153, 64, 2, S * L.Wo * L.Wo, true, 4);
+    if (c3bwd_ok(L, S)) {   // slab z = the partial of samples [z*NSC, z*NSC + NSC)
+        const int64_t z = ceil_div(S, C3_NSC);
+        p.c3 = GemmPlan{4, (int)z, (int)(C3_NSC * L.Wo * L.Wo)};
+    }
     p.c2 = plan_gemm_kw(145, 32, 1, S * L.ncell, true, 8);
     p.c1 = plan_gemm(9 * L.C + 1, 16, 1, S * L.ncell, true);
     p.d1x = plan_gemm_kw(S, L.K1, 2, 64, false, 2);
@@ -1472,7 +1509,58 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
                          s);
         fin(p.d1, L.off_d1w, M1 * 64, slab + sr.d1);
         // conv3: dW over rows (s, pout) | dX onto the bs x bs x 32 input (relu mask on a2)
-        {
+        if (c3bwd_ok(L, S)) {
+            float *c3d = dst(1, p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
+            Conv3BwdArgs ca{w.a2, w.dz3, th + L.off_w3, c3d, w.dz2, (int)S, bs, L.Wo, C3_NSC, p.c3.z, p.c3.z * 9, 0, nullptr};
+            const size_t lds = (size_t)std::max(c3_dw_lds_floats(bs, L.Wo, C3_NSC), c3_dx_lds_floats(L.Wo)) * 4;
+            static size_t attr = 0;
+            if (lds > attr) {
+                SNK_HIP(hipFuncSetAttribute((const void *)conv3_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)lds));
+                attr = lds;
+            }
+            const unsigned nb = (unsigned)(ca.nW + S * (32 / C3_CG));
+            static const bool halves = getenv("SNK_UNPAIR") && atoi(getenv("SNK_UNPAIR")) != 0;
+            static bool dbg = getenv("SNK_C3_DBG") != nullptr;
+            if (dbg) {   // experiment (once): per-block phase clocks of each half, to stderr
+                dbg = false;
+                uint64_t *d = dalloc<uint64_t>((size_t)nb * 8);
+                ca.dbg = d;
+                conv3_bwd_kernel<<<(unsigned)ca.nW, 256, lds, s>>>(ca);
+                ca.boff = ca.nW;
+                conv3_bwd_kernel<<<nb - (unsigned)ca.nW, 256, lds, s>>>(ca);
+                launch_check("conv3_bwd_kernel");
+                std::vector<uint64_t> hb((size_t)nb * 8);
+                SNK_HIP(hipMemcpyAsync(hb.data(), d, hb.size() * 8, hipMemcpyDeviceToHost, s));
+                SNK_HIP(hipStreamSynchronize(s));
+                dfree(d);
+                for (int half = 0; half < 2; ++half) {
+                    const unsigned b0 = half ? (unsigned)ca.nW : 0, b1 = half ? nb : (unsigned)ca.nW;
+                    double ph[3] = {0, 0, 0};
+                    uint64_t w0 = ~0ull, w1 = 0, s1 = 0;
+                    for (unsigned b = b0; b < b1; ++b) {
+                        const uint64_t *q = &hb[(size_t)b * 8];
+                        for (int k = 0; k < 3; ++k) ph[k] += (double)(q[k + 1] - q[k]);
+                        w0 = std::min(w0, q[4]); w1 = std::max(w1, q[5]); s1 = std::max(s1, q[4]);
+                    }
+                    const double n = b1 - b0;
+                    fprintf(stderr, "c3bwd dbg %s: %u blocks, cycles: stage %.0f | compute %.0f | epilogue %.0f; "
+                            "wall %.2f us, last block start %.2f us\n", half ? "dX" : "dW", b1 - b0, ph[0] / n,
+                            ph[1] / n, ph[2] / n, (double)(w1 - w0) / 100.0, (double)(s1 - w0) / 100.0);
+                }
+                ca.dbg = nullptr;
+                ca.boff = 0;
+            }
+            if (halves) {   // profiling: weight-gradient blocks, then data-gradient blocks
+                conv3_bwd_kernel<<<(unsigned)ca.nW, 256, lds, s>>>(ca);
+                ca.boff = ca.nW;
+                conv3_bwd_kernel<<<nb - (unsigned)ca.nW, 256, lds, s>>>(ca);
+            } else {
+                conv3_bwd_kernel<<<nb, 256, lds, s>>>(ca);
+            }
+            launch_check("conv3_bwd_kernel");
+            fin(p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
+        } else {
             float *c3d = dst(1, p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
             const auto wj = gemm_job<2, 4>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)},
                                            BRows{w.dz3, S * no, 64}, EpSlab{c3d, 1153, 64}, 1153, 64, S * no, p.c3);
@@ -1481,16 +1569,28 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             a.nkk = 36;
             int sp = dx_splits(S * nc);
             const dim3 cg((unsigned)ceil_div(S * nc, 128), 1, 1);
+            const bool dx6 = dx_x6();
             if (sp == 1) {
                 a.out = w.dz2;
-                ConvJob<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
-                pair_launch<256>(wj, cj, s);
+                if (dx6) {
+                    ConvX6Job<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK, false, true> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
+                    pair_launch<256>(wj, cj, s);
+                } else {
+                    ConvJob<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
+                    pair_launch<256>(wj, cj, s);
+                }
             } else {
                 a.out = w.cslab;
                 SNK_CHECK((int64_t)sp * S * nc * 32 <= w.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
-                ConvJob<64, 32, 6, 0, MODE_DX, EPI_SLAB> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
-                cj.grid.y = (unsigned)sp;
-                pair_launch<256>(wj, cj, s);
+                if (dx6) {
+                    ConvX6Job<64, 32, 6, 0, MODE_DX, EPI_SLAB, false, true> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
+                    cj.grid.y = (unsigned)sp;
+                    pair_launch<256>(wj, cj, s);
+                } else {
+                    ConvJob<64, 32, 6, 0, MODE_DX, EPI_SLAB> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
+                    cj.grid.y = (unsigned)sp;
+                    pair_launch<256>(wj, cj, s);
+                }
                 const ReduceArgs ra{w.cslab, nullptr, w.a2, w.dz2, nullptr};
                 conv_reduce_launch(&ra, 1, sp, S * nc * 32, 32, s);
             }

@@ -106,6 +106,28 @@ def test_loss_and_grad_vs_oracle(snk, bs, C):
     assert loss2 == loss and np.array_equal(m.grad, grad)
 
 
+@pytest.mark.parametrize("bs,B", [(12, 37), (13, 64), (8, 5)])
+def test_conv3_backward_odd_batches_vs_oracle(snk, bs, B):
+    """conv3_bwd_kernel (snk_bwd3.hpp): two-sample weight-gradient chunks (an odd
+    batch leaves a one-sample chunk), the data gradient's dense GEMM + col2im,
+    at the smallest and largest boards it takes (Wo 3 and 8) and between."""
+    g, rb = _random_replay(snk, bs, 2, n=48, T=6, seed=bs)
+    m = snk.DQNModel(bs, 3, n_frames=2, seed=bs + 3)
+    rng = np.random.default_rng(B)
+    tp = m.get_params() + rng.standard_normal(m.P).astype(np.float32) * 0.01
+    m.set_params(tp, snk.SNK_NET_TARGET)
+    ids = rng.choice(48 * 6, size=B, replace=False)
+    b = snk.stack_exp(rb, ids)
+    loss = m.loss_grad_batch(b)
+    grad = m.grad
+    lref, gref, _ = oracle.dqn_loss_grad(bs, 2, m.get_params(), tp, b["states"], b["actions"] - 1, b["rewards"],
+                                         b["next_states"], b["dones"].astype(np.uint8),
+                                         b["suicidal_mask"].astype(np.uint8))
+    assert abs(loss - lref) <= 1e-5 * abs(lref)
+    assert np.linalg.norm(grad - gref) <= 1e-5 * np.linalg.norm(gref)
+    assert np.all(np.abs(grad - gref) <= 1e-5 * np.abs(gref).max() + 1e-4 * np.abs(gref))
+
+
 def test_rmsprop_bitexact(snk):
     m = snk.DQNModel(12, 3, n_frames=2, seed=5)
     rng = np.random.default_rng(1)
