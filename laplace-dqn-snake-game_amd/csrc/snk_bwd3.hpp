@@ -253,4 +253,203 @@ __global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
     if (a.dbg && threadIdx.x == 0) a.dbg[b * 8 + 5] = wall_clock64();
 }
 
+// ---------------------------------------------------------------- conv2 (3x3, pad 1, 16 -> 32)
+// One launch: blocks [0, S) the weight gradient of sample b, then C2_NXB
+// data-gradient blocks per sample, on v_mfma_f32_16x16x4_f32 from LDS.
+//  * dW block: a1[s] inside a zero border ([(bs+2)^2][16]) and dz2[s]
+//    ([bs^2][48-float rows]); wave w takes a quarter of the output positions
+//    (4 per MFMA step) for all nine 16 (ci) x 32 (co) offset tiles:
+//    A[ci][t] = a1b[(io + du, jo + dv)][ci], B[t][co] = dz2[t][co]; the four
+//    partials are summed in LDS. Slab z = s (grad_update_kernel sums them);
+//    wave 3 also writes the bias row.
+//  * dX block: dz2[s] inside a zero border ([(bs+2)^2][36]) and the weights
+//    [kk][ci][co] ([144][36]); 16-row position tiles round robin over the waves,
+//    K = 9 offsets x 32 channels: dzc1[pin][ci] = sum dz2b[pin + (1,1) - (du,dv)][co]
+//    * W[kk][ci][co], relu-masked by a1.
+struct Conv2BwdArgs {
+    const float *a1;    // [S][bs*bs][16]
+    const float *dz2;   // [S][bs*bs][32]
+    const float *w;     // conv2 weights [9 kk][16 ci][32 co]
+    float *slab;        // dW partials [S][145][32] (row 144: bias)
+    float *dzc1;        // [S][bs*bs][16]
+    int S, bs;
+};
+constexpr int C2_DS = 48, C2_BS = 36, C2_WS = 36;   // LDS row strides (floats), conflict-free reads
+
+__host__ __device__ inline int c2_bwd_lds_floats(int bs) {
+    const int bp2 = (bs + 2) * (bs + 2);
+    int dw = bp2 * 16 + bs * bs * C2_DS, dx = bp2 * C2_BS + 144 * C2_WS;
+    if (dw < 4 * 4608) dw = 4 * 4608;   // the weight-gradient block's cross-wave sum
+    return dw > dx ? dw : dx;
+}
+
+__device__ __forceinline__ void c2_dw_block(const Conv2BwdArgs &a, int s, float *sm) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int bs = a.bs, bp = bs + 2, bs2 = bs * bs, bp2 = bp * bp;
+    float *A1 = sm, *D2 = sm + bp2 * 16;
+    for (int e = tid; e < bp2 * 4; e += 256) reinterpret_cast<f32x4 *>(A1)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    {
+        constexpr int U = 8;   // loads in flight per thread
+        const f32x4 *src = reinterpret_cast<const f32x4 *>(a.a1 + (int64_t)s * bs2 * 16);
+        for (int b = 0; b < bs2 * 4; b += U * 256) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = b + u * 256 + tid;
+                v[u] = src[e < bs2 * 4 ? e : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = b + u * 256 + tid;
+                if (e < bs2 * 4) {
+                    const int p = e >> 2, j = p / bs, i = p - j * bs;
+                    reinterpret_cast<f32x4 *>(A1 + ((i + 1) + (j + 1) * bp) * 16)[e & 3] = v[u];
+                }
+            }
+        }
+        const f32x4 *srd = reinterpret_cast<const f32x4 *>(a.dz2 + (int64_t)s * bs2 * 32);
+        for (int b = 0; b < bs2 * 8; b += U * 256) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = b + u * 256 + tid;
+                v[u] = srd[e < bs2 * 8 ? e : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = b + u * 256 + tid;
+                if (e < bs2 * 8) reinterpret_cast<f32x4 *>(D2 + (e >> 3) * C2_DS)[e & 7] = v[u];
+            }
+        }
+    }
+    __syncthreads();
+    // wave w: output positions [w*q, w*q + q) (q = bs^2/4 rounded up to 4) for all
+    // nine offsets (18 independent accumulator chains), then a fixed-order LDS sum
+    const int r = lane & 15, g = lane >> 4;
+    const int q = ((bs2 + 15) / 16) * 4, t0 = wave * q, t1 = min(bs2, t0 + q);
+    f32x4m acc[9][2];
+#pragma unroll
+    for (int kk = 0; kk < 9; ++kk) acc[kk][0] = acc[kk][1] = f32x4m{0.f, 0.f, 0.f, 0.f};
+    for (int tb = t0; tb < t1; tb += 4) {
+        const int t = tb + g;
+        const bool v = t < t1;
+        const int tt = v ? t : t0;
+        const int jo = tt / bs, io = tt - jo * bs;
+        const float *pa = A1 + (io + jo * bp) * 16 + r;
+        const float y0 = D2[tt * C2_DS + r], y1 = D2[tt * C2_DS + 16 + r];
+        const float b0 = v ? y0 : 0.0f, b1 = v ? y1 : 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < 9; ++kk) {
+            const float x = pa[((kk % 3) + (kk / 3) * bp) * 16];
+            acc[kk][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x, b0, acc[kk][0], 0, 0, 0);
+            acc[kk][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x, b1, acc[kk][1], 0, 0, 0);
+        }
+    }
+    float bsum = 0.0f;
+    if (wave == 3 && lane < 32) {   // bias row: dz2 column sums, position order
+        int t = 0;
+        for (; t + 8 <= bs2; t += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = D2[(t + u) * C2_DS + lane];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bsum += v[u];
+        }
+        for (; t < bs2; ++t) bsum += D2[t * C2_DS + lane];
+    }
+    float *out = a.slab + (int64_t)s * 145 * 32;
+    __syncthreads();   // staging buffers are free: partial tiles [wave][kk][ct][e][lane]
+    float *red = sm;
+#pragma unroll
+    for (int kk = 0; kk < 9; ++kk)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) red[(((wave * 9 + kk) * 2 + ct) * 4 + e) * 64 + lane] = acc[kk][ct][e];
+    __syncthreads();
+    for (int x = tid; x < 9 * 2 * 4 * 64; x += 256) {
+        const float v = ((red[x] + red[4608 + x]) + red[2 * 4608 + x]) + red[3 * 4608 + x];
+        const int ln = x & 63, e = (x >> 6) & 3, ct = (x >> 8) & 1, kk = x >> 9;
+        out[(kk * 16 + 4 * (ln >> 4) + e) * 32 + ct * 16 + (ln & 15)] = v;
+    }
+    if (wave == 3 && lane < 32) out[144 * 32 + lane] = bsum;
+}
+
+constexpr int C2_NXB = 2;   // data-gradient blocks per sample (interleaved 16-row tiles)
+
+__device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb, float *sm) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int bs = a.bs, bp = bs + 2, bs2 = bs * bs, bp2 = bp * bp;
+    float *Db = sm, *Wl = sm + bp2 * C2_BS;
+    for (int e = tid; e < bp2 * (C2_BS / 4); e += 256) reinterpret_cast<f32x4 *>(Db)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    {
+        constexpr int U = 8;
+        const f32x4 *srd = reinterpret_cast<const f32x4 *>(a.dz2 + (int64_t)s * bs2 * 32);
+        for (int b = 0; b < bs2 * 8; b += U * 256) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = b + u * 256 + tid;
+                v[u] = srd[e < bs2 * 8 ? e : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = b + u * 256 + tid;
+                if (e < bs2 * 8) {
+                    const int p = e >> 3, j = p / bs, i = p - j * bs;
+                    reinterpret_cast<f32x4 *>(Db + ((i + 1) + (j + 1) * bp) * C2_BS)[e & 7] = v[u];
+                }
+            }
+        }
+        const f32x4 *sw = reinterpret_cast<const f32x4 *>(a.w);
+        f32x4 v[5];   // 144 rows x 8 float4 = 1152 = 4.5 per thread
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int e = u * 256 + tid;
+            v[u] = sw[e < 1152 ? e : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int e = u * 256 + tid;
+            if (e < 1152) reinterpret_cast<f32x4 *>(Wl + (e >> 3) * C2_WS)[e & 7] = v[u];
+        }
+    }
+    __syncthreads();
+    const int r = lane & 15, g = lane >> 4;
+    const int nt = (bs2 + 15) / 16;
+    for (int t = xb + C2_NXB * wave; t < nt; t += 4 * C2_NXB) {
+        const int p = min(t * 16 + r, bs2 - 1);
+        const int j = p / bs, i = p - j * bs;
+        f32x4m acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 9; ++kk) {
+            const int dv = kk / 3, du = kk - dv * 3;
+            // dz2 at (i + 1 - du, j + 1 - dv) in the input grid = bordered (i + 2 - du, j + 2 - dv)
+            const float *pa = Db + ((i + 2 - du) + (j + 2 - dv) * bp) * C2_BS + g;
+            const float *pb = Wl + (kk * 16 + r) * C2_WS + g;
+#pragma unroll
+            for (int c = 0; c < 32; c += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[c], pb[c], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int row = t * 16 + 4 * g + e;
+            if (row < bs2) {
+                const int64_t o = ((int64_t)s * bs2 + row) * 16 + r;
+                a.dzc1[o] = a.a1[o] > 0.0f ? acc[e] : 0.0f;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void conv2_bwd_kernel(Conv2BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float c2sm[];
+    const int b = blockIdx.x;
+    if (b < a.S)
+        c2_dw_block(a, b, c2sm);
+    else
+        c2_dx_block(a, (b - a.S) / C2_NXB, (b - a.S) % C2_NXB, c2sm);
+}
+
 }  // namespace snk

@@ -1398,6 +1398,12 @@ static bool c3bwd_ok(const QLayout &L, int64_t S) {
            (size_t)c3_dx_lds_floats(L.Wo) <= lim;
 }
 
+// conv2's backward on conv2_bwd_kernel (snk_bwd3.hpp); SNK_C2BWD=0: the generic pair
+static bool c2bwd_ok(const QLayout &L, int64_t S) {
+    static const bool on = !getenv("SNK_C2BWD") || atoi(getenv("SNK_C2BWD")) != 0;
+    return on && S <= (1 << 20) && (size_t)c2_bwd_lds_floats(L.bs) * sizeof(float) <= 160 * 1024;
+}
+
 static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
     BwdPlan p;
     p.d1 = plan_gemm_kw(L.K1 + 1, 64, 2, S, true, 2);
@@ -1407,6 +1413,7 @@ static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
         p.c3 = GemmPlan{4, (int)z, (int)(C3_NSC * L.Wo * L.Wo)};
     }
     p.c2 = plan_gemm_kw(145, 32, 1, S * L.ncell, true, 8);
+    if (c2bwd_ok(L, S)) p.c2 = GemmPlan{8, (int)S, (int)L.ncell};   // slab z = sample z
     p.c1 = plan_gemm(9 * L.C + 1, 16, 1, S * L.ncell, true);
     p.d1x = plan_gemm_kw(S, L.K1, 2, 64, false, 2);
     p.c2x = plan_gemm_kw(S * L.ncell, 16, 1, 288, false, 8);
@@ -1598,6 +1605,18 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         }
         // conv2: dW | dX (relu mask on a1)
         float *c2d = dst(2, p.c2, L.off_w2, 145 * 32, slab + sr.c2);
+        if (c2bwd_ok(L, S)) {
+            const Conv2BwdArgs ca{w.a1, w.dz2, th + L.off_w2, c2d, w.dzc1, (int)S, bs};
+            const size_t lds = (size_t)c2_bwd_lds_floats(bs) * sizeof(float);
+            static size_t attr = 0;
+            if (lds > attr) {
+                SNK_HIP(hipFuncSetAttribute((const void *)conv2_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)lds));
+                attr = lds;
+            }
+            conv2_bwd_kernel<<<(unsigned)((1 + C2_NXB) * S), 256, lds, s>>>(ca);
+            launch_check("conv2_bwd_kernel");
+        } else
         pair_launch<512>(gemm_job<1, 8>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)},
                                         BRows{w.dz2, S * nc, 32}, EpSlab{c2d, 145, 32}, 145, 32, S * nc, p.c2),
                          gemm_job<1, 8>(AConvDx<32, 3, 1>{w.dz2, bs, bs, FastDiv(nc), FastDiv(bs)},
