@@ -34,13 +34,12 @@ H3_PRODUCTS = 3            # fp16 MFMA products per fp32 product in the h3 conv3
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
 
 
-def _latest_traffic(h3: bool):
+def _latest_traffic(kern: str):
     """HBM bytes per conv3 act-forward launch from the newest committed PMC pass
     (profiles/*_conv3_traffic.json, written by tools/traffic.py from separate
     FETCH_SIZE / WRITE_SIZE rocprofv3 --pmc runs; FETCH_SIZE doubled per
     MI355X_MICROARCH.md's gfx950 note), for the kernel this run uses."""
     import glob
-    kern = "conv_h3s_kernel" if h3 else "conv_x6"
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_conv3_traffic.json")), reverse=True):
         try:
             d = json.load(open(f))
@@ -270,7 +269,7 @@ def main():
                    "n_envs_per_gpu": n, "board_size": bs, "n_frames": C, "replay_capacity": args.capacity,
                    "batch_size": 64, "epsilon": args.epsilon, "parallelism": f"dp{world}" if world > 1 else "none",
                    "hipgraph": graph,
-                   "gemm_arithmetic": ("act-forward conv3: f32 operands as fp16 hi/lo parts of power-of-two-scaled "
+                   "gemm_arithmetic": ("act-forward conv2 + conv3: f32 operands as fp16 hi/lo parts of power-of-two-scaled "
                                        "values, 3 f16 MFMA products; other GEMMs: 3-way bf16 split, 6 bf16 MFMA "
                                        "products; f32 accumulation throughout" if os.environ.get("SNK_CONV", "") != "fp32"
                                        else "native f32 MFMA")},
@@ -286,8 +285,12 @@ def main():
         _lib.call("snk_dqn_time_act_layers", tr.model.handle, tr.game.handle, 20, _lib.ptr(ms))
         wo = bs - 5
         flop_conv3 = 2.0 * n * wo * wo * (36 * 32) * 64
+        flop_conv2 = 2.0 * n * bs * bs * 144 * 32
         flop_total = 2.0 * n * (bs * bs * 16 * 9 * C + bs * bs * 32 * 144 + wo * wo * 64 * 1152 + wo * wo * 64 * 64 + 64 * 3)
-        tf = flop_conv3 / (ms[2] * 1e-3) / 1e12
+        # ms[1] == 0: conv2 runs inside conv3's kernel (conv_h3f_kernel), ms[2] times both
+        fused = ms[1] == 0.0
+        flop_dom = flop_conv3 + (flop_conv2 if fused else 0.0)
+        tf = flop_dom / (ms[2] * 1e-3) / 1e12
         # the forward GEMMs run fp32 products as 6 exact bf16 split products on the
         # bf16 MFMA (SNK_CONV=fp32: native f32 MFMA): the fp32-equivalent peak is
         # the bf16 dense peak / 6
@@ -296,19 +299,23 @@ def main():
         h3 = x6 and os.environ.get("SNK_H3S", "1") != "0" and n >= 1024 and 8 <= bs <= 13
         nprod = H3_PRODUCTS if h3 else X6_PRODUCTS
         peak = PEAK_BF16_TFLOPS / nprod if x6 else PEAK_FP32_TFLOPS
-        kname = ("conv_h3s_kernel: fp16 h3 split on v_mfma_f32_16x16x32_f16" if h3 else
+        kname = ("conv_h3f_kernel: conv2 + conv3 in one kernel, fp16 h3 split on v_mfma_f32_16x16x32_f16"
+                 if h3 and fused else
+                 "conv_h3s_kernel: fp16 h3 split on v_mfma_f32_16x16x32_f16" if h3 else
                  "bf16x6 split on v_mfma_f32_16x16x32_bf16" if x6 else "v_mfma_f32_32x32x2_f32")
         out["roofline"] = {"bound": "mfma",
-                           "kernel": "conv3 implicit GEMM, act forward (" + kname + ")",
+                           "kernel": ("conv2 + conv3 implicit GEMMs" if fused else "conv3 implicit GEMM") +
+                                     ", act forward (" + kname + ")",
                            "achieved": tf, "peak": peak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / peak,
-                           "traffic": None, "avg_launch_ms": ms[2], "flop_per_launch": flop_conv3,
+                           "traffic": None, "avg_launch_ms": ms[2], "flop_per_launch": flop_dom,
                            "half_mfma_tflops_executed": tf * nprod if x6 else None,
                            "fp32_mfma_peak": PEAK_FP32_TFLOPS}
-        tr_file = _latest_traffic(h3)
+        tr_file = _latest_traffic("conv_h3f_kernel" if fused else "conv_h3s_kernel" if h3 else "conv_x6")
         if tr_file:
             out["roofline"]["traffic"] = tr_file["bytes_per_launch"]
             out["roofline"]["traffic_source"] = tr_file["source"]
-        out["act_forward_ms"] = {"conv1": ms[0], "conv2": ms[1], "conv3": ms[2], "dense1": ms[3], "head": ms[4],
+        out["act_forward_ms"] = {"conv1": ms[0], "conv2": ms[1], ("conv2+conv3" if fused else "conv3"): ms[2],
+                                 "dense1": ms[3], "head": ms[4],
                                  "total": float(ms.sum()),
                                  "tflops_total": flop_total / (ms.sum() * 1e-3) / 1e12}
         # the fused env step + store kernel (HBM roofline)

@@ -155,7 +155,8 @@ int snk_dqn_forward_env(snk_dqn m, int32_t which, snk_env env, float *q_dev);
 int snk_dqn_act(snk_dqn m, snk_env env, float epsilon, uint64_t seed, uint8_t *act_dev);
 /* measurement: average ms per launch of each stage of the epsilon_greedy
  * forward over env's batch, ms_out[5] = conv1, conv2, conv3, dense1, head
- * (HIP events on the library stream) */
+ * (HIP events on the library stream); when the forward fuses conv2 into
+ * conv3 (conv_h3f_kernel) ms_out[1] = 0 and ms_out[2] is the fused kernel */
 int snk_dqn_time_act_layers(snk_dqn m, snk_env env, int32_t reps, double *ms_out);
 /* measurement: average ms of the fused step(+store) kernel over reps real steps */
 int snk_env_time_step(snk_env env, snk_replay rb_or_null, const uint8_t *act_dev, int32_t reps, double *ms_out);

@@ -1,0 +1,404 @@
+// snk_conv_h3f.hpp — conv2 + conv3 of the large-batch act forward in ONE kernel
+// on the h3 split (snk_conv_h3.hpp).
+//
+// conv_h3s_kernel stages four samples' fp32 conv2 outputs (a2, 18 KB each at
+// 12x12) from HBM, takes a per-sample max and splits them into its LDS A image.
+// Here the same workgroup computes those four samples' conv2 itself: it stages
+// their fp32 conv1 outputs (a1, half the bytes of a2) with a per-sample scale
+// into a zero-bordered fp16 h/l image, splits the conv2 weights (9 x 32 x 16,
+// per-tensor scale) into paired-offset fragments, runs conv2's 16-row tiles on
+// v_mfma_f32_16x16x32_f16 (3 part products), applies bias + relu, reduces the
+// per-sample max of the result in the workgroup and writes the split conv2
+// output straight into conv3's A image (which overlays the conv2 staging
+// area). conv3 then runs conv_h3s_kernel's pipeline unchanged. a2 never goes
+// to memory: per sample this saves the a2 write and re-read (2 x 18 KB) and
+// the conv2 launch; the arithmetic and the error class of each conv are those
+// of conv_h3c2_kernel + conv_h3s_kernel.
+#pragma once
+
+#include "snk_conv_h3.hpp"
+
+namespace snk {
+
+struct H3FArgs {
+    const float *a1;     // conv1 output [S][HIN^2][16] (fp32, relu'd)
+    const float *w2;     // conv2 forward image [9 kk][32 co][16 ci]
+    const float *b2;     // conv2 bias [32]
+    const float *w3;     // conv3 forward image [36 kk][64 co][32 ci]
+    const float *wmax;   // partial max |w3| (conv1_fwd_kernel / wmax_scan_kernel)
+    int nwmax;
+    const float *b3;     // conv3 bias [64]
+    float *out;          // a3 [S][ho^2][64]
+    uint64_t *dbg;       // SNK_H3F_DBG: per-wave phase clocks
+};
+
+template <int HIN>
+constexpr int h3f_lds_bytes() {
+    constexpr int ho = HIN - 5, XW = ho + 8, PL = (HIN * XW + 3) & ~3, XS = 4 * 2 * PL + 4;
+    constexpr int BP = HIN + 2;
+    constexpr int c2 = (4 * 2 * BP * BP * 24 + 5 * 2 * 32 * 40) * 2;   // conv2 staging (halves)
+    constexpr int c3 = 4 * XS * 16;                                     // conv3 A image
+    constexpr int cs = 4 * ho * ho * 80 * 4;                            // output staging
+    constexpr int m = c2 > c3 ? (c2 > cs ? c2 : cs) : (c3 > cs ? c3 : cs);
+    return 2 * 512 * 16 + m;
+}
+
+template <int HIN>
+__global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
+    constexpr int KS = 6, CN = 64, CK = 32, NSG = 4, NB = 2 * CN * CK / 8;
+    constexpr int NKK = KS * KS;
+    constexpr int hin = HIN, ho = HIN - KS + 1, ho2 = ho * ho, hin2 = hin * hin;
+    constexpr int XW = ho + 8, PL = (hin * XW + 3) & ~3, GG = 2 * PL, XS = 4 * GG + 4;
+    constexpr int BP = HIN + 2, NPB = BP * BP, XR = 24, BR = 40;
+    constexpr int A1_H = NSG * 2 * NPB * XR, B2_H = 5 * 2 * 32 * BR;
+    constexpr int R2 = NSG * hin2, T2 = (R2 + 15) / 16, U2 = (T2 + 7) / 8;
+    constexpr int NW4 = 9 * 32 * 16 / 4, LW = (NW4 + 511) / 512, LA = (NSG * hin2 * 4 + 511) / 512;
+    static_assert(XR % 8 == 0 && BR % 8 == 0, "16-byte pieces");
+    extern __shared__ __attribute__((aligned(16))) u32x4 h3f_lds[];
+    __shared__ float red[8][7];
+    u32x4 *Bs = h3f_lds;            // conv3 B [2][NB]
+    u32x4 *As = h3f_lds + 2 * NB;   // conv3 A image; during conv2: A1 image, B2 image
+    u32x2 *Bs2 = reinterpret_cast<u32x2 *>(Bs);
+    uint16_t *A1 = reinterpret_cast<uint16_t *>(As), *B2 = A1 + A1_H;
+    u32x2 *A1v = reinterpret_cast<u32x2 *>(A1), *B2v = reinterpret_cast<u32x2 *>(B2);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int s0 = blockIdx.x * NSG;
+    const int ns = min(NSG, S - s0);
+    uint64_t ts[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0;
+    if (a.dbg) { ts[0] = clock64(); rt0 = wall_clock64(); }
+
+    // conv3 B register sets (as conv_h3s_kernel)
+    const f32x4 *__restrict__ wsrc = reinterpret_cast<const f32x4 *>(a.w3);
+    f32x4 bst[2];
+    auto b_load = [&](int kk, int set) { bst[set] = wsrc[(int64_t)min(kk, NKK - 1) * NB + tid]; };
+    const int bch = (tid >> 3) * 4 + ((tid & 7) >> 1);
+    const int bhalf = tid & 1;
+    int ew = 0;
+    auto b_store = [&](int buf, int set) {
+        u32x2 h, l;
+        h3_split4(bst[set], ew, h, l);
+        Bs2[(buf * NB + x6s_bswz(bch)) * 2 + bhalf] = h;
+        Bs2[(buf * NB + x6s_bswz(256 + bch)) * 2 + bhalf] = l;
+    };
+    b_load(0, 0);
+    b_load(1, 1);
+
+    // conv2 bias of this lane's output channels (16 ct + 4 g + e), early
+    float b2v[2][4];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b2v[ct][e] = a.b2[ct * 16 + 4 * g + e];
+
+    // ---- conv2 staging: zero the A1 image's border positions and B2's pad offset
+    // (kk = 9: k 16..31 of pair 4); the rest is overwritten below
+    {
+        constexpr int NBD = 4 * (BP - 1);   // border positions per plane
+        for (int q = tid; q < NSG * 2 * NBD * 3; q += 512) {
+            const int pc = q / (NBD * 3), rem = q - pc * NBD * 3, bpos = rem / 3, piece = rem - bpos * 3;
+            const int side = bpos / (BP - 1), t = bpos - side * (BP - 1);
+            const int pb = side == 0 ? t : side == 1 ? (BP - 1) + t * BP : side == 2 ? (BP * BP - 1) - t
+                                                                                     : (BP - 1 - t) * BP;
+            reinterpret_cast<u32x4 *>(A1)[((pc * NPB + pb) * XR) / 8 + piece] = u32x4{0u, 0u, 0u, 0u};
+        }
+        if (tid < 2 * 32 * 2) {   // plane, co, two 16-byte pieces (k 16..31)
+            const int pl = tid >> 6, co = (tid >> 1) & 31, piece = tid & 1;
+            reinterpret_cast<u32x4 *>(B2)[(((4 * 2 + pl) * 32 + co) * BR + 16) / 8 + piece] = u32x4{0u, 0u, 0u, 0u};
+        }
+    }
+    f32x4 wv[LW], av[LA];
+    const f32x4 *w4 = reinterpret_cast<const f32x4 *>(a.w2);
+    const f32x4 *x4 = reinterpret_cast<const f32x4 *>(a.a1) + (int64_t)s0 * hin2 * 4;
+    const int na4 = ns * hin2 * 4;
+#pragma unroll
+    for (int u = 0; u < LW; ++u) wv[u] = w4[min(u * 512 + tid, NW4 - 1)];
+#pragma unroll
+    for (int u = 0; u < LA; ++u) av[u] = x4[min(u * 512 + tid, na4 - 1)];
+    float wm3 = 0.0f;
+    for (int i = tid; i < a.nwmax; i += 512) wm3 = fmaxf(wm3, a.wmax[i]);
+    float mw2 = 0.0f, ms[NSG] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < LW; ++u) {
+        const f32x4 v = wv[u];
+        if (u * 512 + tid < NW4)
+            mw2 = fmaxf(mw2, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+        const int e = u * 512 + tid;
+        const int sr = e < na4 ? e / (hin2 * 4) : NSG;
+        const f32x4 v = av[u];
+        const float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+#pragma unroll
+        for (int q = 0; q < NSG; ++q) ms[q] = sr == q ? fmaxf(ms[q], m) : ms[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NSG; ++q) ms[q] = wave_max(ms[q]);
+    mw2 = wave_max(mw2);
+    wm3 = wave_max(wm3);
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < NSG; ++q) red[wave][q] = ms[q];
+        red[wave][4] = mw2;
+        red[wave][5] = wm3;
+    }
+    __syncthreads();   // also: the border fill is complete
+    int ea1[NSG], ew2;
+    {
+        float m[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            m[q] = red[0][q];
+#pragma unroll
+            for (int w8 = 1; w8 < 8; ++w8) m[q] = fmaxf(m[q], red[w8][q]);
+        }
+#pragma unroll
+        for (int q = 0; q < NSG; ++q) ea1[q] = h3_exp(m[q]);
+        ew2 = h3_exp(m[4]);
+        ew = h3_exp(m[5]);
+    }
+#pragma unroll
+    for (int u = 0; u < LW; ++u) {   // image [kk][co][ci]: k = 16 * (kk - 2p) + ci in offset pair p
+        const int e = u * 512 + tid;
+        if (e < NW4) {
+            const int kk = e >> 7, co = (e >> 2) & 31, ci0 = 4 * (e & 3);
+            const int p = kk >> 1, k0 = 16 * (kk & 1) + ci0;
+            u32x2 hh, ll;
+            h3_split4(wv[u], ew2, hh, ll);
+            B2v[(((p * 2 + 0) * 32 + co) * BR + k0) / 4] = hh;
+            B2v[(((p * 2 + 1) * 32 + co) * BR + k0) / 4] = ll;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {   // a1 [s][pos][16] -> bordered [s][part][pos][24 halves]
+        const int e = u * 512 + tid;
+        if (e < na4) {
+            const int sr = e / (hin2 * 4), loc = e - sr * hin2 * 4;
+            const int pos = loc >> 2, c0 = 4 * (loc & 3);
+            const int j = pos / hin, i = pos - j * hin;
+            const int pb = (i + 1) + (j + 1) * BP;
+            const int es = sr == 0 ? ea1[0] : sr == 1 ? ea1[1] : sr == 2 ? ea1[2] : ea1[3];
+            u32x2 hh, ll;
+            h3_split4(av[u], es, hh, ll);
+            A1v[(((sr * 2 + 0) * NPB + pb) * XR + c0) / 4] = hh;
+            A1v[(((sr * 2 + 1) * NPB + pb) * XR + c0) / 4] = ll;
+        }
+    }
+    __syncthreads();
+    if (a.dbg) ts[1] = clock64();
+
+    // ---- conv2, transposed: C^T[co][row] = sum_k W[co][k] * A[row][k] with the weight
+    // fragments as the MFMA's A operand and the activation fragments as its B (the
+    // same register layouts): a lane then holds 4 consecutive channels of one row,
+    // written to conv3's image as one 8-byte piece per part. 16-row tiles
+    // t = wave + 8u; offset pair p outermost so each weight fragment is read once
+    f32x4v acc2[U2][2];
+    int rsl[U2], rpos[U2];   // this lane's row (column r of tile u): sample, A-image position
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+        acc2[u][0] = acc2[u][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        const int q = min((wave + 8 * u) * 16 + r, R2 - 1);
+        rsl[u] = q / hin2;
+        const int pos = q - rsl[u] * hin2, j = pos / hin, i = pos - j * hin;
+        rpos[u] = i + j * BP;
+    }
+#pragma unroll
+    for (int p = 0; p < 5; ++p) {
+        f16x8 wh[2], wl[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            const uint16_t *pb = B2 + ((p * 2) * 32 + ct * 16 + r) * BR + 8 * g;
+            wh[ct] = as_h(*reinterpret_cast<const u32x4 *>(pb));
+            wl[ct] = as_h(*reinterpret_cast<const u32x4 *>(pb + 32 * BR));
+        }
+        const int kk = min(2 * p + (g >> 1), 8), du = kk % 3, dv = kk / 3;
+#pragma unroll
+        for (int u = 0; u < U2; ++u) {
+            if (wave + 8 * u < T2) {
+                const uint16_t *pa = A1 + ((rsl[u] * 2) * NPB + rpos[u] + du + dv * BP) * XR + 8 * (g & 1);
+                const f16x8 ah = as_h(*reinterpret_cast<const u32x4 *>(pa));
+                const f16x8 al = as_h(*reinterpret_cast<const u32x4 *>(pa + NPB * XR));
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    f32x4v c = acc2[u][ct];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ct], al, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[ct], ah, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ct], ah, c, 0, 0, 0);
+                    acc2[u][ct] = c;
+                }
+            }
+        }
+    }
+    // acc2[u][ct][e]: channel co = 16 ct + 4 g + e of row (wave + 8u) * 16 + r.
+    // bias + relu in place; per-sample max (rows of absent samples excluded)
+    float m2[NSG] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+        const int row = (wave + 8 * u) * 16 + r;
+        const int sr = rsl[u];
+        const bool live = wave + 8 * u < T2 && row < R2 && sr < ns;
+        const int es = (sr == 0 ? ea1[0] : sr == 1 ? ea1[1] : sr == 2 ? ea1[2] : ea1[3]) + ew2;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = __builtin_ldexpf(acc2[u][ct][e], -es) + b2v[ct][e];
+                v = (live && v > 0.0f) ? v : 0.0f;
+                acc2[u][ct][e] = v;
+#pragma unroll
+                for (int q = 0; q < NSG; ++q) m2[q] = sr == q ? fmaxf(m2[q], v) : m2[q];
+            }
+    }
+#pragma unroll
+    for (int q = 0; q < NSG; ++q) m2[q] = wave_max(m2[q]);
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < NSG; ++q) red[wave][q] = m2[q];
+    }
+    __syncthreads();   // also: every conv2 fragment read is done (the A image overlays them)
+    if (a.dbg) ts[2] = clock64();
+    int ea[NSG];
+#pragma unroll
+    for (int q = 0; q < NSG; ++q) {
+        float m = red[0][q];
+#pragma unroll
+        for (int w8 = 1; w8 < 8; ++w8) m = fmaxf(m, red[w8][q]);
+        ea[q] = h3_exp(m);
+    }
+    // conv2 output -> conv3's A image: slot(sample, channel group co >> 3, j, i); the lane's
+    // four channels 4g..4g+3 (+16 ct) are halves 4 (g & 1) .. + 3 of one slot: 8-byte pieces
+    u32x2 *Ah2 = reinterpret_cast<u32x2 *>(As);
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+        const int row = (wave + 8 * u) * 16 + r;
+        if (wave + 8 * u < T2 && row < R2) {
+            const int sr = rsl[u], pos = row - sr * hin2;
+            const int j = pos / hin, i = pos - j * hin;
+            const int es = sr == 0 ? ea[0] : sr == 1 ? ea[1] : sr == 2 ? ea[2] : ea[3];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int slot = sr * XS + (ct * 2 + (g >> 1)) * GG + j * XW + i;
+                u32x2 hh, ll;
+                h3_split4(f32x4{acc2[u][ct][0], acc2[u][ct][1], acc2[u][ct][2], acc2[u][ct][3]}, es, hh, ll);
+                Ah2[slot * 2 + (g & 1)] = hh;
+                Ah2[(slot + PL) * 2 + (g & 1)] = ll;
+            }
+        }
+    }
+    b_store(0, 0);
+    b_store(1, 1);
+
+    constexpr int T = (NSG * ho2 + 15) / 16;
+    const int rg = wave >> 1, cg = wave & 1;
+    const int nt = __builtin_amdgcn_readfirstlane(T > rg ? (T - rg + 3) / 4 : 0);
+    const int bslot = (cg * 32 + r) * 4 + (g ^ ((4 - ((r >> 2) & 3)) & 3));
+    __syncthreads();
+    if (a.dbg) ts[3] = clock64();
+
+    // ---- conv3: conv_h3s_kernel's pipeline
+    auto run = [&](auto ntc) {
+        constexpr int NT = decltype(ntc)::value;
+        int abase[NT];
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+            const int q = 16 * (rg + 4 * k) + r;
+            const int p = min(q >> 2, ho2 - 1), sr = q & 3;
+            const int j = p / ho, i = p - j * ho;
+            abase[k] = sr * XS + g * GG + j * XW + i;
+        }
+        f32x4v acc[NT][2];
+#pragma unroll
+        for (int k = 0; k < NT; ++k)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) acc[k][ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        struct Frag {
+            u32x4 a[NT][2], b[2][2];
+        };
+        auto frag_read = [&](int kk, Frag &f) {
+            kk = min(kk, NKK - 1);
+            const int dv = kk / KS, du = kk - dv * KS;
+            const int off = dv * XW + du;
+            const u32x4 *pb = Bs + (kk & 1) * NB + bslot;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl) f.b[ct][pl] = pb[ct * 64 + pl * 256];
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+                const u32x4 *pa = As + abase[k] + off;
+#pragma unroll
+                for (int pl = 0; pl < 2; ++pl) f.a[k][pl] = pa[pl * PL];
+            }
+        };
+        auto mfma_block = [&](const Frag &f) {
+#pragma unroll
+            for (int k = 0; k < NT; ++k) {
+                const f16x8 ah = as_h(f.a[k][0]), al = as_h(f.a[k][1]);
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    const f16x8 bh = as_h(f.b[ct][0]), bl = as_h(f.b[ct][1]);
+                    f32x4v c = acc[k][ct];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+                    acc[k][ct] = c;
+                }
+            }
+        };
+        auto step = [&](int kk, const Frag &cur, Frag &nxt, int set) {
+            b_load(kk + 3, set ^ 1);
+            frag_read(kk + 1, nxt);
+            mfma_block(cur);
+            b_store(kk & 1, set);
+            __syncthreads();
+        };
+        Frag f0, f1;
+        frag_read(0, f0);
+        b_load(2, 0);
+        __syncthreads();
+        static_assert(NKK % 2 == 0, "offsets come in pairs");
+        for (int kk = 0; kk < NKK; kk += 2) {
+            step(kk, f0, f1, 0);
+            step(kk + 1, f1, f0, 1);
+        }
+        if (a.dbg) ts[4] = clock64();
+        // output through LDS as conv_h3s_kernel
+        constexpr int CS = 80;
+        static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN>() - 2 * NB * 16, "output staging fits");
+        float *Cs = reinterpret_cast<float *>(As);
+#pragma unroll
+        for (int k = 0; k < NT; ++k) {
+            const int p = 4 * (rg + 4 * k) + g;
+            if (p >= ho2) continue;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int col = cg * 32 + ct * 16 + r;
+                const float bv = a.b3[col];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = __builtin_ldexpf(acc[k][ct][e], -(ea[e] + ew)) + bv;
+                    Cs[(e * ho2 + p) * CS + col] = v > 0.0f ? v : 0.0f;
+                }
+            }
+        }
+        __syncthreads();
+        const int n4o = ns * ho2 * 16;
+        f32x4 *o4 = reinterpret_cast<f32x4 *>(a.out + (int64_t)s0 * ho2 * CN);
+        const f32x4 *c4 = reinterpret_cast<const f32x4 *>(Cs);
+        for (int q = tid; q < n4o; q += 512) o4[q] = c4[(q >> 4) * (CS / 4) + (q & 15)];
+    };
+    if (nt == 4) run(std::integral_constant<int, 4>{});
+    else if (nt == 3) run(std::integral_constant<int, 3>{});
+    else if (nt == 2) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 1>{});
+    if (a.dbg && lane == 0) {
+        ts[5] = clock64();
+        uint64_t *d = a.dbg + ((int64_t)blockIdx.x * 8 + wave) * 8;
+        for (int q = 0; q < 6; ++q) d[q] = ts[q];
+        d[6] = rt0;
+        d[7] = wall_clock64();
+    }
+}
+
+}  // namespace snk

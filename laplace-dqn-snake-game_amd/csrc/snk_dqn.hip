@@ -360,10 +360,17 @@ extern "C" int snk_dqn_time_act_layers(snk_dqn h, snk_env env, int32_t reps, dou
         hipEvent_t a, b;
         SNK_HIP(hipEventCreate(&a));
         SNK_HIP(hipEventCreate(&b));
+        // conv2 + conv3 fused (conv_h3f_kernel): ms_out[1] = 0, ms_out[2] = the fused kernel
+        const bool f23 = qnet_fused23(h->L, h->theta_q, h->wt_q, h->wtb_q, E.n, h->act);
         for (int layer = 0; layer < 5; ++layer) {
+            if (f23 && layer == 1) {
+                ms_out[1] = 0.0;
+                continue;
+            }
+            const int only = f23 && layer == 2 ? QNET_ONLY_CONV23 : layer;
             SNK_HIP(hipEventRecord(a, s));
             for (int r = 0; r < reps; ++r)
-                qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, layer, h->wtb_q);
+                qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, only, h->wtb_q);
             SNK_HIP(hipEventRecord(b, s));
             SNK_HIP(hipEventSynchronize(b));
             float ms = 0.0f;

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "snk_conv_h3.hpp"
+#include "snk_conv_h3f.hpp"
 #include "snk_bwd3.hpp"
 #include "snk_conv_x6.hpp"
 #include "snk_qnet.hpp"
@@ -1210,6 +1211,61 @@ static void h3c2_launch_bs(const float *a1, const float *wimg, const float *b2, 
     launch_check("conv_h3c2_kernel");
 }
 
+template <int HIN>
+static void h3f_launch_bs(const H3FArgs &fa, int64_t S, hipStream_t s) {
+    constexpr size_t lds = (size_t)h3f_lds_bytes<HIN>();
+    static_assert(lds <= 160 * 1024, "conv_h3f LDS");
+    static bool attr = false;
+    if (!attr) {
+        SNK_HIP(hipFuncSetAttribute((const void *)conv_h3f_kernel<HIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+        attr = true;
+    }
+    const unsigned grid = (unsigned)ceil_div(S, 4);
+    static const bool dbg = getenv("SNK_H3F_DBG") != nullptr;
+    if (dbg) {   // experiment: per-wave phase clocks to stderr
+        const size_t nd = (size_t)grid * 64;
+        uint64_t *d = dalloc<uint64_t>(nd);
+        H3FArgs f2 = fa;
+        f2.dbg = d;
+        conv_h3f_kernel<HIN><<<grid, 512, lds, s>>>(f2, (int)S);
+        launch_check("conv_h3f_kernel");
+        std::vector<uint64_t> hbuf(nd);
+        SNK_HIP(hipMemcpyAsync(hbuf.data(), d, nd * 8, hipMemcpyDeviceToHost, s));
+        SNK_HIP(hipStreamSynchronize(s));
+        dfree(d);
+        double ph[5] = {0, 0, 0, 0, 0};
+        uint64_t rmin = ~0ull, rmax = 0;
+        for (size_t b = 0; b < grid; ++b)
+            for (int w = 0; w < 8; ++w) {
+                const uint64_t *q = &hbuf[(b * 8 + w) * 8];
+                for (int k = 0; k < 5; ++k) ph[k] += (double)(q[k + 1] - q[k]);
+                rmin = std::min(rmin, q[6]);
+                rmax = std::max(rmax, q[7]);
+            }
+        const double n = grid * 8.0;
+        fprintf(stderr, "h3f dbg: %u WGs, per-wave cycles: stage %.0f | conv2 %.0f | A image %.0f | conv3 %.0f | "
+                "epilogue %.0f; wall %.1f us\n", grid, ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, ph[4] / n,
+                (double)(rmax - rmin) / 100.0);
+        return;
+    }
+    conv_h3f_kernel<HIN><<<grid, 512, lds, s>>>(fa, (int)S);
+    launch_check("conv_h3f_kernel");
+}
+
+static void conv_h3f_launch(int bs, const H3FArgs &fa, int64_t S, hipStream_t s) {
+    SNK_CHECK(S <= INT32_MAX, SNK_ERR_INTERNAL, "h3f batch");
+    switch (bs) {
+        case 8: h3f_launch_bs<8>(fa, S, s); return;
+        case 9: h3f_launch_bs<9>(fa, S, s); return;
+        case 10: h3f_launch_bs<10>(fa, S, s); return;
+        case 11: h3f_launch_bs<11>(fa, S, s); return;
+        case 12: h3f_launch_bs<12>(fa, S, s); return;
+        case 13: h3f_launch_bs<13>(fa, S, s); return;
+        default: SNK_CHECK(false, SNK_ERR_INTERNAL, "h3f: board side outside 8..13");
+    }
+}
+
 static void conv_h3c2_launch(const QLayout &L, const FwdNet &n, int64_t S, hipStream_t s) {
     const float *a1 = n.w->a1, *wimg = n.wt + L.off_t2, *b2 = n.th + L.off_b2;
     float *a2 = n.w->a2;
@@ -1225,12 +1281,26 @@ static void conv_h3c2_launch(const QLayout &L, const FwdNet &n, int64_t S, hipSt
     }
 }
 
+static bool h3c2_on() {
+    static const bool on = !getenv("SNK_H3C2") || atoi(getenv("SNK_H3C2")) != 0;
+    return on;
+}
+static bool h3f_on() {
+    static const bool on = !getenv("SNK_H3F") || atoi(getenv("SNK_H3F")) != 0;
+    return on;
+}
+
+// whether an act forward (no training work) of S samples runs conv2 + conv3 as conv_h3f_kernel
+bool qnet_fused23(const QLayout &L, const float *th, const float *wt, const uint16_t *wtb, int64_t S, QWork &w) {
+    const FwdNet net{th, wt, wtb, BoardSrc{}, &w};
+    return h3s_ok(L, &net, 1, S) && h3c2_on() && h3f_on() && !w.has_train;
+}
+
 static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi) {
     const int bs = L.bs, nc = L.ncell;
     const bool h3 = h3s_ok(L, net, ng, S);
     // h3 also for conv2 (conv_h3c2_kernel): conv1 then writes fp32 a1 only. SNK_H3C2=0: x6 conv2.
-    static const bool c2on = !getenv("SNK_H3C2") || atoi(getenv("SNK_H3C2")) != 0;
-    const bool h3c2 = h3 && c2on;
+    const bool h3c2 = h3 && h3c2_on();
     const int64_t n3 = 36LL * 32 * 64;   // conv3 weight image floats
     // x6: conv1 + conv2 fused into one kernel (layer 0; layer 1 is then empty)
     // measured slower than conv1 + conv2 (per-workgroup staging dominates): opt-in
@@ -1291,6 +1361,25 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         }
     }
     FwdIO io[2];
+    // conv2 + conv3 fused (conv_h3f_kernel) when this call runs both. SNK_H3F=0: separate kernels
+    bool h3f = h3c2 && h3f_on() && lo <= 1 && hi >= 2;
+    for (int g = 0; g < ng; ++g) h3f = h3f && !net[g].w->has_train;   // a backward needs a2 in memory
+    if (h3f) {
+        for (int g = 0; g < ng; ++g) {
+            const FwdNet &n = net[g];
+            QWork &w = *n.w;
+            if (!w.wmax_n || w.wmax_img != n.wt + L.off_t3) {   // conv1 did not scan this image
+                wmax_scan_kernel<<<256, 256, 0, s>>>(n.wt + L.off_t3, n3, w.wmax_part);
+                launch_check("wmax_scan_kernel");
+                w.wmax_n = 256;
+                w.wmax_img = n.wt + L.off_t3;
+            }
+            const H3FArgs fa{w.a1, n.wt + L.off_t2, n.th + L.off_b2, n.wt + L.off_t3, w.wmax_part, w.wmax_n,
+                             n.th + L.off_b3, w.a3, nullptr};
+            conv_h3f_launch(L.bs, fa, S, s);
+        }
+        lo = std::max(lo, 3);
+    }
     if (lo <= 1 && hi >= 1 && h3c2) {   // conv2 on the h3 kernel: fp32 a1 -> fp32 a2
         for (int g = 0; g < ng; ++g) conv_h3c2_launch(L, net[g], S, s);
     } else if (lo <= 1 && hi >= 1) {   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
@@ -1346,6 +1435,8 @@ void qnet_forward(const QLayout &L, const float *th, const float *wt, const Boar
     const FwdNet net{th, wt, wtb, src, &w};
     if (only < 0)
         forward_layers(L, &net, 1, S, s, 0, 3);
+    else if (only == QNET_ONLY_CONV23)
+        forward_layers(L, &net, 1, S, s, 1, 2);
     else if (only < 4)
         forward_layers(L, &net, 1, S, s, only, only);
     if (only >= 0 && only != 4) return;

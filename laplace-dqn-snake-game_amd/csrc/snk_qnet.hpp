@@ -124,6 +124,10 @@ void qnet_head_pair(const QLayout &L, const float *theta_t, QWork &wt, const flo
 // the head (Dense1 bias + relu, Dense2, mode epilogue) after the layers
 void qnet_head(const QLayout &L, const float *theta, int64_t S, QWork &w, HeadMode mode, const HeadArgs &ha,
                hipStream_t s);
+// only: -1 all layers + head; 0..3 one layer; 4 the head; QNET_ONLY_CONV23 conv2 and conv3
+constexpr int QNET_ONLY_CONV23 = 12;
+// whether an act forward of S samples runs conv2 + conv3 fused (conv_h3f_kernel)
+bool qnet_fused23(const QLayout &L, const float *theta, const float *wt, const uint16_t *wtb, int64_t S, QWork &w);
 // wtb (optional): bf16 split planes of the image -> conv2/conv3/Dense1 on the x6 kernels
 void qnet_forward(const QLayout &L, const float *theta, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
                   HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1, const uint16_t *wtb = nullptr);
