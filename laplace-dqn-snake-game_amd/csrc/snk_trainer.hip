@@ -123,8 +123,12 @@ struct snk_trainer_s {
     double *loss_log = nullptr;
     int64_t log_cap = 0;
     int32_t B = 64;
-    hipGraph_t graph[2] = {nullptr, nullptr};
-    hipGraphExec_t exec[2] = {nullptr, nullptr};
+    // [2 * learn + unrolled]: one iteration, or `unroll` iterations back to back in one
+    // graph (iterations only communicate through device counters, so a longer graph is
+    // the same launch sequence with the per-graph launch gap paid once per `unroll`)
+    hipGraph_t graph[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipGraphExec_t exec[4] = {nullptr, nullptr, nullptr, nullptr};
+    int unroll = 8;
     hipStream_t graph_stream = nullptr;
     Fork fork;   // side streams: parallel branches of the iteration
 };
@@ -220,6 +224,7 @@ extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, sn
         // this stack (each cross-stream edge cost ~30 us): off unless asked for
         h->fork.enable = 0;
         if (const char *e = getenv("SNK_FORK")) h->fork.enable = (unsigned)strtoul(e, nullptr, 0);
+        if (const char *e = getenv("SNK_GRAPH_UNROLL")) h->unroll = atoi(e) > 0 ? atoi(e) : 1;
         TrainStats st{};
         st.epsilon = cfg->epsilon;
         st.reward_max = -INFINITY;
@@ -246,7 +251,7 @@ extern "C" int snk_trainer_destroy(snk_trainer h) {
     return guard([&] {
         if (!h) return;
         (void)hipStreamSynchronize(stream());
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 4; ++i) {
             if (h->exec[i]) (void)hipGraphExecDestroy(h->exec[i]);
             if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
         }
@@ -267,24 +272,31 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
                       (long long)len, h->B);
         }
         const int g = learn ? 1 : 0;
-        if (use_graph && !h->exec[g]) {
+        auto capture = [&](int slot, int n) {
+            if (h->exec[slot]) return;
             SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             try {
-                trainer_iteration(h, learn != 0, s);
+                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, s);
             } catch (...) {
                 hipGraph_t dummy;
                 (void)hipStreamEndCapture(s, &dummy);
                 throw;
             }
-            SNK_HIP(hipStreamEndCapture(s, &h->graph[g]));
-            SNK_HIP(hipGraphInstantiate(&h->exec[g], h->graph[g], nullptr, nullptr, 0));
+            SNK_HIP(hipStreamEndCapture(s, &h->graph[slot]));
+            SNK_HIP(hipGraphInstantiate(&h->exec[slot], h->graph[slot], nullptr, nullptr, 0));
+        };
+        if (!use_graph) {
+            for (int64_t i = 0; i < iters; ++i) trainer_iteration(h, learn != 0, s);
+            return;
         }
-        for (int64_t i = 0; i < iters; ++i) {
-            if (use_graph)
-                SNK_HIP(hipGraphLaunch(h->exec[g], s));
-            else
-                trainer_iteration(h, learn != 0, s);
+        const int U = h->unroll;
+        int64_t i = 0;
+        if (U > 1 && iters >= U) {
+            capture(2 * g + 1, U);
+            for (; i + U <= iters; i += U) SNK_HIP(hipGraphLaunch(h->exec[2 * g + 1], s));
         }
+        if (i < iters) capture(2 * g, 1);
+        for (; i < iters; ++i) SNK_HIP(hipGraphLaunch(h->exec[2 * g], s));
     });
 }
 
@@ -302,7 +314,7 @@ extern "C" int snk_trainer_set_comm(snk_trainer h, snk_comm comm) {
         }
         SNK_HIP(hipStreamSynchronize(s));
         h->comm = comm;   // NULL: detach (updates local again)
-        for (int i = 0; i < 2; ++i) {   // captured graphs predate the collective
+        for (int i = 0; i < 4; ++i) {   // captured graphs predate the collective
             if (h->exec[i]) (void)hipGraphExecDestroy(h->exec[i]);
             if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
             h->exec[i] = nullptr;

@@ -12,4 +12,5 @@ python -c "import json;d=json.load(open('$OUT/bench.json'));print(d['value'], d[
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || exit 4
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc/p2 -o run -- python tools/act_fwd.py > $OUT/p2.log 2>&1 || exit 5
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE TCC_HIT TCC_MISS --output-format csv -d $OUT/pmc/p3 -o run -- python tools/act_fwd.py > $OUT/p3.log 2>&1 || exit 6
+SNK_GRAPH_UNROLL=1 timeout -k 10 300 python bench.py --no-dbuild --no-cpu-baseline --no-extras > $OUT/bench_u1.json 2>> $OUT/bench.err || exit 7
 echo done
