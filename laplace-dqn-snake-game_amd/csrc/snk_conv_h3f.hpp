@@ -32,7 +32,7 @@ struct H3FArgs {
     uint64_t *dbg;       // SNK_H3F_DBG: per-wave phase clocks
 };
 
-template <int HIN>
+template <int HIN, int NBUF = 4>
 constexpr int h3f_lds_bytes() {
     constexpr int ho = HIN - 5, XW = ho + 8, PL = (HIN * XW + 3) & ~3, XS = 4 * 2 * PL + 4;
     constexpr int BP = HIN + 2;
@@ -40,11 +40,14 @@ constexpr int h3f_lds_bytes() {
     constexpr int c3 = 4 * XS * 16;                                     // conv3 A image
     constexpr int cs = 4 * ho * ho * 80 * 4;                            // output staging
     constexpr int m = c2 > c3 ? (c2 > cs ? c2 : cs) : (c3 > cs ? c3 : cs);
-    return 2 * 512 * 16 + m;
+    return NBUF * 512 * 16 + m;
 }
 
-template <int HIN>
+// NBUF conv3 B buffers: 2 = one barrier per kernel offset (B(kk+2) staged while kk
+// runs); 4 = one barrier per offset PAIR (B(kk+3) staged, read two offsets later)
+template <int HIN, int NBUF = 4>
 __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
+    static_assert(NBUF == 2 || NBUF == 4, "B buffers");
     constexpr int KS = 6, CN = 64, CK = 32, NSG = 4, NB = 2 * CN * CK / 8;
     constexpr int NKK = KS * KS;
     constexpr int hin = HIN, ho = HIN - KS + 1, ho2 = ho * ho, hin2 = hin * hin;
@@ -56,8 +59,8 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     static_assert(XR % 8 == 0 && BR % 8 == 0, "16-byte pieces");
     extern __shared__ __attribute__((aligned(16))) u32x4 h3f_lds[];
     __shared__ float red[8][7];
-    u32x4 *Bs = h3f_lds;            // conv3 B [2][NB]
-    u32x4 *As = h3f_lds + 2 * NB;   // conv3 A image; during conv2: A1 image, B2 image
+    u32x4 *Bs = h3f_lds;               // conv3 B [NBUF][NB]
+    u32x4 *As = h3f_lds + NBUF * NB;   // conv3 A image; during conv2: A1 image, B2 image
     u32x2 *Bs2 = reinterpret_cast<u32x2 *>(Bs);
     uint16_t *A1 = reinterpret_cast<uint16_t *>(As), *B2 = A1 + A1_H;
     u32x2 *A1v = reinterpret_cast<u32x2 *>(A1), *B2v = reinterpret_cast<u32x2 *>(B2);
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             kk = min(kk, NKK - 1);
             const int dv = kk / KS, du = kk - dv * KS;
             const int off = dv * XW + du;
-            const u32x4 *pb = Bs + (kk & 1) * NB + bslot;
+            const u32x4 *pb = Bs + (kk & (NBUF - 1)) * NB + bslot;
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
@@ -346,16 +349,32 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
                 }
             }
         };
+        // NBUF 2: B(kk+3) -> registers, B(kk+2) -> LDS buffer kk & 1, barrier every offset.
+        // NBUF 4: B(kk+4) -> register set kk & 1, B(kk+3) (loaded one offset earlier) ->
+        // buffer (kk+3) & 3, barrier after odd offsets: a buffer written at offset kk is
+        // read at kk+2 and last read at kk-2, so a barrier always separates the two
         auto step = [&](int kk, const Frag &cur, Frag &nxt, int set) {
-            b_load(kk + 3, set ^ 1);
-            frag_read(kk + 1, nxt);
-            mfma_block(cur);
-            b_store(kk & 1, set);
-            __syncthreads();
+            if (NBUF == 2) {
+                b_load(kk + 3, set ^ 1);
+                frag_read(kk + 1, nxt);
+                mfma_block(cur);
+                b_store(kk & 1, set);
+                __syncthreads();
+            } else {
+                b_load(kk + 4, set);
+                frag_read(kk + 1, nxt);
+                mfma_block(cur);
+                b_store((kk + 3) & 3, set ^ 1);
+                if (kk & 1) __syncthreads();
+            }
         };
         Frag f0, f1;
         frag_read(0, f0);
         b_load(2, 0);
+        if (NBUF == 4) {
+            b_load(3, 1);
+            b_store(2, 0);
+        }
         __syncthreads();
         static_assert(NKK % 2 == 0, "offsets come in pairs");
         for (int kk = 0; kk < NKK; kk += 2) {
@@ -365,7 +384,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         if (a.dbg) ts[4] = clock64();
         // output through LDS as conv_h3s_kernel
         constexpr int CS = 80;
-        static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN>() - 2 * NB * 16, "output staging fits");
+        static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN, NBUF>() - NBUF * NB * 16, "output staging fits");
         float *Cs = reinterpret_cast<float *>(As);
 #pragma unroll
         for (int k = 0; k < NT; ++k) {

@@ -1211,13 +1211,13 @@ static void h3c2_launch_bs(const float *a1, const float *wimg, const float *b2, 
     launch_check("conv_h3c2_kernel");
 }
 
-template <int HIN>
-static void h3f_launch_bs(const H3FArgs &fa, int64_t S, hipStream_t s) {
-    constexpr size_t lds = (size_t)h3f_lds_bytes<HIN>();
+template <int HIN, int NBUF>
+static void h3f_launch_nb(const H3FArgs &fa, int64_t S, hipStream_t s) {
+    constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, NBUF>();
     static_assert(lds <= 160 * 1024, "conv_h3f LDS");
     static bool attr = false;
     if (!attr) {
-        SNK_HIP(hipFuncSetAttribute((const void *)conv_h3f_kernel<HIN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        SNK_HIP(hipFuncSetAttribute((const void *)conv_h3f_kernel<HIN, NBUF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
         attr = true;
     }
@@ -1228,7 +1228,7 @@ static void h3f_launch_bs(const H3FArgs &fa, int64_t S, hipStream_t s) {
         uint64_t *d = dalloc<uint64_t>(nd);
         H3FArgs f2 = fa;
         f2.dbg = d;
-        conv_h3f_kernel<HIN><<<grid, 512, lds, s>>>(f2, (int)S);
+        conv_h3f_kernel<HIN, NBUF><<<grid, 512, lds, s>>>(f2, (int)S);
         launch_check("conv_h3f_kernel");
         std::vector<uint64_t> hbuf(nd);
         SNK_HIP(hipMemcpyAsync(hbuf.data(), d, nd * 8, hipMemcpyDeviceToHost, s));
@@ -1249,8 +1249,18 @@ static void h3f_launch_bs(const H3FArgs &fa, int64_t S, hipStream_t s) {
                 (double)(rmax - rmin) / 100.0);
         return;
     }
-    conv_h3f_kernel<HIN><<<grid, 512, lds, s>>>(fa, (int)S);
+    conv_h3f_kernel<HIN, NBUF><<<grid, 512, lds, s>>>(fa, (int)S);
     launch_check("conv_h3f_kernel");
+}
+
+// conv3 B staging: 4 LDS buffers, one barrier per offset pair (SNK_H3F_NBUF=2: one per offset)
+template <int HIN>
+static void h3f_launch_bs(const H3FArgs &fa, int64_t S, hipStream_t s) {
+    static const bool nb2 = getenv("SNK_H3F_NBUF") && atoi(getenv("SNK_H3F_NBUF")) == 2;
+    if (nb2)
+        h3f_launch_nb<HIN, 2>(fa, S, s);
+    else
+        h3f_launch_nb<HIN, 4>(fa, S, s);
 }
 
 static void conv_h3f_launch(int bs, const H3FArgs &fa, int64_t S, hipStream_t s) {
