@@ -32,7 +32,7 @@ extern "C" {
 #define SNK_ERR_FOOD_EXHAUSTED 2   /* utils.jl:37 board[0] = 2 -> BoundsError */
 #define SNK_ERR_HIP 3              /* HIP runtime error */
 #define SNK_ERR_NOMEM 4
-#define SNK_ERR_STATE 5            /* e.g. structs.jl:154 batch_size > capacity */
+#define SNK_ERR_STATE 5            /* e.g. structs.jl:113 batch_size > capacity */
 #define SNK_ERR_INTERNAL 6
 
 #define SNK_ACT_INDEX 0            /* actions are indices into available_actions */
@@ -52,13 +52,13 @@ int snk_memcpy_h2d(void *dst_dev, const void *src_host, int64_t bytes);
 int snk_memcpy_d2h(void *dst_host, const void *src_dev, int64_t bytes);
 int snk_memset(void *dev, int32_t value, int64_t bytes);
 
-/* structs.jl:111 — the 50-entry food list drawn from Xoshiro(seed):
+/* structs.jl:70 — the 50-entry food list drawn from Xoshiro(seed):
  * (rand(rng, 2:bs-1), rand(rng, 2:bs-1)) per entry, returned as cells. */
 int snk_food_list(int32_t board_size, uint32_t seed, int32_t n, int32_t *cells_host);
 
 /* ---------------------------------------------------------------- env
  * A batch of n independent SnakeGame()s stepped in lockstep
- * (structs.jl:47-141 SnakeGame; utils.jl:7-149 env methods). */
+ * (structs.jl:33-99 SnakeGame; utils.jl:7-149 env methods). */
 typedef struct snk_env_s *snk_env;
 
 /* SnakeGame(board_size, n_frames, discount, Xoshiro(food_seed)) for n envs.
@@ -96,7 +96,7 @@ int snk_env_synth_actions(snk_env env, uint64_t seed, uint8_t *act_dev);
 int snk_env_info(snk_env env, int64_t *n, int32_t *board_size, int32_t *n_frames, int64_t *t);
 
 /* ---------------------------------------------------------------- replay
- * ReplayBuffer (structs.jl:145-157) with store! (utils.jl:267-277),
+ * ReplayBuffer (structs.jl:104-116) with store! (utils.jl:267-277),
  * sample (utils.jl:280-287) and stack_exp (utils.jl:343-383). Each slot holds
  * the n_frames+1 boards b_{t-C}..b_t of one transition plus its metadata. */
 typedef struct snk_replay_s *snk_replay;
@@ -123,7 +123,7 @@ int snk_replay_gather(snk_replay rb, const int64_t *idx_dev, int64_t B, float *s
                       uint8_t *dones_dev, uint8_t *mask_dev, uint8_t *dirs_dev);
 
 /* ---------------------------------------------------------------- DQNModel
- * DQNModel (structs.jl:161-185): q_net, t_net = deepcopy(q_net) and the
+ * DQNModel (structs.jl:120-147): q_net, t_net = deepcopy(q_net) and the
  * RMSProp(lr) state. Parameters cross the ABI in Flux.destructure order
  * (per layer weight then bias, each column-major; Conv = true convolution). */
 typedef struct snk_dqn_s *snk_dqn;
@@ -181,7 +181,7 @@ int snk_dqn_update(snk_dqn m, snk_replay rb, const int64_t *idx_dev, int64_t B, 
  * The batched train! loop (utils.jl:420-494) over a batch of envs. */
 typedef struct snk_trainer_s *snk_trainer;
 typedef struct {
-    float epsilon;              /* structs.jl:206 epsilon = 1.0 */
+    float epsilon;              /* structs.jl:165 epsilon = 1.0 */
     float epsilon_end;          /* 0.05 */
     float decay;                /* 1e-6, subtracted per update (utils.jl:480) */
     int32_t updates_per_iter;   /* DQN updates per lockstep env step */

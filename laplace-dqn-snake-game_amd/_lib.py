@@ -40,7 +40,7 @@ class FoodListExhausted(SnakeHipError):
 
 
 class BufferSizeError(SnakeHipError):
-    """structs.jl:154 `batch_size cannot be greater than the capacity of the buffer.`"""
+    """structs.jl:113 `batch_size cannot be greater than the capacity of the buffer.`"""
 
 
 _lib = None

@@ -1,5 +1,5 @@
 """load_trainer (utils.jl:414-418): Julia BSON.jl checkpoints of the reference's
-Trainer (structs.jl:192-216), read as data for warm starts.
+Trainer (structs.jl:151-175), read as data for warm starts.
 
 A BSON.jl file is ordinary BSON (decoded with pymongo's `bson`, nothing in
 the file is executed); Julia objects are tagged documents: {"tag": "struct",
@@ -15,7 +15,7 @@ What is taken from the file:
     the SnakeGame struct gained fields between the reference's versions);
   * frames: conv1's input channels; RMSProp eta/rho/eps: model.opt;
   * n_batches, target_update_rate, epsilon, epsilon_end, decay, losses,
-    episode_rewards: Trainer fields 3..10 (structs.jl:194-204).
+    episode_rewards: Trainer fields 3..10 (structs.jl:153-163).
 The replay buffer is not restored (the reference saves it separately,
 utils.jl:488).
 """

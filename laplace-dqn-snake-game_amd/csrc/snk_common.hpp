@@ -3,7 +3,7 @@
 // Status-code error model (include/snakehip.h): every C-ABI entry point
 // returns an int status and records a thread-local message readable through
 // snk_last_error(). This replaces the reference's Julia exceptions
-// (utils.jl:241 error(), structs.jl:154 throw, utils.jl:37 BoundsError).
+// (utils.jl:241 error(), structs.jl:113 throw, utils.jl:37 BoundsError).
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -1,4 +1,4 @@
-// snk_dqn.hip — DQNModel handle (structs.jl:161-185): q_net, t_net and the
+// snk_dqn.hip — DQNModel handle (structs.jl:120-147): q_net, t_net and the
 // RMSProp state, plus the C-ABI for forward, epsilon_greedy, the DQN update
 // (utils.jl:442-466) and update_target_net! (utils.jl:174-177).
 #include <cmath>
@@ -216,7 +216,7 @@ extern "C" int snk_dqn_create(snk_dqn *out, int32_t bs, int32_t C, float lr, flo
         }
         dqn_permute(h, h->tmp, h->theta_q, true, s);
         dqn_q_changed(h, s);
-        dqn_sync_target_launch(h, nullptr, 1, s);   // t_net = deepcopy(q_net) (structs.jl:177)
+        dqn_sync_target_launch(h, nullptr, 1, s);   // t_net = deepcopy(q_net) (structs.jl:136)
         SNK_HIP(hipMemsetAsync(h->acc, 0, P * 4, s));
         SNK_HIP(hipMemsetAsync(h->grad, 0, P * 4, s));
         SNK_HIP(hipMemsetAsync(h->loss_dev, 0, 8, s));

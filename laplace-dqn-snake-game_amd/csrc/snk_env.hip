@@ -147,7 +147,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *_
                 EnvState ns{};
                 ns.head = 0;
                 ns.len = 2;
-                ring[0] = (uint16_t)((bs - 3) + bs);  // structs.jl:88 (bs-2, 2)
+                ring[0] = (uint16_t)((bs - 3) + bs);  // structs.jl:47 (bs-2, 2)
                 ring[1] = (uint16_t)((bs - 2) + bs);  //              (bs-1, 2)
                 E.state[e] = ns;
                 E.ep_reward[e] = 0.0f;
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *_
             }
         }
         if (f & 2) {
-            // auto-reset: next state is (b0, b0) (structs.jl:94 n_frames copies)
+            // auto-reset: next state is (b0, b0) (structs.jl:53 n_frames copies)
             const int4 v0 = *reinterpret_cast<const int4 *>(E.init_board + c * 16);
             *reinterpret_cast<int4 *>(fr + nxt * PITCH) = v0;
             if (E.C == 2) *reinterpret_cast<int4 *>(fr + cur * PITCH) = v0;
@@ -319,12 +319,12 @@ extern "C" int snk_env_create(snk_env *out, int64_t n, int32_t bs, int32_t C, ui
         d.ring_cap = bs * bs;
         d.n_food = 50;
         const int ncell = bs * bs;
-        // structs.jl:111 food list (host Xoshiro restatement), 50 entries
+        // structs.jl:70 food list (host Xoshiro restatement), 50 entries
         int32_t cells[64];
         if (snk_food_list(bs, food_seed, d.n_food, cells) != SNK_OK) throw Error{SNK_ERR_INTERNAL};
         int16_t food16[64];
         for (int k = 0; k < d.n_food; ++k) food16[k] = (int16_t)cells[k];
-        // structs.jl:75-92 SnakeGame() board
+        // structs.jl:34-51 SnakeGame() board
         std::vector<int8_t> b0(d.pitch, 0);
         for (int j = 0; j < bs; ++j)
             for (int i = 0; i < bs; ++i)

@@ -1,6 +1,6 @@
 // snk_qnet.hip — Q-net forward / backward / RMSProp on gfx950.
 //
-// Forward (structs.jl:168-180 Chain): conv1 on VALU (K = 9*C is tiny), conv2,
+// Forward (structs.jl:127-139 Chain): conv1 on VALU (K = 9*C is tiny), conv2,
 // conv3 and Dense1 as implicit GEMMs on v_mfma_f32_32x32x2_f32, then one
 // wave per sample for Dense2 with a mode-specific epilogue: epsilon_greedy
 // (utils.jl:153-172), the TD target (utils.jl:448-451) or the Huber loss and

@@ -1,4 +1,4 @@
-// snk_qnet.hpp — the DQNModel Q-net on the device (structs.jl:161-180).
+// snk_qnet.hpp — the DQNModel Q-net on the device (structs.jl:127-139).
 //
 //   Conv(3x3, C=>16, relu, pad 1) -> Conv(3x3, 16=>32, relu, pad 1)
 //   -> Conv(6x6, 32=>64, relu) -> flatten -> Dense(64*(bs-5)^2 => 64, relu)

@@ -1,4 +1,4 @@
-// snk_replay.hip — ReplayBuffer on the device (structs.jl:145-157).
+// snk_replay.hip — ReplayBuffer on the device (structs.jl:104-116).
 //
 // A ring of `capacity` transition slots. Slot k holds the n_frames+1 boards
 // b_{t-C}..b_t (int8, 16-byte pitched) from which both s = (b_{t-C}..b_{t-1})
@@ -159,7 +159,7 @@ extern "C" int snk_replay_create(snk_replay *out, int64_t cap, int32_t bs, int32
         SNK_CHECK(out, SNK_ERR_INVALID, "out is NULL");
         SNK_CHECK(cap > 0 && bs >= 6 && bs <= 20 && (C == 1 || C == 2), SNK_ERR_INVALID,
                   "bad replay geometry");
-        // structs.jl:154
+        // structs.jl:113
         SNK_CHECK(batch > 0 && batch <= cap, SNK_ERR_STATE,
                   "batch_size cannot be greater than the capacity of the buffer.");
         SNK_CHECK(batch <= 4096, SNK_ERR_INVALID, "batch_size > 4096 unsupported");

@@ -1,6 +1,6 @@
 // snk_runtime.hip — runtime plumbing of libsnakehip: error reporting, the
 // library stream, device memory helpers, and the host-side food list
-// (structs.jl:111, Julia Random.Xoshiro seeded through SHA-256).
+// (structs.jl:70, Julia Random.Xoshiro seeded through SHA-256).
 #include <cstdarg>
 #include <cstring>
 #include <string>
@@ -201,7 +201,7 @@ extern "C" int snk_food_list(int32_t bs, uint32_t seed, int32_t n, int32_t *cell
         SNK_CHECK(cells && n >= 0 && n <= 64 && bs >= 3, SNK_ERR_INVALID, "bad food_list arguments");
         JuliaXoshiro rng(seed);
         for (int k = 0; k < n; ++k) {
-            const int64_t r = rng.range(2, bs - 1);  // row drawn first (structs.jl:111)
+            const int64_t r = rng.range(2, bs - 1);  // row drawn first (structs.jl:70)
             const int64_t c = rng.range(2, bs - 1);
             cells[k] = (int32_t)((r - 1) + (c - 1) * bs);
         }

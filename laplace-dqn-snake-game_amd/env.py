@@ -1,6 +1,6 @@
 """SnakeGame and the env methods, batched on the GPU.
 
-Mirror of the reference's Julia API (structs.jl:47-141, utils.jl:7-149):
+Mirror of the reference's Julia API (structs.jl:33-99, utils.jl:7-149):
 `SnakeGame(board_size, n_frames, discount, food_rng)` becomes a batch of
 `n_envs` games that step in lockstep inside libsnakehip; `step!` is `step_`,
 `reset!` is `reset_`, `virtual_step` reads the suicidal mask the fused step
@@ -29,7 +29,7 @@ def available_action_codes(prev_dir: int) -> list[int]:
 
 
 def food_list(board_size: int, seed: int = 42, n: int = 50) -> list[tuple[int, int]]:
-    """structs.jl:111 food list as 1-based (row, col) pairs."""
+    """structs.jl:70 food list as 1-based (row, col) pairs."""
     cells = np.zeros(n, np.int32)
     call("snk_food_list", board_size, seed, n, ptr(cells))
     return [(int(c) % board_size + 1, int(c) // board_size + 1) for c in cells]
@@ -38,15 +38,15 @@ def food_list(board_size: int, seed: int = 42, n: int = 50) -> list[tuple[int, i
 class SnakeGame:
     """A batch of `n_envs` reference SnakeGame()s living in GPU memory.
 
-    structs.jl:74 `SnakeGame(board_size=10, n_frames=2, discount=0.99,
+    structs.jl:33 `SnakeGame(board_size=10, n_frames=2, discount=0.99,
     food_rng=Xoshiro(42))`. `autoreset=True` restarts a lost game on its next
     step (the batched trainer's mode); with False a lost game stays frozen
     until `reset_` (the reference's one-episode-per-SnakeGame() mode).
     """
 
-    eating_reward = 1.0      # structs.jl:130
-    suicide_penalty = -1.0   # structs.jl:131
-    male_di_vivere = -0.01   # structs.jl:132
+    eating_reward = 1.0      # structs.jl:89
+    suicide_penalty = -1.0   # structs.jl:90
+    male_di_vivere = -0.01   # structs.jl:91
 
     def __init__(self, board_size: int = 10, n_frames: int = 2, discount: float = 0.99,
                  food_seed: int = 42, *, n_envs: int = 1, max_hist: int = 500, autoreset: bool = False):

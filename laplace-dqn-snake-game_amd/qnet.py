@@ -1,4 +1,4 @@
-"""DQNModel on the GPU (structs.jl:161-185) and update_target_net!
+"""DQNModel on the GPU (structs.jl:120-147) and update_target_net!
 (utils.jl:174-177).
 
 Parameters cross the boundary in `Flux.destructure` order (per layer the
@@ -22,7 +22,7 @@ def nparams(board_size: int, n_frames: int) -> int:
 
 
 class DQNModel:
-    """structs.jl:168 `DQNModel(board_size=10, n_actions=3; lr=0.0005)`.
+    """structs.jl:127 `DQNModel(board_size=10, n_actions=3; lr=0.0005)`.
 
     Weights: Flux glorot_uniform (zero biases) drawn from a counter RNG with
     `seed` (the reference uses Julia's unseeded global RNG); t_net starts as
@@ -31,7 +31,7 @@ class DQNModel:
     def __init__(self, board_size: int = 10, n_actions: int = 3, *, n_frames: int = 2, lr: float = 0.0005,
                  rho: float = 0.9, eps: float = 1e-8, seed: int = 1234):
         if n_actions != 3:
-            raise ValueError("the reference Q-net has 3 outputs (structs.jl:175)")
+            raise ValueError("the reference Q-net has 3 outputs (structs.jl:134)")
         self.board_size, self.n_frames, self.n_actions = int(board_size), int(n_frames), 3
         self.lr, self.rho, self.eps = float(lr), float(rho), float(eps)
         h = vp()

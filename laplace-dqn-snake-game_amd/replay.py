@@ -1,4 +1,4 @@
-"""ReplayBuffer on the GPU (structs.jl:145-157, utils.jl:262-383).
+"""ReplayBuffer on the GPU (structs.jl:104-116, utils.jl:262-383).
 
 The ring holds, per transition, the n_frames+1 boards b_{t-C}..b_t and the
 metadata of the reference's `Experience` tuple (imports.jl:27-36): action
@@ -17,7 +17,7 @@ from .env import ALL_ACTIONS, NULL_ACTION, available_action_codes
 
 
 class ReplayBuffer:
-    """structs.jl:151 `ReplayBuffer(capacity=50000)` with `batch_size = 64`."""
+    """structs.jl:110 `ReplayBuffer(capacity=50000)` with `batch_size = 64`."""
 
     def __init__(self, capacity: int = 50000, *, board_size: int = 10, n_frames: int = 2,
                  batch_size: int = 64):

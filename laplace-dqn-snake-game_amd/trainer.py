@@ -1,5 +1,5 @@
 """Trainer, train!, fill_buffer!, epsilon_greedy and play_episode
-(structs.jl:192-216, utils.jl:153-259, 389-494) on the GPU.
+(structs.jl:151-175, utils.jl:153-259, 389-494) on the GPU.
 
 The batched trainer keeps the reference's per-update schedule — epsilon
 decays by `decay` per update, update_target_net! when nb % rate == 0
@@ -33,7 +33,7 @@ def epsilon_greedy(game: SnakeGame, model: DQNModel, epsilon: float, *, seed: in
 
 
 class Trainer:
-    """structs.jl:205 `Trainer(; n_batches=1000, target_update_rate=1000,
+    """structs.jl:164 `Trainer(; n_batches=1000, target_update_rate=1000,
     epsilon=1.0, epsilon_end=0.05, decay=1e-6, save=true, game, model)`."""
 
     def __init__(self, *, n_batches: int = 1000, target_update_rate: int = 1000, epsilon: float = 1.0,

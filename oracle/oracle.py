@@ -76,7 +76,7 @@ def xoshiro_seed(seed: int = 42) -> np.ndarray:
 
 
 def food_list(bs: int, seed: int = 42, n: int = 50):
-    """structs.jl:111 — returns (cells int32[n] column-major 0-based, rng state after)."""
+    """structs.jl:70 — returns (cells int32[n] column-major 0-based, rng state after)."""
     cells = np.zeros(n, np.int32)
     st = np.zeros(4, np.uint64)
     lib().orc_food_list(bs, seed, n, cells, st)

@@ -70,7 +70,7 @@ static void sha_final(sha256_ctx *c, uint8_t out[32]) {
 /* Julia Random hash_seed(seed::Integer): SHA-256 over the seed's UInt32
  * little-endian words (one word for 42); Xoshiro's s0..s3 are the first four
  * little-endian UInt64 of the digest, s4 = s0 + 3s1 + 5s2 + 7s3.
- * Used by structs.jl:74 `food_rng = Xoshiro(42)`. */
+ * Used by structs.jl:33 `food_rng = Xoshiro(42)`. */
 void orc_julia_xoshiro_seed(uint32_t seed, uint64_t st[5]) {
     sha256_ctx c; uint8_t dg[32], w[4];
     for (int i = 0; i < 4; i++) w[i] = (uint8_t)(seed >> (8 * i));
@@ -109,7 +109,7 @@ int64_t orc_rand_range(uint64_t st[4], int64_t a, int64_t b) {
     return a + (int64_t)(uint64_t)(m >> 64);
 }
 
-/* structs.jl:111: food_list = [CartesianIndex(rand(rng,2:bs-1), rand(rng,2:bs-1)) for _ in 1:50]
+/* structs.jl:70: food_list = [CartesianIndex(rand(rng,2:bs-1), rand(rng,2:bs-1)) for _ in 1:50]
  * (row drawn first). Output cells are column-major 0-based. */
 void orc_food_list(int bs, uint32_t seed, int n, int32_t *cells, uint64_t st_after[4]) {
     uint64_t st[5];
@@ -129,7 +129,7 @@ static int dir_delta(int bs, int d) {
 
 int orc_game_sizeof(void) { return (int)sizeof(orc_game); }
 
-/* SnakeGame(board_size, n_frames, ...) structs.jl:74-141 */
+/* SnakeGame(board_size, n_frames, ...) structs.jl:33-99 */
 void orc_game_init(orc_game *g, int bs, int n_frames, int max_hist, const int32_t *food, int n_food) {
     memset(g, 0, sizeof *g);
     g->bs = bs; g->n_frames = n_frames; g->max_hist = max_hist;
@@ -337,7 +337,7 @@ uint32_t orc_synth_action(uint64_t seed, uint64_t env, uint64_t step) {
     return (uint32_t)((h >> 32) % 3);
 }
 
-/* ======================= Q-net (structs.jl:168-180) ======================= */
+/* ======================= Q-net (structs.jl:127-139) ======================= */
 /* Flux Conv = true convolution (kernel flipped), WHCN with dim1 = board row;
  * Flux.flatten is column-major (i, j, c); Dense W is (out, in). */
 typedef struct { int off_w1, off_b1, off_w2, off_b2, off_w3, off_b3, off_d1w, off_d1b, off_d2w, off_d2b, P, F1, Wo; } qlayout;

@@ -38,10 +38,10 @@ extern "C" {
 void orc_julia_xoshiro_seed(uint32_t seed, uint64_t state5[5]);
 uint64_t orc_xoshiro_next(uint64_t st[4]);
 int64_t orc_rand_range(uint64_t st[4], int64_t a, int64_t b);
-/* structs.jl:111 — n pairs (rand(rng,2:bs-1), rand(rng,2:bs-1)); cells out */
+/* structs.jl:70 — n pairs (rand(rng,2:bs-1), rand(rng,2:bs-1)); cells out */
 void orc_food_list(int bs, uint32_t seed, int n, int32_t *cells, uint64_t st_after[4]);
 
-/* ---- env (structs.jl:74-141, utils.jl:7-149) ---------------------------- */
+/* ---- env (structs.jl:33-99, utils.jl:7-149) ---------------------------- */
 typedef struct orc_game {
     int32_t bs, n_frames, max_hist;
     int32_t len;            /* snake length */
@@ -87,7 +87,7 @@ void orc_batch_states(const orc_batch *b, int8_t *states /* [n][C][bs*bs] */);
 uint64_t orc_splitmix64(uint64_t x);
 uint32_t orc_synth_action(uint64_t seed, uint64_t env, uint64_t step);
 
-/* ---- Q-net (structs.jl:168-180), Flux destructure param order ------------ */
+/* ---- Q-net (structs.jl:127-139), Flux destructure param order ------------ */
 int64_t orc_qnet_nparams(int bs, int C);
 /* x: [B][C][bs][bs] Julia (bs,bs,C,B) memory, q: [B][3] */
 void orc_qnet_forward(int bs, int C, const float *params, int B, const double *x, double *q);

@@ -11,7 +11,7 @@ def test_food_list_matches_bson(golden):
     cells, st = oracle.food_list(10, 42, 50)
     got = [[int(c) % 10 + 1, int(c) // 10 + 1] for c in cells]
     assert got == fx["food_list_1based"]
-    # RNG state after the 100 draws of structs.jl:111 equals the stored food_rng
+    # RNG state after the 100 draws of structs.jl:70 equals the stored food_rng
     assert ["%016x" % int(w) for w in st] == fx["food_rng_state_s0_s4_hex"][:4]
     s0 = oracle.xoshiro_seed(42)
     assert "%016x" % int(s0[4]) == fx["food_rng_state_s0_s4_hex"][4]   # s4 = s0+3s1+5s2+7s3
