@@ -189,9 +189,10 @@ typedef struct {
     double gamma;               /* 0.97 (utils.jl:451) */
     uint64_t seed;              /* counter-RNG seed for actions and sampling */
     int64_t loss_log_capacity;  /* ring of per-update losses (tr.losses) */
+    int32_t graph_unroll;       /* lockstep iterations per captured hipGraph (0 = 8) */
 } snk_trainer_cfg_t;
 typedef struct {
-    int64_t episodes, score_sum, updates, env_steps;
+    int64_t episodes, score_sum, updates, nb, env_steps;
     double reward_sum, last_loss;
     float reward_max;
     int32_t score_max;
@@ -203,6 +204,13 @@ int snk_trainer_destroy(snk_trainer t);
 /* iters lockstep iterations; learn = 0 is fill_buffer! (utils.jl:389-402);
  * use_graph = 1 replays one captured hipGraph per iteration */
 int snk_trainer_run(snk_trainer t, int64_t iters, int32_t learn, int32_t use_graph);
+/* one lockstep iteration with n_updates <= updates_per_iter updates (the last,
+ * partial iteration of train! when n_batches + 1 is not a multiple) */
+int snk_trainer_run_partial(snk_trainer t, int32_t n_updates);
+/* the reference's batch counter nb: update_target_net! runs after an update
+ * when nb % target_update_rate == 0, then nb += 1. train! starts at 0
+ * (utils.jl:431,469), compute_D at 1 (compute_D.jl:56,134). Default 0. */
+int snk_trainer_set_nb(snk_trainer t, int64_t nb);
 int snk_trainer_stats(snk_trainer t, snk_trainer_stats_t *out);
 /* tr.losses: loss of update u at host[u % loss_log_capacity] */
 int snk_trainer_losses(snk_trainer t, double *host, int64_t n);

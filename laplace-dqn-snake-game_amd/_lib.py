@@ -104,6 +104,8 @@ _PROTOS = {
     "snk_trainer_create": [P(vp), vp, vp, vp, vp],
     "snk_trainer_destroy": [vp],
     "snk_trainer_run": [vp, i64, i32, i32],
+    "snk_trainer_run_partial": [vp, i32],
+    "snk_trainer_set_nb": [vp, i64],
     "snk_trainer_stats": [vp, vp],
     "snk_trainer_losses": [vp, vp, i64],
     "snk_trainer_act_ptr": [vp, P(vp)],
@@ -142,12 +144,13 @@ SNK_LAP_D32 = 4
 class TrainerCfg(C.Structure):
     """snk_trainer_cfg_t"""
     _fields_ = [("epsilon", f32), ("epsilon_end", f32), ("decay", f32), ("updates_per_iter", i32),
-                ("target_update_rate", i64), ("gamma", f64), ("seed", u64), ("loss_log_capacity", i64)]
+                ("target_update_rate", i64), ("gamma", f64), ("seed", u64), ("loss_log_capacity", i64),
+                ("graph_unroll", i32)]
 
 
 class TrainerStats(C.Structure):
     """snk_trainer_stats_t"""
-    _fields_ = [("episodes", i64), ("score_sum", i64), ("updates", i64), ("env_steps", i64),
+    _fields_ = [("episodes", i64), ("score_sum", i64), ("updates", i64), ("nb", i64), ("env_steps", i64),
                 ("reward_sum", f64), ("last_loss", f64), ("reward_max", f32), ("score_max", i32),
                 ("epsilon", f32)]
 _RESTYPE = {"snk_last_error": C.c_char_p}

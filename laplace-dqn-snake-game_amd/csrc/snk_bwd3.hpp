@@ -34,14 +34,7 @@ struct Conv3BwdArgs {
     float *slab;        // dW partials [Z][1153][64] (row 1152: bias)
     float *dz2;         // [S][bs*bs][32]
     int S, bs, wo, nsc, Z, nW;
-    int boff;           // first block index of this launch (the halves as separate launches: profiling)
-    uint64_t *dbg;      // SNK_C3_DBG: per-block [clock at start, staged, computed, end, wall start, wall end]
 };
-#define C3_TS(k)                                                                  \
-    do {                                                                          \
-        if (a.dbg && threadIdx.x == 0) a.dbg[(blockIdx.x + a.boff) * 8 + (k)] = clock64(); \
-    } while (0)
-
 constexpr int C3_CG = 4;          // dX input channels per workgroup
 constexpr int C3_DLD = 68;        // LDS row stride of dz3 / weights in dX (16x16x4 reads conflict-free)
 constexpr int C3_TLD = 36 * C3_CG + 1;
@@ -105,7 +98,6 @@ __device__ __forceinline__ void c3_dw_block(const Conv3BwdArgs &a, int z, int gr
     c3_copy<8>(reinterpret_cast<f32x4 *>(D), reinterpret_cast<const f32x4 *>(a.dz3 + (int64_t)s0 * wo2 * 64),
                ns * wo2 * 16);
     __syncthreads();
-    C3_TS(1);
     const int r = lane & 31, h = lane >> 5;
     const int kk = grp * 4 + wave;
     const int dv = kk / 6, du = kk - dv * 6;
@@ -127,7 +119,6 @@ __device__ __forceinline__ void c3_dw_block(const Conv3BwdArgs &a, int z, int gr
             acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv ? x : 0.0f, y1, acc[1], 0, 0, 0);
         }
     }
-    C3_TS(2);
     float *out = a.slab + (int64_t)z * 1153 * 64;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -172,7 +163,6 @@ __device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg
     c3_copy_rows<4>(Dz, a.dz3 + (int64_t)s * wo2 * 64, wo2, [](int row) { return row; });
     c3_copy_rows<9>(Wl, a.w, NN, [cg](int n) { return (n / C3_CG) * 32 + cg * C3_CG + n % C3_CG; });
     __syncthreads();
-    C3_TS(1);
     // T in 16x16 tiles (v_mfma_f32_16x16x4_f32: lane l holds A[l&15][k + (l>>4)],
     // B[k + (l>>4)][l&15]; C rows 4*(l>>4) + e, column l&15), round robin over the waves
     // (all tiles kept in registers, then written over the operands after a barrier)
@@ -206,7 +196,6 @@ __device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg
         }
     }
     __syncthreads();
-    C3_TS(2);
     // col2im + relu mask, (pin, ci) per thread: the 36 terms load together (out-of-grid
     // terms read a valid slot and add 0), summed kk ascending
 #pragma unroll
@@ -234,9 +223,7 @@ __device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg
 
 __global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float c3sm[];
-    const int b = blockIdx.x + a.boff;
-    C3_TS(0);
-    if (a.dbg && threadIdx.x == 0) a.dbg[b * 8 + 4] = wall_clock64();
+    const int b = blockIdx.x;
     if (b < a.nW) {
         switch (a.wo) {
             case 3: c3_dw_block<3>(a, b / 9, b % 9, c3sm); break;
@@ -248,9 +235,6 @@ __global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
         }
     } else
         c3_dx_block(a, (b - a.nW) / (32 / C3_CG), (b - a.nW) % (32 / C3_CG), c3sm);
-    __syncthreads();
-    C3_TS(3);
-    if (a.dbg && threadIdx.x == 0) a.dbg[b * 8 + 5] = wall_clock64();
 }
 
 // ---------------------------------------------------------------- conv2 (3x3, pad 1, 16 -> 32)

@@ -57,46 +57,9 @@ int guard(F &&f) {
     }
 }
 
-// Fork/join of independent launch sequences onto side streams: eagerly, or
-// under stream capture, where the side streams join the capture through the
-// events and become parallel branches of the graph. With no side streams
-// every call is a no-op and everything stays on `main`.
-enum ForkBits : unsigned { FK_SAMPLE = 1, FK_STATS = 2, FK_TARGET = 4, FK_WGRAD = 8, FK_LOSS = 16 };
-struct Fork {
-    static constexpr int NS = 3, NE = 48;
-    hipStream_t main = nullptr;
-    hipStream_t side[NS] = {};
-    hipEvent_t ev[NE] = {};
-    int nside = 0, next = 0;
-    unsigned enable = ~0u;   // FK_* branches taken (others stay on main)
-    bool on_side(unsigned bit) const { return nside && (enable & bit); }
-    // returns the stream the branch runs on
-    hipStream_t fork(int k, unsigned bit) {
-        if (!on_side(bit)) return main;
-        hipEvent_t e = ev[next++ % NE];
-        SNK_HIP(hipEventRecord(e, main));
-        SNK_HIP(hipStreamWaitEvent(side[k % nside], e, 0));
-        return side[k % nside];
-    }
-    void join(int k, unsigned bit) {
-        if (!on_side(bit)) return;
-        hipEvent_t e = ev[next++ % NE];
-        SNK_HIP(hipEventRecord(e, side[k % nside]));
-        SNK_HIP(hipStreamWaitEvent(main, e, 0));
-    }
-    void create() {
-        for (auto &q : side) SNK_HIP(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-        for (auto &e : ev) SNK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        nside = NS;
-    }
-    void destroy() {
-        for (auto &q : side)
-            if (q) (void)hipStreamDestroy(q);
-        for (auto &e : ev)
-            if (e) (void)hipEventDestroy(e);
-        nside = 0;
-    }
-};
+// hipFuncAttributeMaxDynamicSharedMemorySize of a kernel on the current
+// device, raised to at least `bytes` (set once per kernel, device and size)
+void set_lds_limit(const void *kernel, size_t bytes);
 
 template <class T>
 T *dalloc(size_t n) {
@@ -112,6 +75,29 @@ T *dalloc(size_t n) {
 inline void dfree(void *p) {
     if (p) (void)hipFree(p);
 }
+
+// Owning device allocation for host-side scopes that may throw (guard()'s
+// catch path then frees it). Moves, never copies.
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    DevBuf() = default;
+    explicit DevBuf(size_t n) : p(dalloc<T>(n)) {}
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p(o.p) { o.p = nullptr; }
+    DevBuf &operator=(DevBuf &&o) noexcept {
+        if (this != &o) {
+            dfree(p);
+            p = o.p;
+            o.p = nullptr;
+        }
+        return *this;
+    }
+    ~DevBuf() { dfree(p); }
+    T *get() const { return p; }
+    operator T *() const { return p; }
+};
 
 inline void launch_check(const char *what) {
     hipError_t e = hipGetLastError();

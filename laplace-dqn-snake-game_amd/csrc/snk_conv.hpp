@@ -40,7 +40,6 @@ struct ConvArgs {
     uint16_t *outb;      // x6 EPI_BIAS_RELU: also write the output's bf16 planes [M][3][CN]
     const float *wmax;   // h3 kernels: per-block partial max |w| of the weight image (conv1 writes them)
     int nwmax;           //   their count
-    uint64_t *dbg;       // debug: per-workgroup timestamps (SNK_H3S_DBG), else null
     int M, HIN, HOUT, nkk, kk_per_split;
     uint32_t d2m, d2s, d1m, d1s;   // FastDiv(HOUT*HOUT), FastDiv(HOUT) magic/shift
 };

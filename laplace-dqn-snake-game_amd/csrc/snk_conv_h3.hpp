@@ -110,8 +110,6 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     const int r = lane & 15, g = lane >> 4;
     const int s0 = blockIdx.x * NSG;
     const int ns = min(NSG, S - s0);
-    uint64_t ts[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0;   // SNK_H3S_DBG phase stamps
-    if (a.dbg) { ts[0] = clock64(); rt0 = wall_clock64(); }
 
     // B register sets: set kk & 1 carries B(kk) (fp32, unsplit) from global to LDS
     f32x4 bst[2];
@@ -154,12 +152,10 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     sm2 = wave_max(sm2);
     sm3 = wave_max(sm3);
     wm = wave_max(wm);
-    if (a.dbg) ts[1] = clock64();
     if (lane == 0) {
         red[wave][0] = sm0; red[wave][1] = sm1; red[wave][2] = sm2; red[wave][3] = sm3; red[wave][4] = wm;
     }
     __syncthreads();
-    if (a.dbg) ts[2] = clock64();
     int ea[NSG];
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
@@ -192,7 +188,6 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     const int nt = __builtin_amdgcn_readfirstlane(T > rg ? (T - rg + 3) / 4 : 0);
     const int bslot = (cg * 32 + r) * 4 + (g ^ ((4 - ((r >> 2) & 3)) & 3));
     __syncthreads();
-    if (a.dbg) ts[3] = clock64();
 
     // conv_x6s_kernel's pipeline (see there): offset kk's MFMAs on fragments
     // read during kk-1, B(kk+2) split into LDS while B(kk+3) is in flight
@@ -261,7 +256,6 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
             step(kk, f0, f1, 0);
             step(kk + 1, f1, f0, 1);
         }
-        if (a.dbg) ts[4] = clock64();
 
         // acc[k][ct][e]: tile row 4g + e = position 4t + g of sample e; column 16ct + r
         if (!a.outb) {
@@ -321,13 +315,6 @@ __global__ __launch_bounds__(512) void conv_h3s_kernel(ConvPair pr, int S) {
     else if (nt == 3) run(std::integral_constant<int, 3>{});
     else if (nt == 2) run(std::integral_constant<int, 2>{});
     else run(std::integral_constant<int, 1>{});
-    if (a.dbg && lane == 0) {
-        ts[5] = clock64();
-        uint64_t *d = a.dbg + ((int64_t)blockIdx.x * 8 + wave) * 8;
-        for (int q = 0; q < 6; ++q) d[q] = ts[q];
-        d[6] = rt0;
-        d[7] = wall_clock64();
-    }
 }
 
 // conv2 (3x3, 16 -> 32, pad 1, EPI_BIAS_RELU) of a large batch on the h3 split.

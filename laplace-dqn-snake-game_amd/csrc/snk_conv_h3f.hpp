@@ -29,7 +29,6 @@ struct H3FArgs {
     int nwmax;
     const float *b3;     // conv3 bias [64]
     float *out;          // a3 [S][ho^2][64]
-    uint64_t *dbg;       // SNK_H3F_DBG: per-wave phase clocks
 };
 
 template <int HIN, int NBUF = 4>
@@ -68,8 +67,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     const int r = lane & 15, g = lane >> 4;
     const int s0 = blockIdx.x * NSG;
     const int ns = min(NSG, S - s0);
-    uint64_t ts[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0;
-    if (a.dbg) { ts[0] = clock64(); rt0 = wall_clock64(); }
 
     // conv3 B register sets (as conv_h3s_kernel)
     const f32x4 *__restrict__ wsrc = reinterpret_cast<const f32x4 *>(a.w3);
@@ -189,7 +186,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         }
     }
     __syncthreads();
-    if (a.dbg) ts[1] = clock64();
 
     // ---- conv2, transposed: C^T[co][row] = sum_k W[co][k] * A[row][k] with the weight
     // fragments as the MFMA's A operand and the activation fragments as its B (the
@@ -260,7 +256,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         for (int q = 0; q < NSG; ++q) red[wave][q] = m2[q];
     }
     __syncthreads();   // also: every conv2 fragment read is done (the A image overlays them)
-    if (a.dbg) ts[2] = clock64();
     int ea[NSG];
 #pragma unroll
     for (int q = 0; q < NSG; ++q) {
@@ -297,7 +292,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     const int nt = __builtin_amdgcn_readfirstlane(T > rg ? (T - rg + 3) / 4 : 0);
     const int bslot = (cg * 32 + r) * 4 + (g ^ ((4 - ((r >> 2) & 3)) & 3));
     __syncthreads();
-    if (a.dbg) ts[3] = clock64();
 
     // ---- conv3: conv_h3s_kernel's pipeline
     auto run = [&](auto ntc) {
@@ -381,7 +375,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             step(kk, f0, f1, 0);
             step(kk + 1, f1, f0, 1);
         }
-        if (a.dbg) ts[4] = clock64();
         // output through LDS as conv_h3s_kernel
         constexpr int CS = 80;
         static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN, NBUF>() - NBUF * NB * 16, "output staging fits");
@@ -411,13 +404,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     else if (nt == 3) run(std::integral_constant<int, 3>{});
     else if (nt == 2) run(std::integral_constant<int, 2>{});
     else run(std::integral_constant<int, 1>{});
-    if (a.dbg && lane == 0) {
-        ts[5] = clock64();
-        uint64_t *d = a.dbg + ((int64_t)blockIdx.x * 8 + wave) * 8;
-        for (int q = 0; q < 6; ++q) d[q] = ts[q];
-        d[6] = rt0;
-        d[7] = wall_clock64();
-    }
 }
 
 }  // namespace snk

@@ -304,7 +304,7 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 // (2 x CN/16 tiles of 16x16); C/D: col = l&15, row = 4*(l>>4) + reg.
 // B rows in LDS are padded to CK + 16 bf16 (96 B at CK = 32): conflict-free
 // for the four ds_read_b128 lane groups.
-// WPW waves per workgroup (4: 128 rows, 8: 256 rows sharing each staged B tile)
+// WPW waves per workgroup (4: 128 rows)
 template <int CK, int CN, int KS, int PAD, int EPI, int WPW>
 __global__ __launch_bounds__(64 * WPW) void conv_x6m16_kernel(ConvPair pr) {
     const ConvArgs &a = pr.g[blockIdx.z];
@@ -457,189 +457,6 @@ __global__ __launch_bounds__(64 * WPW) void conv_x6m16_kernel(ConvPair pr) {
                         for (int pl = 0; pl < 3; ++pl) pb[pl * CN] = split_part(v, pl);
                     }
                 } else {   // EPI_SLAB
-                    a.out[(int64_t)blockIdx.y * a.M * CN + o] = acc[rt][ct][e];
-                }
-            }
-        }
-    }
-}
-
-}  // namespace snk
-
-namespace snk {
-
-// conv_x6m16 with the workgroup's whole input resident in LDS: the 128 output
-// rows of a workgroup come from at most nsmax samples, whose pre-split planes
-// are copied into LDS once, so the 36 kernel offsets read A from LDS instead
-// of re-streaming it from L2 (the x6m16 kernel moved ~2 GB of L2 traffic per
-// 4096-sample conv3, 70 % of the L2 gather rate). LDS image of A: input
-// position (i, j) of staged sample sr at (sr*XS + j*XJ + i*XI) bf16 with
-// XI = 3*CK + 16 and XJ = 12*XI + 80 (a bank-conflict simulation of every
-// read of the layer picked it: 5.25 LDS cycles per ds_read_b128 against 12
-// unpadded). 8 waves: wave w owns rows 32*(w>>1) .. +31 and columns
-// 32*(w&1) .. +31 (2 x 2 tiles of 16x16). The next offset's A fragments are
-// read during this offset's MFMAs; B is staged per offset in ONE buffer (two
-// barriers per offset) to leave the LDS to A.
-template <int CK, int CN, int KS, int PAD, int EPI>
-__global__ __launch_bounds__(512) void conv_x6a_kernel(ConvPair pr, int nsmax) {
-    static_assert(CK % 32 == 0 && CN == 64, "shape");
-    constexpr int KC = CK / 32;
-    constexpr int RW = 3 * CK;                   // bf16 per input position (global)
-    constexpr int LDB = CK + 16;
-    constexpr int PLANE = CN * LDB;
-    constexpr int NE = 3 * CN * CK / 8;
-    constexpr int NV = (NE + 511) / 512;
-    const ConvArgs &a = pr.g[blockIdx.z];
-    const uint16_t *__restrict__ wb = pr.wb[blockIdx.z];
-    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-    const int hin2 = a.HIN * a.HIN, ho2 = a.HOUT * a.HOUT;
-    const int XI = RW + 16, XJ = a.HIN * XI + 80, XS = a.HIN * XJ;
-    uint16_t *As = smem;                                // A image
-    uint16_t *Bs = smem + ((nsmax * XS + 7) & ~7);     // [BBUF]
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = lane & 15, g = lane >> 4;
-    const int m0 = blockIdx.x * 128;
-    const int s_lo = m0 / ho2;
-    const int s_hi = (min(a.M, m0 + 128) - 1) / ho2;
-    {   // stage the samples' planes: 16-byte pieces, RW/8 per position
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(a.xb + (int64_t)s_lo * hin2 * RW);
-        const int n16 = (s_hi - s_lo + 1) * hin2 * (RW / 8);
-        for (int e = tid; e < n16; e += 512) {
-            const int pos = e / (RW / 8), c = e - pos * (RW / 8);
-            const int sr = pos / hin2, q = pos - sr * hin2;
-            const int jj = q / a.HIN, ii = q - jj * a.HIN;
-            *reinterpret_cast<u32x4 *>(As + sr * XS + jj * XJ + ii * XI + c * 8) = src[e];
-        }
-    }
-    const int rb = (wave >> 1) * 32, cb = (wave & 1) * 32;
-    int rbase[2];   // LDS row (input position) of the output row at kernel offset 0
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-        const int m = min(m0 + rb + rt * 16 + r, a.M - 1);
-        const int s = m / ho2;
-        const int p = m - s * ho2;
-        const int j = p / a.HOUT, i = p - j * a.HOUT;
-        rbase[rt] = (s - s_lo) * XS + j * XJ + i * XI;
-    }
-    const int kk0 = blockIdx.y * a.kk_per_split;
-    const int kk1 = min(a.nkk, kk0 + a.kk_per_split);
-
-    f32x4v acc[2][2];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[rt][ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
-
-    const u32x4 *wsrc = reinterpret_cast<const u32x4 *>(wb);
-    int s_src[NV], s_dst[NV];
-#pragma unroll
-    for (int q = 0; q < NV; ++q) {
-        const int e = tid + q * 512;
-        const bool in = (NE % 512 == 0) || e < NE;
-        const int ee = in ? e : 0;
-        const int pl = ee / (CN * CK / 8), rem = ee - pl * (CN * CK / 8);
-        const int n = rem / (CK / 8), c8 = rem - n * (CK / 8);
-        s_src[q] = ee;
-        s_dst[q] = in ? pl * PLANE + n * LDB + c8 * 8 : 3 * PLANE;
-    }
-    u32x4 acur[2][KC][3], anxt[2][KC][3];   // [rt][kc][plane]
-    auto a_read = [&](int kk, u32x4 (&dst)[2][KC][3]) {
-        const int dv = kk / KS, du = kk - dv * KS;
-        const int off = (du - PAD) * XI + (dv - PAD) * XJ;   // PAD == 0 here: always inside
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
-            const uint16_t *pa = As + rbase[rt] + off + 8 * g;
-#pragma unroll
-            for (int kc = 0; kc < KC; ++kc)
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl) dst[rt][kc][pl] = *reinterpret_cast<const u32x4 *>(pa + pl * CK + kc * 32);
-        }
-    };
-    // B tiles ride a 3-deep register pipeline: b1 = offset kk+1, b2 = kk+2,
-    // b3 = kk+3 in flight (one workgroup per CU: nothing else hides the latency)
-    u32x4 b1[NV], b2[NV], b3[NV];
-    auto b_load = [&](int kk, u32x4 (&dst)[NV]) {
-        const int kc = kk < kk1 ? kk : kk1 - 1;
-#pragma unroll
-        for (int q = 0; q < NV; ++q) dst[q] = wsrc[(int64_t)kc * NE + s_src[q]];
-    };
-    b_load(kk0, b3);
-#pragma unroll
-    for (int q = 0; q < NV; ++q) *reinterpret_cast<u32x4 *>(&Bs[s_dst[q]]) = b3[q];
-    b_load(kk0 + 1, b1);
-    b_load(kk0 + 2, b2);
-    __syncthreads();
-    a_read(kk0, acur);
-    for (int kk = kk0; kk < kk1; ++kk) {
-        const bool more = kk + 1 < kk1;
-        const int kn = more ? kk + 1 : kk;
-        b_load(kk + 3, b3);
-        // A of the next offset (LDS, no barrier needed: A is read-only)
-        a_read(kn, anxt);
-        const uint16_t *bb = Bs + (cb + r) * LDB + 8 * g;
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-                const uint16_t *pb = bb + ct * 16 * LDB + kc * 32;
-                const bf16x8 bh = as_bf(*reinterpret_cast<const u32x4 *>(pb));
-                const bf16x8 bm = as_bf(*reinterpret_cast<const u32x4 *>(pb + PLANE));
-                const bf16x8 bl = as_bf(*reinterpret_cast<const u32x4 *>(pb + 2 * PLANE));
-#pragma unroll
-                for (int rt = 0; rt < 2; ++rt) {
-                    const bf16x8 ah = as_bf(acur[rt][kc][0]), am = as_bf(acur[rt][kc][1]),
-                                 al = as_bf(acur[rt][kc][2]);
-                    f32x4v c = acc[rt][ct];
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
-                    acc[rt][ct] = c;
-                }
-            }
-        }
-        __syncthreads();   // every wave is done reading this offset's B
-#pragma unroll
-        for (int q = 0; q < NV; ++q) *reinterpret_cast<u32x4 *>(&Bs[s_dst[q]]) = b1[q];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < NV; ++q) {
-            b1[q] = b2[q];
-            b2[q] = b3[q];
-        }
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int kc = 0; kc < KC; ++kc)
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl) acur[rt][kc][pl] = anxt[rt][kc][pl];
-    }
-
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-        const int rowb = m0 + rb + rt * 16 + 4 * g;
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-            const int col = cb + ct * 16 + r;
-            const float b = EPI == EPI_BIAS_RELU ? a.bias[col] : 0.0f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int row = rowb + e;
-                if (row >= a.M) continue;
-                const int64_t o = (int64_t)row * CN + col;
-                if (EPI == EPI_BIAS_RELU) {
-                    float v = acc[rt][ct][e] + b;
-                    v = v > 0.0f ? v : 0.0f;
-                    if (a.out) a.out[o] = v;
-                    if (a.outb) {
-                        uint16_t *pb = a.outb + (int64_t)row * 3 * CN + col;
-#pragma unroll
-                        for (int pl = 0; pl < 3; ++pl) pb[pl * CN] = split_part(v, pl);
-                    }
-                } else {
                     a.out[(int64_t)blockIdx.y * a.M * CN + o] = acc[rt][ct][e];
                 }
             }

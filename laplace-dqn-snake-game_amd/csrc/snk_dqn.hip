@@ -106,10 +106,8 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
         dfree(h->slab);
         h->slab = dalloc<float>(need);
         h->slab_cap = need;
+        ++h->slab_gen;
     }
-    Fork serial;
-    serial.main = s;
-    Fork &F = o.fork ? *o.fork : serial;
     HeadArgs ta = meta;
     ta.gamma = gamma;
     ta.target = h->trn.target;
@@ -119,27 +117,15 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
     la.loss = h->trn.loss;
     la.dq = h->trn.dq;
     la.dz1 = h->trn.dz1;
-    if (o.fork && o.fork->on_side(FK_TARGET)) {   // separate branches (measured slower)
-        hipStream_t q0 = F.fork(0, FK_TARGET);
-        qnet_forward(h->L, h->theta_t, h->wt_t, sn_src, B, h->tgt, HEAD_TARGET, ta, q0, -1, h->wtb_t);
-        for (int layer = 0; layer < 4; ++layer)
-            qnet_forward(h->L, h->theta_q, h->wt_q, s_src, B, h->trn, HEAD_LOSS, la, s, layer, h->wtb_q);
-        F.join(0, FK_TARGET);
-    } else {
-        const FwdNet nets[2] = {FwdNet{h->theta_t, h->wt_t, h->wtb_t, sn_src, &h->tgt},
-                                FwdNet{h->theta_q, h->wt_q, h->wtb_q, s_src, &h->trn}};
-        qnet_forward_pair(h->L, nets, B, s);
-        qnet_head_pair(h->L, h->theta_t, h->tgt, h->theta_q, h->trn, B, la, s);
-    }
-    if (o.fork && o.fork->on_side(FK_TARGET)) qnet_head(h->L, h->theta_q, B, h->trn, HEAD_LOSS, la, s);
-    hipStream_t q1 = o.loss_mean ? F.fork(1, FK_LOSS) : s;
-    if (o.loss_mean) loss_mean_launch(h->trn.loss, B, h->loss_dev, q1);
+    const FwdNet nets[2] = {FwdNet{h->theta_t, h->wt_t, h->wtb_t, sn_src, &h->tgt},
+                            FwdNet{h->theta_q, h->wt_q, h->wtb_q, s_src, &h->trn}};
+    qnet_forward_pair(h->L, nets, B, s);
+    qnet_head_pair(h->L, h->theta_t, h->tgt, h->theta_q, h->trn, B, la, s);
+    if (o.loss_mean) loss_mean_launch(h->trn.loss, B, h->loss_dev, s);
     BwdOpts bo;
-    bo.fork = o.fork;
     bo.defer = o.defer;
     bo.dz1_ready = true;
     qnet_backward(h->L, h->theta_q, s_src, B, h->trn, h->grad, h->slab, h->slab_cap, s, bo);
-    if (o.loss_mean) F.join(1, FK_LOSS);
 }
 
 UpdateTarget dqn_update_target(snk_dqn_s *h, const int64_t *counter, int64_t rate) {

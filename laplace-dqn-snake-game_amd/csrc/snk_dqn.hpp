@@ -12,6 +12,7 @@ struct snk_dqn_s {
     snk::QWork act, tgt, trn;       // workspaces: acting (n_envs), target net, training batch
     float *slab = nullptr;
     int64_t slab_cap = 0;
+    int64_t slab_gen = 0;           // bumped on every slab reallocation
     double *loss_dev = nullptr;
     uint8_t *meta = nullptr;
     int64_t meta_cap = 0;
@@ -37,7 +38,6 @@ BoardSrc src_env(const EnvDev &E);
 BoardSrc src_replay(const ReplayDev &R, const int64_t *idx, int chan0);
 BoardSrc src_float(const QLayout &L, const float *x);
 struct LossOpts {
-    Fork *fork = nullptr;            // target forward / weight gradients / loss mean on side streams
     GradSlabs *defer = nullptr;      // leave K-split slabs and Dense2 to grad_update_launch
     bool loss_mean = true;           // reduce the per-sample losses into h->loss_dev here
 };
@@ -49,4 +49,6 @@ void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, 
 void dqn_permute(snk_dqn_s *h, const float *src, float *dst, bool to_packed, hipStream_t s);
 // q_net parameters changed: rebuild its forward weight image
 void dqn_q_changed(snk_dqn_s *h, hipStream_t s);
+// generation of every buffer a captured trainer graph points into
+inline int64_t dqn_ws_gen(const snk_dqn_s *h) { return h->act.gen + h->tgt.gen + h->trn.gen + h->slab_gen; }
 }  // namespace snk

@@ -156,31 +156,14 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s) {
     SyrkArgs a = a0;
     const int64_t T = ceil_div(a.N, SY_T);
     a.ntiles = T * (T + 1) / 2;
-    static const bool rowmajor = getenv("SNK_SYRK_ORDER") && strcmp(getenv("SNK_SYRK_ORDER"), "rows") == 0;
-    a.tiles = (rowmajor || T < 16) ? nullptr : syrk_tile_order(a.N);
+    a.tiles = T < 16 ? nullptr : syrk_tile_order(a.N);   // XCD-aware supertile order
     SNK_CHECK(a.K % 4 == 0 && a.ld % 4 == 0 && a.kchunk % 4 == 0, SNK_ERR_INTERNAL, "syrk: K/ld not multiples of 4");
     SNK_CHECK(a.ntiles < (int64_t)1 << 31 && z <= 65535, SNK_ERR_INVALID, "syrk: problem too large");
     dim3 grid((unsigned)a.ntiles, (unsigned)z);
-    // SNK_SYRK=fp32: the exact-f32 32x32x2 MFMA everywhere; =x6: the bf16 x6 split also
-    // for pre-split (h3) callers; default: x6, and h3 where the caller pre-split x
-    static const char *env = getenv("SNK_SYRK");
-    static const bool f32 = env && strcmp(env, "fp32") == 0, nox3 = env && strcmp(env, "x6") == 0;
-    if (f32) {
-        switch (out) {
-            case SYRK_F32: syrk_kernel<SYRK_F32, SY_F32><<<grid, 256, 0, s>>>(a); break;
-            case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, SY_F32><<<grid, 256, 0, s>>>(a); break;
-            default: syrk_kernel<SYRK_DENSE_ADD, SY_F32><<<grid, 256, 0, s>>>(a); break;
-        }
-    } else if (a.xh && !nox3) {
+    if (a.xh) {   // pre-split rows (h3): fp16 parts, 3 products per fp32 product
         SNK_CHECK(out == SYRK_F32 && z == 1 && a.ldh % SY_KS == 0 && a.xe, SNK_ERR_INTERNAL, "syrk h3 arguments");
-        static const char *hk = getenv("SNK_SYRK_H3K");   // "4": 4 waves of 64 x 64 (one per SIMD)
-        if (hk && strcmp(hk, "4") == 0)
-            syrk_h3_kernel<4><<<grid, 256, 0, s>>>(a);
-        else if (getenv("SNK_SYRK_PRIO"))
-            syrk_h3_kernel<8, true><<<grid, 512, 0, s>>>(a);
-        else
-            syrk_h3_kernel<8><<<grid, 512, 0, s>>>(a);
-    } else {
+        syrk_h3_kernel<8><<<grid, 512, 0, s>>>(a);
+    } else {      // fp32 rows: bf16 x6 split in the kernel
         switch (out) {
             case SYRK_F32: syrk_kernel<SYRK_F32, SY_X6><<<grid, 256, 0, s>>>(a); break;
             case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, SY_X6><<<grid, 256, 0, s>>>(a); break;
@@ -393,9 +376,7 @@ extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_d
         if (ms_out) SNK_HIP(hipEventRecord(ev[2], s));
         SyrkArgs a{};
         a.x = m->jbuf; a.ld = Kc; a.K = Kc; a.kchunk = Kc; a.N = (int)n; a.g32 = G_dev; a.ldg = n;
-        static const char *senv = getenv("SNK_SYRK");
-        if (!senv || strcmp(senv, "h3") == 0) {
-            // h3 Gram: rows pre-split once into scaled fp16 planes (snk_syrk.hpp h3_rows_kernel)
+        {   // h3 Gram: rows pre-split once into scaled fp16 planes (snk_syrk.hpp h3_rows_kernel)
             const int64_t ldh = (Kc + SY_KS - 1) / SY_KS * SY_KS;
             const int64_t npad = (n + SW_ROWS_B - 1) / SW_ROWS_B * SW_ROWS_B;   // zero rows past n (whole row blocks)
             if (2 * npad * ldh > m->jplanes_halves) {
@@ -415,7 +396,6 @@ extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_d
             h3_rows_kernel<<<(unsigned)n, 256, 0, s>>>(m->jbuf, Kc, Kc, m->jplanes, m->jexp, ldh);
             launch_check("h3_rows_kernel");
             a.xh = m->jplanes; a.xe = m->jexp; a.ldh = ldh;
-            if (getenv("SNK_SYRK_EXP_NOLOAD")) a.kchunk = -4;   // experiment: every stage re-reads k = 0
         }
         syrk_launch(SYRK_F32, a, 1, s);
         if (ms_out) SNK_HIP(hipEventRecord(ev[3], s));
@@ -713,26 +693,33 @@ __global__ void lap_count_add_kernel(int64_t *count, int64_t n) { *count += n; }
 
 }  // namespace snk
 
+// env / scratch replay handles owned by a host scope (freed on the throw path too)
+struct EnvHold {
+    snk_env e = nullptr;
+    ~EnvHold() {
+        if (e) snk_env_destroy(e);
+    }
+};
+struct ReplayHold {
+    snk_replay r = nullptr;
+    ~ReplayHold() {
+        if (r) snk_replay_destroy(r);
+    }
+};
+
 // greedy lockstep episodes of G models whose packed weights are W [G][ldw];
-// per-model length / Float32 reward; scratch ring (slot t*G + g) left in *scratch
+// per-model length / Float32 reward; scratch ring (slot t*G + g) left in sc
 static void lap_rollout(snk_dqn m, const float *W, int64_t ldw, int64_t G, float *rew_dev, int32_t *len_dev,
-                        snk_env *env_out, snk_replay *scratch_out) {
+                        EnvHold &env, ReplayHold &sc) {
     const QLayout &L = m->L;
     hipStream_t s = stream();
     const int T = 501;   // the first episode is over by step 500 (utils.jl:88 truncation)
-    snk_env env = nullptr;
-    snk_replay sc = nullptr;
-    if (snk_env_create(&env, G, L.bs, L.C, 42, 500, 1) != SNK_OK) throw Error{SNK_ERR_HIP};
-    if (snk_replay_create(&sc, G * T, L.bs, L.C, 1) != SNK_OK) {
-        snk_env_destroy(env);
-        throw Error{SNK_ERR_HIP};
-    }
-    *env_out = env;
-    *scratch_out = sc;
-    const EnvDev &E = env_dev(env);
-    const ReplayDev &R = replay_dev(sc);
-    uint8_t *fin = dalloc<uint8_t>(G), *act = dalloc<uint8_t>(G);
-    int32_t *nfin = dalloc<int32_t>(1);
+    if (snk_env_create(&env.e, G, L.bs, L.C, 42, 500, 1) != SNK_OK) throw Error{SNK_ERR_HIP};
+    if (snk_replay_create(&sc.r, G * T, L.bs, L.C, 1) != SNK_OK) throw Error{SNK_ERR_HIP};
+    const EnvDev &E = env_dev(env.e);
+    const ReplayDev &R = replay_dev(sc.r);
+    DevBuf<uint8_t> fin(G), act(G);
+    DevBuf<int32_t> nfin(1);
     SNK_HIP(hipMemsetAsync(fin, 0, G, s));
     SNK_HIP(hipMemsetAsync(nfin, 0, sizeof(int32_t), s));
     SNK_HIP(hipMemsetAsync(len_dev, 0, G * sizeof(int32_t), s));
@@ -741,11 +728,7 @@ static void lap_rollout(snk_dqn m, const float *W, int64_t ldw, int64_t G, float
                   (G == 1 || ldw % 4 == 0),
               SNK_ERR_INVALID,
               "Laplace sampling: board side %d too large", L.bs);
-    static size_t attr = 0;
-    if (lds > attr) {
-        SNK_HIP(hipFuncSetAttribute((const void *)lap_act_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = lds;
-    }
+    set_lds_limit((const void *)lap_act_kernel, lds);
     const BoardSrc src = src_env(E);
     for (int t = 0; t < T; ++t) {
         lap_act_kernel<<<(unsigned)G, 256, lds, s>>>(L, W, ldw, src, fin, act, nullptr);
@@ -763,9 +746,6 @@ static void lap_rollout(snk_dqn m, const float *W, int64_t ldw, int64_t G, float
         }
     }
     SNK_HIP(hipStreamSynchronize(s));
-    dfree(fin);
-    dfree(act);
-    dfree(nfin);
 }
 
 extern "C" int snk_laplace_normals(uint64_t seed, int64_t model, int32_t which, int64_t i0, int64_t n, double *out_host) {
@@ -825,21 +805,16 @@ extern "C" int snk_laplace_sampling(snk_laplace h, snk_dqn m, snk_replay rb, int
         const int64_t P = L.P;
         const int64_t G0 = chunk > 0 ? chunk : std::max<int64_t>(1, std::min<int64_t>(n_models, 4096));
         const int64_t ldw = (P + 3) & ~int64_t(3);   // 16-byte aligned model rows (float4 weight loads)
-        float *W = dalloc<float>((size_t)std::max<int64_t>(G0, 1) * ldw);
-        float *rew = dalloc<float>(std::max<int64_t>(G0, 1));
-        int32_t *len = dalloc<int32_t>(std::max<int64_t>(G0, 1));
-        auto cleanup = [&](snk_env e, snk_replay r) {
-            if (e) snk_env_destroy(e);
-            if (r) snk_replay_destroy(r);
-        };
+        DevBuf<float> W((size_t)std::max<int64_t>(G0, 1) * ldw);
+        DevBuf<float> rew(std::max<int64_t>(G0, 1));
+        DevBuf<int32_t> len(std::max<int64_t>(G0, 1));
         // play_episode(tr.model, 0f0): the current q_net (packed theta) as a one-model batch
         float tr_reward = 0.0f;
         {
-            snk_env e = nullptr;
-            snk_replay r = nullptr;
-            lap_rollout(m, m->theta_q, P, 1, rew, len, &e, &r);
+            EnvHold e;
+            ReplayHold r;
+            lap_rollout(m, m->theta_q, P, 1, rew, len, e, r);
             SNK_HIP(hipMemcpy(&tr_reward, rew, sizeof(float), hipMemcpyDeviceToHost));
-            cleanup(e, r);
         }
         int64_t n_better = 0;
         std::vector<float> hr;
@@ -847,9 +822,9 @@ extern "C" int snk_laplace_sampling(snk_laplace h, snk_dqn m, snk_replay rb, int
         for (int64_t n0 = 0; n0 < n_models; n0 += G0) {
             const int64_t G = std::min(G0, n_models - n0);
             lap_build(h, m, seed, n0, G, W, ldw);
-            snk_env e = nullptr;
-            snk_replay r = nullptr;
-            lap_rollout(m, W, ldw, G, rew, len, &e, &r);
+            EnvHold e;
+            ReplayHold r;
+            lap_rollout(m, W, ldw, G, rew, len, e, r);
             hr.resize(G);
             hl.resize(G);
             SNK_HIP(hipMemcpy(hr.data(), rew, G * sizeof(float), hipMemcpyDeviceToHost));
@@ -865,24 +840,23 @@ extern "C" int snk_laplace_sampling(snk_laplace h, snk_dqn m, snk_replay rb, int
                 }
             }
             if (!slots.empty()) {
+                // store! in (model, step) order: with more transitions than capacity only
+                // the last cap survive, each in the ring slot the sequential stores leave it
+                // in; count still advances by all ns (utils.jl:267-277)
                 const int64_t ns = (int64_t)slots.size();
-                int64_t *sd = dalloc<int64_t>(ns);
+                const int64_t skip = ns > D.cap ? ns - D.cap : 0, nc = ns - skip;
+                DevBuf<int64_t> sd(nc);
                 int64_t dcount = 0;
-                SNK_HIP(hipMemcpyAsync(sd, slots.data(), ns * sizeof(int64_t), hipMemcpyHostToDevice, s));
+                SNK_HIP(hipMemcpyAsync(sd, slots.data() + skip, nc * sizeof(int64_t), hipMemcpyHostToDevice, s));
                 SNK_HIP(hipMemcpyAsync(&dcount, D.count, sizeof(int64_t), hipMemcpyDeviceToHost, s));
                 SNK_HIP(hipStreamSynchronize(s));
-                lap_copy_kernel<<<(unsigned)ns, 256, 0, s>>>(replay_dev(r), D, sd, ns, dcount);
+                lap_copy_kernel<<<(unsigned)nc, 256, 0, s>>>(replay_dev(r.r), D, sd, nc, dcount + skip);
                 launch_check("lap_copy_kernel");
                 lap_count_add_kernel<<<1, 1, 0, s>>>(D.count, ns);
                 launch_check("lap_count_add_kernel");
                 SNK_HIP(hipStreamSynchronize(s));
-                dfree(sd);
             }
-            cleanup(e, r);
         }
-        dfree(W);
-        dfree(rew);
-        dfree(len);
         *tr_reward_out = tr_reward;
         *n_better_out = n_better;
     });

@@ -260,10 +260,8 @@ struct GemmPlan {
 static GemmPlan plan_gemm(int64_t M, int N, int NT, int64_t K, bool allow_z) {
     const int64_t tiles = ceil_div(M, 32) * ceil_div(N, NT * 32);
     // these GEMMs (the B = 64 backward) are latency-bound: many short waves
-    // env overrides for tuning: SNK_GEMM_WAVES (4096), SNK_GEMM_MINK (32); measured flat from 4096/32
-    // to 16384/8 on the B = 64 update
-    static const int64_t target = getenv("SNK_GEMM_WAVES") ? atoll(getenv("SNK_GEMM_WAVES")) : 4096;
-    static const int64_t mink = getenv("SNK_GEMM_MINK") ? atoll(getenv("SNK_GEMM_MINK")) : 32;
+    // (~4096 waves of >= 32 k each; measured flat from 4096/32 to 16384/8 on the B = 64 update)
+    constexpr int64_t target = 4096, mink = 32;
     int kw = 1;
     while (kw < 8 && tiles * kw * 2 <= target && K / (kw * 2) >= mink) kw *= 2;
     int z = 1;
@@ -277,8 +275,7 @@ static GemmPlan plan_gemm(int64_t M, int N, int NT, int64_t K, bool allow_z) {
 // the same with the waves per tile fixed (paired launches need equal block sizes)
 static GemmPlan plan_gemm_kw(int64_t M, int N, int NT, int64_t K, bool allow_z, int kw) {
     const int64_t tiles = ceil_div(M, 32) * ceil_div(N, NT * 32);
-    static const int64_t target = getenv("SNK_KW_WAVES") ? atoll(getenv("SNK_KW_WAVES")) : 4096;
-    static const int64_t mink = getenv("SNK_KW_MINK") ? atoll(getenv("SNK_KW_MINK")) : 32;
+    constexpr int64_t target = 4096, mink = 32;
     int z = 1;
     if (allow_z)
         while (z < 64 && tiles * kw * z * 2 <= target && K / ((int64_t)kw * z * 2) >= mink) z *= 2;
@@ -336,21 +333,9 @@ __global__ __launch_bounds__(NTH) void pair_kernel(J1 j1, J2 j2) {
     else
         j2(unflatten(blockIdx.x - n1, j2.grid));
 }
-template <int NTH, class J>
-__global__ __launch_bounds__(NTH) void job_kernel(J j) {
-    j(unflatten(blockIdx.x, j.grid));
-}
 template <int NTH, class J1, class J2>
 static void pair_launch(const J1 &j1, const J2 &j2, hipStream_t s) {
     const unsigned n1 = j1.grid.x * j1.grid.y * j1.grid.z, n2 = j2.grid.x * j2.grid.y * j2.grid.z;
-    // SNK_UNPAIR=1: the two jobs as separate launches (profiling each half)
-    static const bool unpair = getenv("SNK_UNPAIR") && atoi(getenv("SNK_UNPAIR")) != 0;
-    if (unpair) {
-        job_kernel<NTH><<<n1, NTH, 0, s>>>(j1);
-        job_kernel<NTH><<<n2, NTH, 0, s>>>(j2);
-        launch_check("job_kernel");
-        return;
-    }
     pair_kernel<NTH><<<n1 + n2, NTH, 0, s>>>(j1, j2);
     launch_check("pair_kernel");
 }
@@ -371,24 +356,12 @@ static void gemm(const AL &al, const BL &bl, const EP &ep, int64_t M, int N, int
 // ---------------------------------------------------------------- LDS-staged conv
 static int conv_splits(int64_t M, int nkk) {
     const int64_t wgs = ceil_div(M, 128);
-    // offsets at or below this count run unsplit (no reduce launch); SNK_SPLIT_MIN_KK
-    static const int min_kk = getenv("SNK_SPLIT_MIN_KK") ? atoi(getenv("SNK_SPLIT_MIN_KK")) : 0;
-    if (wgs >= 512 || nkk <= min_kk) return 1;
+    if (wgs >= 512) return 1;
     return (int)std::min<int64_t>(std::min(nkk, 16), ceil_div(512, wgs));
 }
 
-// conv3 data gradients on the bf16x6 split (dz3 and the fp32 weights split in the
-// kernel: 2.7x the exact-fp32 MFMA rate, same error class); SNK_DX_X6=0: fp32 MFMA
-static bool dx_x6() {
-    static const bool on = !getenv("SNK_DX_X6") || atoi(getenv("SNK_DX_X6")) != 0;
-    return on;
-}
-
-// kk splits of the conv3 data gradient (36 offsets): SNK_DX_SPLITS overrides (tuning)
-static int dx_splits(int64_t M) {
-    static const int dxs = getenv("SNK_DX_SPLITS") ? atoi(getenv("SNK_DX_SPLITS")) : 0;
-    return dxs > 0 ? std::min(dxs, 36) : conv_splits(M, 36);
-}
+// kk splits of the conv3 data gradient (36 offsets)
+static int dx_splits(int64_t M) { return conv_splits(M, 36); }
 
 // wb != nullptr: the bf16x6 split-precision kernel on the weight planes wb
 // ng groups (1 or 2) of the same geometry in one launch (grid.z = group);
@@ -419,40 +392,9 @@ static void h3s_launch(const ConvPair &pr, int ng, int splits, hipStream_t s) {
     SNK_CHECK(splits == 1 && lds && S * ho2 == a.M && a.HOUT == HIN - KS + 1 && !a.xb && a.x && a.w &&
                   (ng == 1 || pr.g[1].wmax),
               SNK_ERR_INTERNAL, "h3s conv3 geometry");
-    static size_t attr = 0;   // dynamic bytes only: the kernel's static LDS counts against the 160 KB
-    if (lds > attr) {
-        SNK_HIP(hipFuncSetAttribute((const void *)conv_h3s_kernel<KS, EPI, HIN>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = lds;
-    }
+    // dynamic bytes only: the kernel's static LDS counts against the 160 KB
+    set_lds_limit((const void *)conv_h3s_kernel<KS, EPI, HIN>, lds);
     const dim3 g3((unsigned)ceil_div(S, 4), 1, (unsigned)ng);
-    static const bool dbg = getenv("SNK_H3S_DBG") != nullptr;
-    if (dbg && ng == 1) {   // experiment: per-workgroup phase timestamps to stderr
-        const size_t nd = (size_t)g3.x * 64;
-        uint64_t *d = dalloc<uint64_t>(nd);
-        ConvPair p2 = pr;
-        p2.g[0].dbg = d;
-        conv_h3s_kernel<KS, EPI, HIN><<<g3, 512, lds, s>>>(p2, S);
-        launch_check("conv_h3s_kernel");
-        std::vector<uint64_t> hbuf(nd);
-        SNK_HIP(hipMemcpyAsync(hbuf.data(), d, nd * 8, hipMemcpyDeviceToHost, s));
-        SNK_HIP(hipStreamSynchronize(s));
-        dfree(d);
-        double ph[5] = {0, 0, 0, 0, 0};
-        uint64_t rmin = ~0ull, rmax = 0;
-        int n = 0;
-        for (size_t b = 0; b < g3.x; ++b)
-            for (int w = 0; w < 8; ++w) {
-                const uint64_t *q = &hbuf[(b * 8 + w) * 8];
-                for (int k = 0; k < 5; ++k) ph[k] += (double)(q[k + 1] - q[k]);
-                rmin = std::min(rmin, q[6]); rmax = std::max(rmax, q[7]);
-                ++n;
-            }
-        fprintf(stderr, "h3s dbg: %u WGs, per-wave cycles: A loads %.0f | reduce+barrier %.0f | split+write "
-                "%.0f | loop %.0f | epilogue %.0f; wall %.1f us\n", g3.x, ph[0] / n, ph[1] / n, ph[2] / n,
-                ph[3] / n, ph[4] / n, (double)(rmax - rmin) / 100.0);
-        return;
-    }
     conv_h3s_kernel<KS, EPI, HIN><<<g3, 512, lds, s>>>(pr, S);
     launch_check("conv_h3s_kernel");
 }
@@ -476,11 +418,11 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
         }
     }
     if constexpr (MODE == MODE_DX) {
-        if (dx_x6()) {   // bf16x6, dz and the fp32 weights split in the kernel
-            conv_x6_split_kernel<CK, CN, KS, PAD, MODE, EPI><<<grid, 256, 0, s>>>(pr);
-            launch_check("conv_x6_split_kernel");
-            return;
-        }
+        // conv3 data gradients on the bf16x6 split (dz3 and the fp32 weights split in
+        // the kernel: 2.7x the exact-fp32 MFMA rate, same error class)
+        conv_x6_split_kernel<CK, CN, KS, PAD, MODE, EPI><<<grid, 256, 0, s>>>(pr);
+        launch_check("conv_x6_split_kernel");
+        return;
     }
     if constexpr (MODE != MODE_DX) {
         if (pr.wb[0]) {
@@ -488,51 +430,21 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
                 if (a.xb) {   // pre-split input, 32-channel chunks: the 16x16x32 layouts
                     if constexpr (CN == 64 && PAD == 0 && CK == 32 && KS == 6 && EPI == EPI_BIAS_RELU) {
                         // large batches: four samples' planes resident in LDS per workgroup
+                        // SNK_X6S=0 (tests): x6m16 instead, the same sums in the same order
                         static const bool x6s = !getenv("SNK_X6S") || atoi(getenv("SNK_X6S")) != 0;
-                        static const int smin = getenv("SNK_X6S_MIN") ? atoi(getenv("SNK_X6S_MIN")) : 1024;
+                        constexpr int smin = 1024;
                         const int ho2 = a.HOUT * a.HOUT;
                         const int S = a.M / ho2;
                         const size_t lds = conv_x6s_lds(a.HIN);
                         if (x6s && splits == 1 && lds && S >= smin && S * ho2 == a.M && a.HOUT == a.HIN - 5) {
-                            static bool attr = false;
-                            if (!attr) {
-                                SNK_HIP(hipFuncSetAttribute((const void *)conv_x6s_kernel<KS, EPI>,
-                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-                                attr = true;
-                            }
+                            set_lds_limit((const void *)conv_x6s_kernel<KS, EPI>, lds);
                             const dim3 g3((unsigned)ceil_div(S, 4), 1, (unsigned)ng);
                             conv_x6s_kernel<KS, EPI><<<g3, 512, lds, s>>>(pr, S);
                             launch_check("conv_x6s_kernel");
                             return;
                         }
                     }
-                    if constexpr (CN == 64 && PAD == 0) {
-                        // whole input of the workgroup resident in LDS when it fits
-                        const int ho2 = a.HOUT * a.HOUT;
-                        const int nsmax = ceil_div(127, ho2) + 1;
-                        const size_t xs = (size_t)a.HIN * (a.HIN * (3 * CK + 16) + 80);   // conv_x6a A image
-                        const size_t lds = ((nsmax * xs + 7) & ~size_t(7)) * 2 + (3 * CN * (CK + 16) + 8) * 2;
-                        // measured slower than x6m16 (one workgroup per CU): opt-in
-                        static const bool x6a = getenv("SNK_X6A") != nullptr;
-                        if (lds <= 160 * 1024 && x6a) {
-                            static bool attr = false;
-                            if (!attr) {
-                                SNK_HIP(hipFuncSetAttribute((const void *)conv_x6a_kernel<CK, CN, KS, PAD, EPI>,
-                                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                                attr = true;
-                            }
-                            conv_x6a_kernel<CK, CN, KS, PAD, EPI><<<grid, 512, lds, s>>>(pr, nsmax);
-                            launch_check("conv_x6a_kernel");
-                            return;
-                        }
-                    }
-                    static const int rows = getenv("SNK_M16_ROWS") ? atoi(getenv("SNK_M16_ROWS")) : 128;
-                    if (rows == 256) {
-                        dim3 g2((unsigned)ceil_div(a.M, 256), grid.y, grid.z);
-                        conv_x6m16_kernel<CK, CN, KS, PAD, EPI, 8><<<g2, 512, 0, s>>>(pr);
-                    } else {
-                        conv_x6m16_kernel<CK, CN, KS, PAD, EPI, 4><<<grid, 256, 0, s>>>(pr);
-                    }
+                    conv_x6m16_kernel<CK, CN, KS, PAD, EPI, 4><<<grid, 256, 0, s>>>(pr);
                     launch_check("conv_x6m16_kernel");
                     return;
                 }
@@ -770,152 +682,6 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
             __syncthreads();
         }
     }
-}
-
-// ---------------------------------------------------------------- conv1 + conv2 fused (x6)
-// One workgroup = 128 conv2 output rows (positions) of at most 2 samples. It
-// computes conv1 for those samples straight into LDS as bf16 split planes
-// inside a zero border ((bs+2)^2 positions, 112-byte rows), then runs conv2's
-// 9 kernel offsets on 32x32x16 bf16 MFMA (6 products per offset, as
-// conv_x6_kernel) with every operand in LDS: no barrier inside the offset
-// loop, no a1 round trip through HBM/L2. Outputs as conv_fwd: a2 (fp32,
-// training) and/or its planes a2b; a1 (fp32) too when training needs it.
-// LDS: conv1 weights, boards (floats, bordered), a1 planes, all conv2 planes.
-struct Conv12Args {
-    BoardSrc src;
-    const float *w1, *b1;        // conv1 packed weights / bias
-    const uint16_t *wb2;         // conv2 weight planes [9][3][32][16]
-    const float *b2;
-    float *a1;                   // optional fp32 a1 [S*bs*bs][16]
-    float *a2;                   // optional fp32 a2 [S*bs*bs][32]
-    uint16_t *a2b;               // optional planes [S*bs*bs][3][32]
-};
-struct Conv12Pair {
-    Conv12Args g[2];
-};
-template <int C>
-__global__ __launch_bounds__(256) void conv12_x6_kernel(Conv12Pair cp, int64_t S, int bs, int nsmax) {
-    constexpr int A1ST = 56;   // bf16 per bordered position: 3 planes x 16 + 8 pad
-    const Conv12Args &ca = cp.g[blockIdx.z];
-    extern __shared__ __attribute__((aligned(16))) float sm12[];
-    const int bp = bs + 2, bp2 = bp * bp, nc = bs * bs;
-    float *sw = sm12;                                   // [9C*16 + 16]
-    float *sx = sw + ((9 * C * 16 + 16 + 3) & ~3);      // [nsmax][C][bp2]
-    uint16_t *A1 = reinterpret_cast<uint16_t *>(sx + ((nsmax * C * bp2 + 3) & ~3));   // [nsmax][bp2][A1ST]
-    uint16_t *Bw = A1 + ((nsmax * bp2 * A1ST + 7) & ~7);                              // [9][3][32][16]
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t M = S * nc;
-    const int64_t m0 = (int64_t)blockIdx.x * 128;
-    const int64_t s_lo = m0 / nc;
-    const int64_t s_hi = (min(M, m0 + 128) - 1) / nc;
-    const int ns = (int)(s_hi - s_lo + 1);
-    // ---- stage: conv1 weights, zeroed board borders and a1 image, conv2 planes, boards
-    for (int e = tid; e < 9 * C * 16; e += 256) sw[e] = ca.w1[e];
-    if (tid < 16) sw[9 * C * 16 + tid] = ca.b1[tid];
-    for (int e = tid; e < nsmax * C * bp2; e += 256) sx[e] = 0.0f;
-    {
-        u32x4 *a = reinterpret_cast<u32x4 *>(A1);
-        const u32x4 z = {0u, 0u, 0u, 0u};
-        for (int e = tid; e < nsmax * bp2 * A1ST / 8; e += 256) a[e] = z;
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(ca.wb2);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(Bw);
-        for (int e = tid; e < 9 * 3 * 32 * 16 / 8; e += 256) dst[e] = src[e];
-    }
-    __syncthreads();
-    for (int e = tid; e < ns * C * nc; e += 256) {
-        const int sc = e / nc, cell = e - sc * nc;
-        const int sl = sc / C, c = sc - sl * C;
-        const int jj = cell / bs, ii = cell - jj * bs;
-        const int8_t *pl = ca.src.plane(s_lo + sl, c);
-        const float v = pl ? (float)pl[cell] : ca.src.fbase[((s_lo + sl) * C + c) * nc + cell];
-        sx[sc * bp2 + (ii + 1) + (jj + 1) * bp] = v;
-    }
-    __syncthreads();
-    // ---- conv1 for every position of the staged samples -> a1 planes (bordered)
-    for (int q = tid; q < ns * nc; q += 256) {
-        const int sl = q / nc, p = q - sl * nc;
-        const int j = p / bs, i = p - j * bs;
-        float acc[16];
-#pragma unroll
-        for (int co = 0; co < 16; ++co) acc[co] = sw[9 * C * 16 + co];
-#pragma unroll
-        for (int kk = 0; kk < 9; ++kk) {
-            const int du = kk % 3, dv = kk / 3;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const float v = sx[(sl * C + c) * bp2 + (i + du) + (j + dv) * bp];
-#pragma unroll
-                for (int co = 0; co < 16; ++co) acc[co] = __builtin_fmaf(v, sw[(kk * C + c) * 16 + co], acc[co]);
-            }
-        }
-#pragma unroll
-        for (int co = 0; co < 16; ++co) acc[co] = fmaxf(acc[co], 0.f);
-        if (ca.a1) {
-            float4 *o = reinterpret_cast<float4 *>(ca.a1 + ((s_lo + sl) * nc + p) * 16);
-#pragma unroll
-            for (int v = 0; v < 4; ++v) o[v] = make_float4(acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]);
-        }
-        u32x4 *o = reinterpret_cast<u32x4 *>(A1 + (sl * bp2 + (i + 1) + (j + 1) * bp) * A1ST);
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const Split3 sp = split3(f32x4{acc[8 * half], acc[8 * half + 1], acc[8 * half + 2], acc[8 * half + 3]},
-                                     f32x4{acc[8 * half + 4], acc[8 * half + 5], acc[8 * half + 6], acc[8 * half + 7]});
-            o[0 + half] = sp.h;   // plane p at bf16 16p, channels 8*half..
-            o[2 + half] = sp.m;
-            o[4 + half] = sp.l;
-        }
-    }
-    __syncthreads();
-    // ---- conv2: wave = 32 rows x 32 columns, 9 offsets x 6 products
-    const int r = lane & 31, h = lane >> 5;
-    const int64_t m = m0 + wave * 32 + r;
-    const int64_t mm = m < M ? m : M - 1;
-    const int64_t sidx = mm / nc;
-    const int p = (int)(mm - sidx * nc);
-    const int j = p / bs, i = p - j * bs;
-    const int rowb = (int)(sidx - s_lo) * bp2 + i + j * bp;   // bordered position at offset (0, 0)
-    f32x16 acc;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
-#pragma unroll
-    for (int kk = 0; kk < 9; ++kk) {
-        const int du = kk % 3, dv = kk / 3;
-        const uint16_t *pa = A1 + (rowb + du + dv * bp) * A1ST + 8 * h;
-        const uint16_t *pb = Bw + kk * 3 * 512 + r * 16 + 8 * h;
-        const bf16x8 ah = as_bf(*reinterpret_cast<const u32x4 *>(pa));
-        const bf16x8 am = as_bf(*reinterpret_cast<const u32x4 *>(pa + 16));
-        const bf16x8 al = as_bf(*reinterpret_cast<const u32x4 *>(pa + 32));
-        const bf16x8 bh = as_bf(*reinterpret_cast<const u32x4 *>(pb));
-        const bf16x8 bm = as_bf(*reinterpret_cast<const u32x4 *>(pb + 512));
-        const bf16x8 bl = as_bf(*reinterpret_cast<const u32x4 *>(pb + 1024));
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
-    }
-    const float b = ca.b2[r];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-        const int64_t row = m0 + wave * 32 + acc_row(g, lane);
-        if (row >= M) continue;
-        float v = acc[g] + b;
-        v = v > 0.0f ? v : 0.0f;
-        if (ca.a2) ca.a2[row * 32 + r] = v;
-        if (ca.a2b) {
-            uint16_t *pb2 = ca.a2b + row * 96 + r;
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) pb2[pl * 32] = split_part(v, pl);
-        }
-    }
-}
-
-static int conv12_nsmax(int bs) { return ceil_div(127, bs * bs) + 1; }
-static size_t conv12_lds(int C, int bs) {
-    const int bp2 = (bs + 2) * (bs + 2), ns = conv12_nsmax(bs);
-    return (((9 * C * 16 + 16 + 3) & ~3) + ((ns * C * bp2 + 3) & ~3)) * 4 + ((ns * bp2 * 56 + 7) & ~7) * 2 +
-           9 * 3 * 32 * 16 * 2;
 }
 
 // ---------------------------------------------------------------- heads
@@ -1157,7 +923,9 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     const int64_t slab = std::max({need_slab, w.slab_floats, (int64_t)d1_split(L, cap, kc) * cap * 64});
     const bool tr = train || w.has_train;
     const int64_t cslab = std::max({need_cslab, w.cslab_floats, conv_slab_floats(L, cap, tr)});
+    const int64_t gen = w.gen + 1;
     qwork_free(w);
+    w.gen = gen;
     w.cap = cap;
     w.slab_floats = slab;
     w.cslab_floats = cslab;
@@ -1189,11 +957,10 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
 // conv3 of this forward on the fp16 h3 kernel (snk_conv_h3.hpp): split-precision
 // (x6) nets, large batches, one unsplit launch. SNK_H3S=0: the bf16 x6 kernels.
 static bool h3s_ok(const QLayout &L, const FwdNet *net, int ng, int64_t S) {
-    static const bool on = !getenv("SNK_H3S") || atoi(getenv("SNK_H3S")) != 0;
-    static const int smin = getenv("SNK_X6S_MIN") ? atoi(getenv("SNK_X6S_MIN")) : 1024;
+    static const bool on = !getenv("SNK_H3S") || atoi(getenv("SNK_H3S")) != 0;   // tests: x6 comparisons
+    constexpr int smin = 1024;
     for (int g = 0; g < ng; ++g)
         if (!net[g].wtb) return false;
-    if (getenv("SNK_CONV12")) return false;   // the fused conv1+conv2 kernel writes a2 as x6 planes only
     return on && S >= smin && L.bs >= 8 && L.bs <= 13 && conv_h3s_lds(L.bs) && L.Wo == L.bs - 5 &&
            conv_splits(S * L.Wo * L.Wo * ng, 36) == 1;
 }
@@ -1201,66 +968,19 @@ static bool h3s_ok(const QLayout &L, const FwdNet *net, int ng, int64_t S) {
 template <int BS>
 static void h3c2_launch_bs(const float *a1, const float *wimg, const float *b2, float *a2, int64_t S, hipStream_t s) {
     const size_t lds = conv_h3c2_lds<BS>();
-    static size_t attr = 0;
-    if (lds > attr) {
-        SNK_HIP(hipFuncSetAttribute((const void *)conv_h3c2_kernel<BS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds));
-        attr = lds;
-    }
+    set_lds_limit((const void *)conv_h3c2_kernel<BS>, lds);
     conv_h3c2_kernel<BS><<<(unsigned)ceil_div(S, 2), 256, lds, s>>>(a1, wimg, b2, a2, (int)S);
     launch_check("conv_h3c2_kernel");
 }
 
-template <int HIN, int NBUF>
-static void h3f_launch_nb(const H3FArgs &fa, int64_t S, hipStream_t s) {
-    constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, NBUF>();
-    static_assert(lds <= 160 * 1024, "conv_h3f LDS");
-    static bool attr = false;
-    if (!attr) {
-        SNK_HIP(hipFuncSetAttribute((const void *)conv_h3f_kernel<HIN, NBUF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds));
-        attr = true;
-    }
-    const unsigned grid = (unsigned)ceil_div(S, 4);
-    static const bool dbg = getenv("SNK_H3F_DBG") != nullptr;
-    if (dbg) {   // experiment: per-wave phase clocks to stderr
-        const size_t nd = (size_t)grid * 64;
-        uint64_t *d = dalloc<uint64_t>(nd);
-        H3FArgs f2 = fa;
-        f2.dbg = d;
-        conv_h3f_kernel<HIN, NBUF><<<grid, 512, lds, s>>>(f2, (int)S);
-        launch_check("conv_h3f_kernel");
-        std::vector<uint64_t> hbuf(nd);
-        SNK_HIP(hipMemcpyAsync(hbuf.data(), d, nd * 8, hipMemcpyDeviceToHost, s));
-        SNK_HIP(hipStreamSynchronize(s));
-        dfree(d);
-        double ph[5] = {0, 0, 0, 0, 0};
-        uint64_t rmin = ~0ull, rmax = 0;
-        for (size_t b = 0; b < grid; ++b)
-            for (int w = 0; w < 8; ++w) {
-                const uint64_t *q = &hbuf[(b * 8 + w) * 8];
-                for (int k = 0; k < 5; ++k) ph[k] += (double)(q[k + 1] - q[k]);
-                rmin = std::min(rmin, q[6]);
-                rmax = std::max(rmax, q[7]);
-            }
-        const double n = grid * 8.0;
-        fprintf(stderr, "h3f dbg: %u WGs, per-wave cycles: stage %.0f | conv2 %.0f | A image %.0f | conv3 %.0f | "
-                "epilogue %.0f; wall %.1f us\n", grid, ph[0] / n, ph[1] / n, ph[2] / n, ph[3] / n, ph[4] / n,
-                (double)(rmax - rmin) / 100.0);
-        return;
-    }
-    conv_h3f_kernel<HIN, NBUF><<<grid, 512, lds, s>>>(fa, (int)S);
-    launch_check("conv_h3f_kernel");
-}
-
-// conv3 B staging: 4 LDS buffers, one barrier per offset pair (SNK_H3F_NBUF=2: one per offset)
+// conv3 B staging: 4 LDS buffers, one barrier per offset pair
 template <int HIN>
 static void h3f_launch_bs(const H3FArgs &fa, int64_t S, hipStream_t s) {
-    static const bool nb2 = getenv("SNK_H3F_NBUF") && atoi(getenv("SNK_H3F_NBUF")) == 2;
-    if (nb2)
-        h3f_launch_nb<HIN, 2>(fa, S, s);
-    else
-        h3f_launch_nb<HIN, 4>(fa, S, s);
+    constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, 4>();
+    static_assert(lds <= 160 * 1024, "conv_h3f LDS");
+    set_lds_limit((const void *)conv_h3f_kernel<HIN, 4>, lds);
+    conv_h3f_kernel<HIN, 4><<<(unsigned)ceil_div(S, 4), 512, lds, s>>>(fa, (int)S);
+    launch_check("conv_h3f_kernel");
 }
 
 static void conv_h3f_launch(int bs, const H3FArgs &fa, int64_t S, hipStream_t s) {
@@ -1295,15 +1015,11 @@ static bool h3c2_on() {
     static const bool on = !getenv("SNK_H3C2") || atoi(getenv("SNK_H3C2")) != 0;
     return on;
 }
-static bool h3f_on() {
-    static const bool on = !getenv("SNK_H3F") || atoi(getenv("SNK_H3F")) != 0;
-    return on;
-}
 
 // whether an act forward (no training work) of S samples runs conv2 + conv3 as conv_h3f_kernel
 bool qnet_fused23(const QLayout &L, const float *th, const float *wt, const uint16_t *wtb, int64_t S, QWork &w) {
     const FwdNet net{th, wt, wtb, BoardSrc{}, &w};
-    return h3s_ok(L, &net, 1, S) && h3c2_on() && h3f_on() && !w.has_train;
+    return h3s_ok(L, &net, 1, S) && h3c2_on() && !w.has_train;
 }
 
 static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi) {
@@ -1312,41 +1028,10 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
     // h3 also for conv2 (conv_h3c2_kernel): conv1 then writes fp32 a1 only. SNK_H3C2=0: x6 conv2.
     const bool h3c2 = h3 && h3c2_on();
     const int64_t n3 = 36LL * 32 * 64;   // conv3 weight image floats
-    // x6: conv1 + conv2 fused into one kernel (layer 0; layer 1 is then empty)
-    // measured slower than conv1 + conv2 (per-workgroup staging dominates): opt-in
-    static const bool use12 = getenv("SNK_CONV12") != nullptr;
-    const bool fused12 = net[0].wtb && use12 && conv12_lds(L.C, bs) <= 160 * 1024;
-    if (fused12 && lo <= 0 && hi >= 0) {
-        const size_t lds = conv12_lds(L.C, bs);
-        Conv12Pair cp{};
-        for (int g = 0; g < 2; ++g) {
-            const FwdNet &n = net[g < ng ? g : 0];
-            cp.g[g] = Conv12Args{n.src, n.th + L.off_w1, n.th + L.off_b1, n.wtb + 3 * L.off_t2, n.th + L.off_b2,
-                                 n.w->has_train ? n.w->a1 : nullptr, n.w->has_train ? n.w->a2 : nullptr, n.w->a2b};
-        }
-        const dim3 grid((unsigned)ceil_div(S * nc, 128), 1, (unsigned)ng);
-        static size_t attr = 0;
-        if (lds > attr) {
-            SNK_HIP(hipFuncSetAttribute((const void *)conv12_x6_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds));
-            SNK_HIP(hipFuncSetAttribute((const void *)conv12_x6_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds));
-            attr = lds;
-        }
-        if (L.C == 1)
-            conv12_x6_kernel<1><<<grid, 256, lds, s>>>(cp, S, bs, conv12_nsmax(bs));
-        else
-            conv12_x6_kernel<2><<<grid, 256, lds, s>>>(cp, S, bs, conv12_nsmax(bs));
-        launch_check("conv12_x6_kernel");
-    }
-    if (fused12) {
-        lo = std::max(lo, 2);
-        for (int g = 0; g < ng; ++g) net[g].w->x0_valid = 0;
-    }
     if (lo <= 0 && hi >= 0) {
         // samples per workgroup: S*ng/1024 capped at 8 (4 at the 4096-env act forward: measured
         // 20 us against 25 at 8; 1 sample per workgroup costs the per-workgroup weight/board latency)
-        static const int c1div = getenv("SNK_C1_DIV") ? atoi(getenv("SNK_C1_DIV")) : 1024;
+        constexpr int c1div = 1024;
         const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S * ng / c1div));
         const dim3 grid((unsigned)ceil_div(S, ns), (unsigned)ng);
         const size_t lds = (size_t)(9 * L.C * 16 + 16 + ((ns * L.C * (bs + 2) * (bs + 2) + 3) & ~3) + 256 * 24) * sizeof(float);
@@ -1371,8 +1056,8 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         }
     }
     FwdIO io[2];
-    // conv2 + conv3 fused (conv_h3f_kernel) when this call runs both. SNK_H3F=0: separate kernels
-    bool h3f = h3c2 && h3f_on() && lo <= 1 && hi >= 2;
+    // conv2 + conv3 fused (conv_h3f_kernel) when this call runs both
+    bool h3f = h3c2 && lo <= 1 && hi >= 2;
     for (int g = 0; g < ng; ++g) h3f = h3f && !net[g].w->has_train;   // a backward needs a2 in memory
     if (h3f) {
         for (int g = 0; g < ng; ++g) {
@@ -1385,7 +1070,7 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
                 w.wmax_img = n.wt + L.off_t3;
             }
             const H3FArgs fa{w.a1, n.wt + L.off_t2, n.th + L.off_b2, n.wt + L.off_t3, w.wmax_part, w.wmax_n,
-                             n.th + L.off_b3, w.a3, nullptr};
+                             n.th + L.off_b3, w.a3};
             conv_h3f_launch(L.bs, fa, S, s);
         }
         lo = std::max(lo, 3);
@@ -1489,20 +1174,18 @@ struct BwdPlan {
 // waves per tile fixed so that the layer pairs (d1 wgrad | d1x: 2, c3 wgrad |
 // conv3 data grad: 4 = the conv kernel's 256 threads, c2 wgrad | c2x: 8) launch together
 // conv3's backward on conv3_bwd_kernel (snk_bwd3.hpp): both halves' LDS within a CU's
-// 160 KB (boards up to 13x13 at two samples per weight-gradient chunk). SNK_C3BWD=0: the
-// generic pair (gemm_body weight gradient | implicit-GEMM data gradient + reduce).
+// 160 KB (boards up to 13x13 at two samples per weight-gradient chunk). Larger boards:
+// the generic pair (gemm_body weight gradient | implicit-GEMM data gradient + reduce).
 constexpr int C3_NSC = 2;
 static bool c3bwd_ok(const QLayout &L, int64_t S) {
-    static const bool on = !getenv("SNK_C3BWD") || atoi(getenv("SNK_C3BWD")) != 0;
     const size_t lim = 160 * 1024 / sizeof(float);
-    return on && S <= (1 << 24) && L.Wo >= 3 && L.Wo <= 8 && (size_t)c3_dw_lds_floats(L.bs, L.Wo, C3_NSC) <= lim &&
+    return S <= (1 << 24) && L.Wo >= 3 && L.Wo <= 8 && (size_t)c3_dw_lds_floats(L.bs, L.Wo, C3_NSC) <= lim &&
            (size_t)c3_dx_lds_floats(L.Wo) <= lim;
 }
 
-// conv2's backward on conv2_bwd_kernel (snk_bwd3.hpp); SNK_C2BWD=0: the generic pair
+// conv2's backward on conv2_bwd_kernel (snk_bwd3.hpp); larger boards: the generic pair
 static bool c2bwd_ok(const QLayout &L, int64_t S) {
-    static const bool on = !getenv("SNK_C2BWD") || atoi(getenv("SNK_C2BWD")) != 0;
-    return on && S <= (1 << 20) && (size_t)c2_bwd_lds_floats(L.bs) * sizeof(float) <= 160 * 1024;
+    return S <= (1 << 20) && (size_t)c2_bwd_lds_floats(L.bs) * sizeof(float) <= 160 * 1024;
 }
 
 static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
@@ -1577,9 +1260,6 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
     const SlabRegions sr = slab_regions(L, S);
     SNK_CHECK(slab_cap >= sr.total, SNK_ERR_INTERNAL, "backward slab too small");
     const int bs = L.bs, nc = L.ncell, no = L.Wo * L.Wo;
-    Fork serial;
-    serial.main = s;
-    Fork &F = o.fork ? *o.fork : serial;
     GradSlabs *D = o.defer;
     if (D) {
         *D = GradSlabs{};
@@ -1587,7 +1267,7 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         D->h1 = w.h1;
         D->S = S;
     }
-    if (!F.on_side(FK_WGRAD)) {
+    {
         // each layer's weight gradient and data gradient in ONE launch
         auto dst = [&](int k, const GemmPlan &g, int64_t off, int64_t n, float *sl) -> float * {
             if (g.z == 1) return grad + off;
@@ -1619,53 +1299,10 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         // conv3: dW over rows (s, pout) | dX onto the bs x bs x 32 input (relu mask on a2)
         if (c3bwd_ok(L, S)) {
             float *c3d = dst(1, p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
-            Conv3BwdArgs ca{w.a2, w.dz3, th + L.off_w3, c3d, w.dz2, (int)S, bs, L.Wo, C3_NSC, p.c3.z, p.c3.z * 9, 0, nullptr};
+            const Conv3BwdArgs ca{w.a2, w.dz3, th + L.off_w3, c3d, w.dz2, (int)S, bs, L.Wo, C3_NSC, p.c3.z, p.c3.z * 9};
             const size_t lds = (size_t)std::max(c3_dw_lds_floats(bs, L.Wo, C3_NSC), c3_dx_lds_floats(L.Wo)) * 4;
-            static size_t attr = 0;
-            if (lds > attr) {
-                SNK_HIP(hipFuncSetAttribute((const void *)conv3_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)lds));
-                attr = lds;
-            }
-            const unsigned nb = (unsigned)(ca.nW + S * (32 / C3_CG));
-            static const bool halves = getenv("SNK_UNPAIR") && atoi(getenv("SNK_UNPAIR")) != 0;
-            static bool dbg = getenv("SNK_C3_DBG") != nullptr;
-            if (dbg) {   // experiment (once): per-block phase clocks of each half, to stderr
-                dbg = false;
-                uint64_t *d = dalloc<uint64_t>((size_t)nb * 8);
-                ca.dbg = d;
-                conv3_bwd_kernel<<<(unsigned)ca.nW, 256, lds, s>>>(ca);
-                ca.boff = ca.nW;
-                conv3_bwd_kernel<<<nb - (unsigned)ca.nW, 256, lds, s>>>(ca);
-                launch_check("conv3_bwd_kernel");
-                std::vector<uint64_t> hb((size_t)nb * 8);
-                SNK_HIP(hipMemcpyAsync(hb.data(), d, hb.size() * 8, hipMemcpyDeviceToHost, s));
-                SNK_HIP(hipStreamSynchronize(s));
-                dfree(d);
-                for (int half = 0; half < 2; ++half) {
-                    const unsigned b0 = half ? (unsigned)ca.nW : 0, b1 = half ? nb : (unsigned)ca.nW;
-                    double ph[3] = {0, 0, 0};
-                    uint64_t w0 = ~0ull, w1 = 0, s1 = 0;
-                    for (unsigned b = b0; b < b1; ++b) {
-                        const uint64_t *q = &hb[(size_t)b * 8];
-                        for (int k = 0; k < 3; ++k) ph[k] += (double)(q[k + 1] - q[k]);
-                        w0 = std::min(w0, q[4]); w1 = std::max(w1, q[5]); s1 = std::max(s1, q[4]);
-                    }
-                    const double n = b1 - b0;
-                    fprintf(stderr, "c3bwd dbg %s: %u blocks, cycles: stage %.0f | compute %.0f | epilogue %.0f; "
-                            "wall %.2f us, last block start %.2f us\n", half ? "dX" : "dW", b1 - b0, ph[0] / n,
-                            ph[1] / n, ph[2] / n, (double)(w1 - w0) / 100.0, (double)(s1 - w0) / 100.0);
-                }
-                ca.dbg = nullptr;
-                ca.boff = 0;
-            }
-            if (halves) {   // profiling: weight-gradient blocks, then data-gradient blocks
-                conv3_bwd_kernel<<<(unsigned)ca.nW, 256, lds, s>>>(ca);
-                ca.boff = ca.nW;
-                conv3_bwd_kernel<<<nb - (unsigned)ca.nW, 256, lds, s>>>(ca);
-            } else {
-                conv3_bwd_kernel<<<nb, 256, lds, s>>>(ca);
-            }
+            set_lds_limit((const void *)conv3_bwd_kernel, lds);
+            conv3_bwd_kernel<<<(unsigned)(ca.nW + S * (32 / C3_CG)), 256, lds, s>>>(ca);
             launch_check("conv3_bwd_kernel");
             fin(p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
         } else {
@@ -1677,28 +1314,16 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             a.nkk = 36;
             int sp = dx_splits(S * nc);
             const dim3 cg((unsigned)ceil_div(S * nc, 128), 1, 1);
-            const bool dx6 = dx_x6();
             if (sp == 1) {
                 a.out = w.dz2;
-                if (dx6) {
-                    ConvX6Job<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK, false, true> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
-                    pair_launch<256>(wj, cj, s);
-                } else {
-                    ConvJob<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
-                    pair_launch<256>(wj, cj, s);
-                }
+                ConvX6Job<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK, false, true> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
+                pair_launch<256>(wj, cj, s);
             } else {
                 a.out = w.cslab;
                 SNK_CHECK((int64_t)sp * S * nc * 32 <= w.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
-                if (dx6) {
-                    ConvX6Job<64, 32, 6, 0, MODE_DX, EPI_SLAB, false, true> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
-                    cj.grid.y = (unsigned)sp;
-                    pair_launch<256>(wj, cj, s);
-                } else {
-                    ConvJob<64, 32, 6, 0, MODE_DX, EPI_SLAB> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
-                    cj.grid.y = (unsigned)sp;
-                    pair_launch<256>(wj, cj, s);
-                }
+                ConvX6Job<64, 32, 6, 0, MODE_DX, EPI_SLAB, false, true> cj{make_conv_pair(&a, 1, sp, nullptr), cg};
+                cj.grid.y = (unsigned)sp;
+                pair_launch<256>(wj, cj, s);
                 const ReduceArgs ra{w.cslab, nullptr, w.a2, w.dz2, nullptr};
                 conv_reduce_launch(&ra, 1, sp, S * nc * 32, 32, s);
             }
@@ -1709,12 +1334,7 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         if (c2bwd_ok(L, S)) {
             const Conv2BwdArgs ca{w.a1, w.dz2, th + L.off_w2, c2d, w.dzc1, (int)S, bs};
             const size_t lds = (size_t)c2_bwd_lds_floats(bs) * sizeof(float);
-            static size_t attr = 0;
-            if (lds > attr) {
-                SNK_HIP(hipFuncSetAttribute((const void *)conv2_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)lds));
-                attr = lds;
-            }
+            set_lds_limit((const void *)conv2_bwd_kernel, lds);
             conv2_bwd_kernel<<<(unsigned)((1 + C2_NXB) * S), 256, lds, s>>>(ca);
             launch_check("conv2_bwd_kernel");
         } else
@@ -1738,83 +1358,7 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         gemm<1>(ABoardDw{xs, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
                 EpSlab{c1d, (int)Mc1, 16}, Mc1, 16, S * nc, p.c1, s);
         fin(p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
-        return;
     }
-    // a weight gradient: straight into grad, through slabs + reduce, or left
-    // as slabs for grad_update_launch (section k of D)
-    auto wg = [&](int k, auto launch, const GemmPlan &g, int64_t off, int64_t n, float *sl, hipStream_t q) {
-        if (g.z == 1) {
-            launch(grad + off, q);
-        } else {
-            launch(sl, q);
-            if (D) {
-                D->slab[k] = sl; D->z[k] = g.z; D->off[k] = off; D->n[k] = n;
-            } else {
-                reduce_into(sl, g.z, n, grad + off, q);
-            }
-        }
-    };
-    // critical path: dz1 -> dz3 -> dz2 -> dzc1 -> conv1 weights; each weight
-    // gradient forks off as soon as its dz exists
-    if (!o.dz1_ready) {
-        head_bwd_kernel<<<ceil_div(S, 4), 256, 0, s>>>(w.dq, w.h1, th, L, S, w.dz1);
-        launch_check("head_bwd_kernel");
-    }
-    {
-        hipStream_t q = F.fork(0, FK_WGRAD);
-        if (!D) {
-            d2_grad_kernel<<<1, 256, 0, q>>>(w.dq, w.h1, S, L, grad);
-            launch_check("d2_grad_kernel");
-        }
-        const int64_t M = L.K1 + 1;
-        wg(0, [&](float *dst, hipStream_t qq) {
-            gemm<2>(ADenseDw{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, EpSlab{dst, (int)M, 64}, M, 64, S, p.d1, qq);
-        }, p.d1, L.off_d1w, M * 64, slab + sr.d1, q);
-    }
-    gemm<2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + L.off_d1w, 64, L.K1, 64}, EpReluMask{w.dz3, w.a3, (int)S, L.K1},
-            S, L.K1, 64, p.d1x, s);
-    {
-        hipStream_t q = F.fork(1, FK_WGRAD);
-        wg(1, [&](float *dst, hipStream_t qq) {
-            gemm<2>(AConvDw<32, 6, 0>{w.a2, bs, L.Wo, S * no, FastDiv(no), FastDiv(L.Wo)}, BRows{w.dz3, S * no, 64},
-                    EpSlab{dst, 1153, 64}, 1153, 64, S * no, p.c3, qq);
-        }, p.c3, L.off_w3, 1153 * 64, slab + sr.c3, q);
-    }
-    {
-        ConvArgs a{};
-        a.x = w.dz3; a.w = th + L.off_w3; a.act = w.a2; a.M = (int)(S * nc); a.HIN = L.Wo; a.HOUT = bs; a.nkk = 36;
-        const int sp = dx_splits(S * nc);
-        if (sp == 1) {
-            a.out = w.dz2;
-            conv_launch<64, 32, 6, 0, MODE_DX, EPI_RELU_MASK>(a, 1, s);
-        } else {
-            a.out = w.cslab;
-            SNK_CHECK((int64_t)sp * S * nc * 32 <= w.cslab_floats, SNK_ERR_INTERNAL, "conv slab too small");
-            conv_launch<64, 32, 6, 0, MODE_DX, EPI_SLAB>(a, sp, s);
-            const int used = ceil_div(36, ceil_div(36, sp));
-            const ReduceArgs ra{w.cslab, nullptr, w.a2, w.dz2, nullptr};
-            conv_reduce_launch(&ra, 1, used, S * nc * 32, 32, s);
-        }
-    }
-    {
-        hipStream_t q = F.fork(2, FK_WGRAD);
-        wg(2, [&](float *dst, hipStream_t qq) {
-            gemm<1>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dz2, S * nc, 32},
-                    EpSlab{dst, 145, 32}, 145, 32, S * nc, p.c2, qq);
-        }, p.c2, L.off_w2, 145 * 32, slab + sr.c2, q);
-    }
-    gemm<1>(AConvDx<32, 3, 1>{w.dz2, bs, bs, FastDiv(nc), FastDiv(bs)}, BConvT<16, 32>{th + L.off_w2, 288},
-            EpReluMask{w.dzc1, w.a1, (int)(S * nc), 16}, S * nc, 16, 288, p.c2x, s);
-    {
-        const int64_t M = 9 * L.C + 1;
-        wg(3, [&](float *dst, hipStream_t qq) {
-            gemm<1>(ABoardDw{src, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
-                    EpSlab{dst, (int)M, 16}, M, 16, S * nc, p.c1, qq);
-        }, p.c1, L.off_w1, M * 16, slab + sr.c1, s);
-    }
-    F.join(0, FK_WGRAD);
-    F.join(1, FK_WGRAD);
-    F.join(2, FK_WGRAD);
 }
 
 // ---------------------------------------------------------------- fused update

@@ -78,6 +78,7 @@ struct QWork {
     const float *wmax_img = nullptr; //   of this image
     double *target = nullptr, *loss = nullptr;
     int has_train = 0;
+    int64_t gen = 0;          // bumped on every reallocation (captured graphs hold the old pointers)
 };
 
 void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train);
@@ -142,7 +143,6 @@ struct GradSlabs {
     int64_t S = 0;
 };
 struct BwdOpts {
-    Fork *fork = nullptr;        // weight gradients on side streams
     GradSlabs *defer = nullptr;  // leave slabs + Dense2 to grad_update_launch
     bool dz1_ready = false;      // the LOSS head already wrote w.dz1
 };

@@ -3,6 +3,8 @@
 // (structs.jl:70, Julia Random.Xoshiro seeded through SHA-256).
 #include <cstdarg>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "snk_internal.hpp"
@@ -21,6 +23,18 @@ void set_error(const char *fmt, ...) {
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
     g_err = buf;
+}
+
+void set_lds_limit(const void *kernel, size_t bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<const void *, int>, size_t> done;
+    int dev = 0;
+    SNK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    size_t &have = done[{kernel, dev}];
+    if (bytes <= have) return;
+    SNK_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    have = bytes;
 }
 
 hipStream_t stream() {

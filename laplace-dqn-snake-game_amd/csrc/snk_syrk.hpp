@@ -390,7 +390,7 @@ __device__ __forceinline__ constexpr int waitcnt_vm(int n) { return (n & 15) | (
 
 // NW waves: 8 (two per SIMD, 64 x 32 per wave) or 4 (one per SIMD, 64 x 64 per wave:
 // half the fragment reads per MFMA)
-template <int NW, bool SH_PRIO = false>
+template <int NW>
 __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
     constexpr int NC = NW == 4 ? 2 : 1, NJ = 32 / NW;   // column tiles per wave, DMA jobs per wave and stage
     __shared__ __attribute__((aligned(16))) uint16_t lds[SH_BUF * 2 * 2 * SY_T * SH_ROW];   // 128 KB
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
         ddst[q] = ((op * 2 + pl) * SY_T + rb * 16) * SH_ROW;
     }
     auto dma = [&](int st, int buf) {
-        const int64_t k = a.kchunk < 0 ? 0 : (int64_t)min(st, nst - 1) * 2 * SY_KS;   // past the end: harmless reloads
+        const int64_t k = (int64_t)min(st, nst - 1) * 2 * SY_KS;   // past the end: harmless reloads
 #pragma unroll
         for (int q = 0; q < NJ; ++q)
             __builtin_amdgcn_global_load_lds((const void *)(dsrc[q] + k),
@@ -517,9 +517,7 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         frag(B, 1, f1);
         __builtin_amdgcn_sched_barrier(0);
-        if (SH_PRIO) __builtin_amdgcn_s_setprio(1);
         mfma_rest(f0);
-        if (SH_PRIO) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         dma(st + 3, (B + 3) & 3);
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * NJ));   // my part of stage st+1 landed
@@ -529,9 +527,7 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         frag((B + 1) & 3, 0, f0);
         __builtin_amdgcn_sched_barrier(0);
-        if (SH_PRIO) __builtin_amdgcn_s_setprio(1);
         mfma_rest(f1);
-        if (SH_PRIO) __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if (st % SY_FLUSH == SY_FLUSH - 1) flush();
     };

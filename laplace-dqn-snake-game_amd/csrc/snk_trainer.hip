@@ -20,7 +20,9 @@ namespace snk {
 struct alignas(16) TrainStats {
     int64_t episodes;      // finished episodes
     int64_t score_sum;
-    int64_t updates;       // nb (utils.jl:431)
+    int64_t updates;       // updates run by this trainer
+    int64_t nb;            // the reference's batch counter: update_target_net! when nb % rate == 0
+                           // (train!: nb = 0, 1, ... utils.jl:431-469; compute_D: from 1, compute_D.jl:56-134)
     int64_t env_steps;
     double reward_sum;     // sum of finished episode rewards
     double last_loss;
@@ -101,6 +103,7 @@ __global__ __launch_bounds__(256) void post_update_kernel(TrainStats *st, const 
     if (log) log[st->updates % log_cap] = l;          // track_loss! (utils.jl:404-406)
     st->epsilon = fmaxf(st->epsilon - decay, eps_end); // utils.jl:480
     st->updates += 1;
+    st->nb += 1;
 }
 
 void comm_allreduce_mean(snk_comm h, float *buf, int64_t n, hipStream_t s);
@@ -129,29 +132,27 @@ struct snk_trainer_s {
     hipGraph_t graph[4] = {nullptr, nullptr, nullptr, nullptr};
     hipGraphExec_t exec[4] = {nullptr, nullptr, nullptr, nullptr};
     int unroll = 8;
-    hipStream_t graph_stream = nullptr;
-    Fork fork;   // side streams: parallel branches of the iteration
+    int64_t ws_gen = 0;   // dqn workspace generation the graphs were captured against
+    void drop_graphs() {
+        for (int i = 0; i < 4; ++i) {
+            if (exec[i]) (void)hipGraphExecDestroy(exec[i]);
+            if (graph[i]) (void)hipGraphDestroy(graph[i]);
+            exec[i] = nullptr;
+            graph[i] = nullptr;
+        }
+    }
 };
 
-// One iteration's launch sequence (capturable: no host sync, no allocation).
-// Side branches: the first update's replay draw runs beside the act forward
-// (it only needs the transition count, which it offsets by the n transitions
-// this step stores; the advance kernel waits for it), episode statistics run
-// beside the update, and the update itself forks the target forward and the
-// weight gradients (dqn_loss_grad / qnet_backward).
-static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
+// One iteration's launch sequence (capturable: no host sync, no allocation),
+// with n_upd DQN updates after the env step. The first update's replay draw
+// counts the n transitions this step stores.
+static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream_t s) {
     const EnvDev &E = env_dev(h->env);
     const ReplayDev &R = replay_dev(h->rb);
     snk_dqn_s *q = h->dqn;
-    Fork &F = h->fork;
-    F.main = s;
-    F.next = 0;
-    const bool upd = learn && h->cfg.updates_per_iter > 0;
+    const bool upd = learn && n_upd > 0;
     const uint64_t sseed = h->cfg.seed ^ 0x5A4D504C45ULL;
-    if (upd) {
-        hipStream_t q2 = F.fork(2, FK_SAMPLE);
-        replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, q2, E.n);
-    }
+    if (upd) replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s, E.n);
     HeadArgs ha;
     ha.act = h->act;
     ha.seed = h->cfg.seed;
@@ -159,42 +160,36 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, hipStream_t s) {
     ha.eps_dev = &h->stats->epsilon;
     qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q);
     env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s);
-    if (upd) F.join(2, FK_SAMPLE);
-    hipStream_t q1 = F.fork(1, FK_STATS);
-    episode_stats_kernel<<<1, 1024, 0, q1>>>(E.out_done, E.out_ep_reward, E.out_score, E.n, h->stats, E.ctl,
-                                             R.count);
+    episode_stats_kernel<<<1, 1024, 0, s>>>(E.out_done, E.out_ep_reward, E.out_score, E.n, h->stats, E.ctl,
+                                            R.count);
     launch_check("episode_stats_kernel");
-    if (upd) {
-        for (int u = 0; u < h->cfg.updates_per_iter; ++u) {
-            if (u > 0)
-                replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s);
-            HeadArgs m;
-            m.idx = h->idx;
-            m.rew = R.reward;
-            m.done = R.done;
-            m.mask = R.mask;
-            m.act_idx = R.act;
-            GradSlabs pend;
-            LossOpts lo;
-            lo.fork = &F;
-            lo.defer = &pend;
-            lo.loss_mean = false;
-            dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s, lo);
-            // one pass: finish the gradient, RMSProp, forward image, update_target_net! when due
-            const UpdateTarget ut = dqn_update_target(q, &h->stats->updates, h->cfg.target_update_rate);
-            if (h->comm) {   // data-parallel replicas: mean gradient before the step
-                grad_update_launch(q->L, &pend, q->grad, nullptr, s);
-                comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
-                grad_update_launch(q->L, nullptr, q->grad, &ut, s);
-            } else {
-                grad_update_launch(q->L, &pend, q->grad, &ut, s);
-            }
-            post_update_kernel<<<1, 256, 0, s>>>(h->stats, q->trn.loss, h->B, q->loss_dev, h->loss_log, h->log_cap,
-                                                 h->cfg.decay, h->cfg.epsilon_end);
-            launch_check("post_update_kernel");
+    if (!upd) return;
+    for (int u = 0; u < n_upd; ++u) {
+        if (u > 0) replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s);
+        HeadArgs m;
+        m.idx = h->idx;
+        m.rew = R.reward;
+        m.done = R.done;
+        m.mask = R.mask;
+        m.act_idx = R.act;
+        GradSlabs pend;
+        LossOpts lo;
+        lo.defer = &pend;
+        lo.loss_mean = false;
+        dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s, lo);
+        // one pass: finish the gradient, RMSProp, forward image, update_target_net! when nb % rate == 0
+        const UpdateTarget ut = dqn_update_target(q, &h->stats->nb, h->cfg.target_update_rate);
+        if (h->comm) {   // data-parallel replicas: mean gradient before the step
+            grad_update_launch(q->L, &pend, q->grad, nullptr, s);
+            comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
+            grad_update_launch(q->L, nullptr, q->grad, &ut, s);
+        } else {
+            grad_update_launch(q->L, &pend, q->grad, &ut, s);
         }
+        post_update_kernel<<<1, 256, 0, s>>>(h->stats, q->trn.loss, h->B, q->loss_dev, h->loss_log, h->log_cap,
+                                             h->cfg.decay, h->cfg.epsilon_end);
+        launch_check("post_update_kernel");
     }
-    F.join(1, FK_STATS);
 }
 
 extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, snk_replay rb,
@@ -219,12 +214,11 @@ extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, sn
         h->act = dalloc<uint8_t>(E.n);
         h->idx = dalloc<int64_t>(h->B);
         h->loss_log = dalloc<double>(h->log_cap);
-        h->fork.create();
-        // parallel graph branches measured slower than one serial chain on
-        // this stack (each cross-stream edge cost ~30 us): off unless asked for
-        h->fork.enable = 0;
-        if (const char *e = getenv("SNK_FORK")) h->fork.enable = (unsigned)strtoul(e, nullptr, 0);
-        if (const char *e = getenv("SNK_GRAPH_UNROLL")) h->unroll = atoi(e) > 0 ? atoi(e) : 1;
+        // iterations per captured graph: they only communicate through device
+        // counters, so a longer graph is the same launch sequence with the
+        // graph launch gap paid once per `unroll` (measured 12.34 M env-steps/s
+        // at 8 against 12.28 M at 1)
+        h->unroll = cfg->graph_unroll > 0 ? cfg->graph_unroll : 8;
         TrainStats st{};
         st.epsilon = cfg->epsilon;
         st.reward_max = -INFINITY;
@@ -241,8 +235,10 @@ extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, sn
             dfree(dqn->slab);
             dqn->slab = dalloc<float>(need);
             dqn->slab_cap = need;
+            ++dqn->slab_gen;
         }
         SNK_HIP(hipStreamSynchronize(s));
+        h->ws_gen = dqn_ws_gen(dqn);
         *out = h;
     });
 }
@@ -251,32 +247,48 @@ extern "C" int snk_trainer_destroy(snk_trainer h) {
     return guard([&] {
         if (!h) return;
         (void)hipStreamSynchronize(stream());
-        for (int i = 0; i < 4; ++i) {
-            if (h->exec[i]) (void)hipGraphExecDestroy(h->exec[i]);
-            if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
-        }
+        h->drop_graphs();
         for (void *p : {(void *)h->stats, (void *)h->act, (void *)h->idx, (void *)h->loss_log}) dfree(p);
-        h->fork.destroy();
         delete h;
     });
+}
+
+// the trainer's buffers (allocated at create) may have been reallocated since
+// a graph was captured: a model call with a larger batch grows the shared dqn
+// workspaces. Re-size what the iteration touches and drop stale graphs.
+static void trainer_refresh(snk_trainer_s *h) {
+    snk_dqn_s *q = h->dqn;
+    qwork_ensure(q->act, q->L, env_dev(h->env).n, false);
+    qwork_ensure(q->tgt, q->L, h->B, false);
+    qwork_ensure(q->trn, q->L, h->B, true);
+    const int64_t gen = dqn_ws_gen(q);
+    if (gen != h->ws_gen) {
+        SNK_HIP(hipStreamSynchronize(stream()));
+        h->drop_graphs();
+        h->ws_gen = gen;
+    }
+}
+
+static void trainer_check_replay(snk_trainer_s *h) {
+    int64_t len = 0;
+    if (snk_replay_length(h->rb, &len) != SNK_OK) throw Error{SNK_ERR_HIP};
+    SNK_CHECK(len >= h->B, SNK_ERR_STATE, "replay holds %lld < batch_size %d transitions (fill it first)",
+              (long long)len, h->B);
 }
 
 extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int32_t use_graph) {
     return guard([&] {
         SNK_CHECK(h && iters >= 0, SNK_ERR_INVALID, "bad trainer_run arguments");
         hipStream_t s = stream();
-        if (learn && h->cfg.updates_per_iter > 0) {
-            int64_t len = 0;
-            if (snk_replay_length(h->rb, &len) != SNK_OK) throw Error{SNK_ERR_HIP};
-            SNK_CHECK(len >= h->B, SNK_ERR_STATE, "replay holds %lld < batch_size %d transitions (fill it first)",
-                      (long long)len, h->B);
-        }
+        const int upi = h->cfg.updates_per_iter;
+        if (learn && upi > 0) trainer_check_replay(h);
+        trainer_refresh(h);
         const int g = learn ? 1 : 0;
         auto capture = [&](int slot, int n) {
             if (h->exec[slot]) return;
             SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             try {
-                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, s);
+                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s);
             } catch (...) {
                 hipGraph_t dummy;
                 (void)hipStreamEndCapture(s, &dummy);
@@ -286,7 +298,7 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
             SNK_HIP(hipGraphInstantiate(&h->exec[slot], h->graph[slot], nullptr, nullptr, 0));
         };
         if (!use_graph) {
-            for (int64_t i = 0; i < iters; ++i) trainer_iteration(h, learn != 0, s);
+            for (int64_t i = 0; i < iters; ++i) trainer_iteration(h, learn != 0, upi, s);
             return;
         }
         const int U = h->unroll;
@@ -297,6 +309,24 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
         }
         if (i < iters) capture(2 * g, 1);
         for (; i < iters; ++i) SNK_HIP(hipGraphLaunch(h->exec[2 * g], s));
+    });
+}
+
+extern "C" int snk_trainer_run_partial(snk_trainer h, int32_t n_updates) {
+    return guard([&] {
+        SNK_CHECK(h && n_updates >= 0 && n_updates <= h->cfg.updates_per_iter, SNK_ERR_INVALID,
+                  "run_partial: 0 <= n_updates <= updates_per_iter");
+        if (n_updates > 0) trainer_check_replay(h);
+        trainer_refresh(h);
+        trainer_iteration(h, true, n_updates, stream());
+    });
+}
+
+extern "C" int snk_trainer_set_nb(snk_trainer h, int64_t nb) {
+    return guard([&] {
+        SNK_CHECK(h && nb >= 0, SNK_ERR_INVALID, "bad set_nb arguments");
+        SNK_HIP(hipMemcpyAsync(&h->stats->nb, &nb, sizeof nb, hipMemcpyHostToDevice, stream()));
+        SNK_HIP(hipStreamSynchronize(stream()));
     });
 }
 
@@ -314,12 +344,7 @@ extern "C" int snk_trainer_set_comm(snk_trainer h, snk_comm comm) {
         }
         SNK_HIP(hipStreamSynchronize(s));
         h->comm = comm;   // NULL: detach (updates local again)
-        for (int i = 0; i < 4; ++i) {   // captured graphs predate the collective
-            if (h->exec[i]) (void)hipGraphExecDestroy(h->exec[i]);
-            if (h->graph[i]) (void)hipGraphDestroy(h->graph[i]);
-            h->exec[i] = nullptr;
-            h->graph[i] = nullptr;
-        }
+        h->drop_graphs();  // captured graphs predate the collective
     });
 }
 
@@ -333,6 +358,7 @@ extern "C" int snk_trainer_stats(snk_trainer h, snk_trainer_stats_t *out) {
         out->episodes = st.episodes;
         out->score_sum = st.score_sum;
         out->updates = st.updates;
+        out->nb = st.nb;
         out->env_steps = st.env_steps;
         out->reward_sum = st.reward_sum;
         out->last_loss = st.last_loss;

@@ -124,27 +124,48 @@ class LaplaceD:
 
 
 def compute_D(tr, K: int = 1000, thin: int = 10, burn_in: int = 50_000, graph: bool = True,
-              reset_optimizer: bool = True) -> LaplaceD:
+              reset_optimizer: bool = True, schedule: str = "episode") -> LaplaceD:
     """compute_D.jl:33-86 on a Trainer: fill_buffer!, a fresh RMSProp state
-    (`Flux.setup`, :47), then the training loop; at update nb (1-based) with
-    nb >= burn_in and nb % thin == 0 the current q_net goes into the next
-    column, *before* that update runs; after the K-th column: Welford +
-    centring, return (the BSON save of :84 is the caller's business)."""
-    from .trainer import fill_buffer_
+    (`Flux.setup`, :47), then the training loop over nb = 1, 2, ...: from
+    nb == burn_in on, at nb % thin == 0 the current q_net goes into the next
+    column *before* that update runs; after the K-th column: Welford +
+    centring, return (the BSON save of :84 is the caller's business).
+    update_target_net! runs after update nb when nb % rate == 0 (:129-132).
 
-    if tr.updates_per_iter != 1:
-        raise ValueError("compute_D snapshots between single updates: use updates_per_iter = 1")
+    schedule="episode": the reference's loop body, one full epsilon-greedy
+    episode stored and one B-sample update per nb (:89-138, EpisodeLoop).
+    schedule="batched": one lockstep step of tr's n_envs games per update
+    (the device trainer, graph-replayed), with the same nb bookkeeping."""
+    from .trainer import EpisodeLoop, fill_buffer_
+
     model = tr.model
     lap = LaplaceD(model.P, K)
-    fill_buffer_(tr, graph=graph)
-    if reset_optimizer:
-        model.set_params(np.zeros(model.P, np.float32), _lib.SNK_NET_OPT_STATE)
-    first = burn_in if burn_in % thin == 0 else burn_in + (thin - burn_in % thin)
-    tr.run(first - 1, learn=True, graph=graph)          # updates nb = 1 .. first-1
-    for pos in range(K):
-        lap.snapshot(model, pos)                          # before update nb = first + pos*thin
-        if pos + 1 < K:
-            tr.run(thin, learn=True, graph=graph)
+    first = burn_in if burn_in % thin == 0 else burn_in + (thin - burn_in % thin)   # first nb snapshotted
+    if schedule == "episode":
+        loop = EpisodeLoop(tr)
+        loop.fill()
+        if reset_optimizer:
+            model.set_params(np.zeros(model.P, np.float32), _lib.SNK_NET_OPT_STATE)
+        nb = 1
+        for pos in range(K):
+            while nb < first + pos * thin:
+                loop.step(nb)
+                nb += 1
+            lap.snapshot(model, pos)
+    elif schedule == "batched":
+        if tr.updates_per_iter != 1:
+            raise ValueError("compute_D snapshots between single updates: use updates_per_iter = 1")
+        fill_buffer_(tr, graph=graph)
+        if reset_optimizer:
+            model.set_params(np.zeros(model.P, np.float32), _lib.SNK_NET_OPT_STATE)
+        tr.set_nb(1)
+        tr.run(first - 1, learn=True, graph=graph)          # updates nb = 1 .. first-1
+        for pos in range(K):
+            lap.snapshot(model, pos)                          # before update nb = first + pos*thin
+            if pos + 1 < K:
+                tr.run(thin, learn=True, graph=graph)
+    else:
+        raise ValueError(f"unknown schedule {schedule!r}")
     lap.fit_center()
     return lap
 

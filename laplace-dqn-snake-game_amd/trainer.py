@@ -40,7 +40,7 @@ class Trainer:
                  epsilon_end: float = 0.05, decay: float = 1e-6, save: bool = False, game: SnakeGame | None = None,
                  model: DQNModel | None = None, n_envs: int = 1, board_size: int = 10, n_frames: int = 2,
                  capacity: int = 50000, batch_size: int = 64, updates_per_iter: int = 1, gamma: float = 0.97,
-                 seed: int = 1234, loss_log_capacity: int = 1 << 20):
+                 seed: int = 1234, loss_log_capacity: int = 1 << 20, graph_unroll: int = 0):
         self.game = game if game is not None else SnakeGame(board_size, n_frames, n_envs=n_envs, autoreset=True)
         if not self.game.autoreset:
             raise ValueError("the batched trainer needs auto-reset games")
@@ -56,7 +56,8 @@ class Trainer:
         self.episode_rewards: list[float] = []
         self.episode_losses: list[float] = []
         cfg = _lib.TrainerCfg(self.epsilon, self.epsilon_end, self.decay, self.updates_per_iter,
-                              self.target_update_rate, self.gamma, self.seed, self.loss_log_capacity)
+                              self.target_update_rate, self.gamma, self.seed, self.loss_log_capacity,
+                              int(graph_unroll))
         h = vp()
         call("snk_trainer_create", C.byref(h), self.game.handle, self.model.handle, self.buffer.handle,
              C.byref(cfg))
@@ -73,6 +74,16 @@ class Trainer:
 
     def run(self, iters: int, learn: bool = True, graph: bool = True) -> None:
         call("snk_trainer_run", self._h, int(iters), int(learn), int(graph))
+
+    def run_partial(self, n_updates: int) -> None:
+        """One lockstep iteration with n_updates (< updates_per_iter) updates."""
+        call("snk_trainer_run_partial", self._h, int(n_updates))
+
+    def set_nb(self, nb: int) -> None:
+        """The reference's batch counter for update_target_net! (nb % rate == 0,
+        then nb += 1): train! starts at 0 (utils.jl:431), compute_D at 1
+        (compute_D.jl:56)."""
+        call("snk_trainer_set_nb", self._h, int(nb))
 
     def stats(self) -> dict:
         st = _lib.TrainerStats()
@@ -117,32 +128,56 @@ def _episode_into(tr: "Trainer", game: SnakeGame, act: DeviceArray, epsilon: flo
     return L, float(ep)
 
 
+class EpisodeLoop:
+    """The reference's one-episode-per-update loop body, host-driven over the
+    device primitives: one SnakeGame, tr.buffer, tr.model. Shared by train!
+    (utils.jl:420-482, nb from 0) and compute_D (compute_D.jl:89-138, nb from 1).
+    The replay draw of update u is `sample(seed, draw=u)` with u counting
+    this loop's updates."""
+
+    def __init__(self, tr: "Trainer"):
+        self.tr = tr
+        self.game = SnakeGame(tr.game.board_size, tr.game.n_frames, n_envs=1, autoreset=True)
+        self.act = DeviceArray(1, np.uint8)
+        self.eps = np.float32(tr.epsilon)
+        self.draws = 0
+
+    def fill(self) -> int:
+        """fill_buffer! (utils.jl:389-402): play until more than capacity
+        transitions were played."""
+        tr, played = self.tr, 0
+        while played <= tr.buffer.capacity:
+            L, _ = _episode_into(tr, self.game, self.act, float(self.eps), tr.seed)
+            played += L
+        return played
+
+    def step(self, nb: int) -> tuple[float, float]:
+        """One episode into the buffer, one B-sample update (sample -> t_net
+        target -> Huber -> backward -> RMSProp), update_target_net! when
+        nb % rate == 0, epsilon decay (utils.jl:480). Returns (episode reward, loss)."""
+        tr = self.tr
+        _, ep_reward = _episode_into(tr, self.game, self.act, float(self.eps), tr.seed)
+        idx, B = sample(tr.buffer, seed=tr.seed, draw=self.draws)
+        self.draws += 1
+        loss = tr.model.update(tr.buffer, idx, B, tr.gamma)
+        if nb % tr.target_update_rate == 0:
+            call("snk_dqn_sync_target", tr.model.handle)
+        self.eps = max(np.float32(self.eps - np.float32(tr.decay)), np.float32(tr.epsilon_end))
+        tr.epsilon = float(self.eps)
+        return ep_reward, loss
+
+
 def _train_episodes(tr: "Trainer") -> dict:
     """utils.jl:389-402 (fill_buffer!) and 420-482 (train!'s loop), one env:
     fill until more than `capacity` experiences were played; then for
-    nb = 0..n_batches: one epsilon-greedy episode into the buffer, one
-    B-sample DQN update (sample -> t_net target -> Huber -> backward ->
-    RMSProp), update_target_net! when nb % rate == 0, epsilon decay."""
-    bs, nf = tr.game.board_size, tr.game.n_frames
-    game = SnakeGame(bs, nf, n_envs=1, autoreset=True)
-    act = DeviceArray(1, np.uint8)
-    seed = tr.seed
-    played = 0
-    while played <= tr.buffer.capacity:                       # utils.jl:392
-        L, _ = _episode_into(tr, game, act, tr.epsilon, seed)
-        played += L
-    eps = np.float32(tr.epsilon)
+    nb = 0..n_batches one EpisodeLoop.step."""
+    loop = EpisodeLoop(tr)
+    loop.fill()
     for nb in range(tr.n_batches + 1):                        # utils.jl:435 (nb <= n_batches)
-        _, ep_reward = _episode_into(tr, game, act, float(eps), seed)
-        idx, B = sample(tr.buffer, seed=seed, draw=nb)
-        loss = tr.model.update(tr.buffer, idx, B, tr.gamma)
-        if nb % tr.target_update_rate == 0:                   # utils.jl:469-472
-            call("snk_dqn_sync_target", tr.model.handle)
+        ep_reward, loss = loop.step(nb)
         tr.episode_rewards.append(ep_reward)
         tr.episode_losses.append(loss)
-        eps = max(np.float32(eps - np.float32(tr.decay)), np.float32(tr.epsilon_end))   # utils.jl:480
-    tr.epsilon = float(eps)
-    return {"updates": tr.n_batches + 1, "episodes": len(tr.episode_rewards), "epsilon": float(eps),
+    return {"updates": tr.n_batches + 1, "episodes": len(tr.episode_rewards), "epsilon": float(loop.eps),
             "buffer_length": len(tr.buffer)}
 
 
@@ -158,7 +193,11 @@ def train_(tr: Trainer, trainer_name: str | None = None, graph: bool = True, sch
     if tr.updates_per_iter > 0:
         total = tr.n_batches + 1 - tr.stats()["updates"]
         if total > 0:
-            tr.run(math.ceil(total / tr.updates_per_iter), learn=True, graph=graph)
+            # exactly n_batches + 1 updates: full iterations, then one partial one
+            full, rest = divmod(total, tr.updates_per_iter)
+            tr.run(full, learn=True, graph=graph)
+            if rest:
+                tr.run_partial(rest)
     return tr.stats()
 
 

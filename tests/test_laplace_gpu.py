@@ -165,13 +165,13 @@ def test_spectrum_ncols_and_trajectory_match_svd(snk):
 
 
 # ---------------------------------------------------------------- Laplace sampling (la_utils.jl:83-118)
-def _fitted_lap(snk, m, K, seed=0):
+def _fitted_lap(snk, m, K, seed=0, spread=0.02):
     """K q_net snapshots spread around m's weights, Welford-fitted and centred."""
     rng = np.random.default_rng(seed)
     p0 = m.get_params()
     lap = snk.LaplaceD(m.P, K)
     for k in range(K):
-        m.set_params((p0 + rng.standard_normal(p0.size).astype(np.float32) * np.float32(0.02)).astype(np.float32))
+        m.set_params((p0 + rng.standard_normal(p0.size).astype(np.float32) * np.float32(spread)).astype(np.float32))
         lap.snapshot(m, k)
     m.set_params(p0)
     lap.fit_center()
@@ -266,3 +266,37 @@ def test_laplace_sampling_lockstep_episodes(snk):
                 s = np.float32(s + np.float32(v))
             assert s == res["rewards"][n] and got["dones"][o + L - 1]
             o += L
+
+
+def test_laplace_sampling_wraps_small_buffer(snk):
+    """More better-model transitions than the buffer holds: store! in
+    (model, step) order keeps exactly the last `capacity` of them, each in the
+    ring slot the sequential stores leave it in, and the count advances by all
+    of them (utils.jl:267-277). Checked against the same sampling into a
+    buffer large enough to hold everything."""
+    bs, C, K, cap = 10, 2, 5, 8
+    big = snk.Trainer(n_envs=1, board_size=bs, n_frames=C, capacity=20000, seed=5)
+    small = snk.Trainer(n_envs=1, board_size=bs, n_frames=C, capacity=cap, batch_size=4, seed=5)
+    # tr.model always takes action index 0 (Dense2 = 0, bias (1, 0, 0)): straight up
+    # into the wall, 7 steps and reward -1.06; sampled models that die sooner beat it
+    p = big.model.get_params()
+    p[-195:] = 0
+    p[-3] = 1
+    for t in (big, small):
+        t.model.set_params(p)
+    lap = _fitted_lap(snk, big.model, K, seed=1, spread=0.5)
+    c0 = 3                                   # a partly filled ring to start from
+    fr = np.zeros((c0, C + 1, bs * bs), np.int8)
+    snk.store_(small.buffer, fr, np.zeros(c0), np.zeros(c0, np.float32), np.zeros(c0), np.zeros((c0, 3)),
+               np.zeros(c0))
+    rb = snk.laplace_sampling_(big, lap, n_models=32, seed=21, chunk=16)
+    rs = snk.laplace_sampling_(small, lap, n_models=32, seed=21, chunk=16)
+    assert rs["n_better_models"] == rb["n_better_models"]
+    grown = len(big.buffer)
+    assert grown > cap, "the sampling must overflow the small ring for this test"
+    assert small.buffer.count == c0 + grown and len(small.buffer) == cap
+    ref = snk.stack_exp(big.buffer, np.arange(grown - cap, grown))
+    slots = (c0 + np.arange(grown - cap, grown)) % cap
+    got = snk.stack_exp(small.buffer, slots)
+    for k in ("states", "next_states", "actions", "rewards", "dones", "suicidal_mask"):
+        assert np.array_equal(got[k], ref[k]), k
