@@ -207,7 +207,7 @@ def test_compute_D_episode_schedule_vs_oracle(snk):
     over 14 RMSProp steps, whose g / sqrt(acc) amplifies tiny-gradient
     differences), while the replica on
     train!'s phase (nb from 0: syncs after nb = 0, 2, ...) misses by more than
-    10x that: the test pins the phase. The Welford mean (~theta) within 5e-5.
+    10x that: the test pins the phase. The Welford mean (~theta) within 5e-5."""
     from oracle_loops import OracleEpisodeLoop
     bs, C, cap, seed = 10, 2, 300, 0xD00D
     tr = snk.Trainer(n_envs=1, board_size=bs, n_frames=C, capacity=cap, target_update_rate=2, seed=seed)
