@@ -108,6 +108,94 @@ def cpu_baseline(args) -> dict:
                        f"fwd {t_fwd:.2f}s + step {t_step:.3f}s + update {t_upd:.2f}s")}
 
 
+def d_buffer(snk, bs, C, n):
+    """The D(50k) replay: n transitions of lockstep play (5000 envs x n/5000
+    steps, counter-RNG actions from a fixed seed). Deterministic, so every
+    rank of a multi-GPU build holds the same buffer without moving it."""
+    import numpy as np
+    n_env = 5000 if n % 5000 == 0 else n
+    g = snk.SnakeGame(bs, C, n_envs=n_env, autoreset=True)
+    rb = snk.ReplayBuffer(n, board_size=bs, n_frames=C, batch_size=64)
+    act = snk.DeviceArray(n_env, np.uint8)
+    for _ in range(n // n_env):
+        snk.synth_actions_dev(g, 0xD50, act)
+        snk.step_indices_dev(g, act.ptr, replay=rb)
+    return rb
+
+
+def d_build_gram(args, snk, model, dist, rank, world) -> dict:
+    """D(50k): G = J J' over the 50,000 per-sample Jacobians of the D buffer
+    (north_star / configs[4]). world > 1: each rank computes its contiguous
+    run of the lower-triangle tiles (snk_jacobian_gram_shard), then rank 0
+    receives the others' tiles over RCCL send/recv (snk_jacobian_gram_gather).
+    d_build_sec = max-over-ranks shard time + the gather (G complete on rank 0)."""
+    import time
+
+    import numpy as np
+    from snake_amd import _lib
+
+    n = args.d_samples or 50_000
+    rb = d_buffer(snk, args.board_size, args.n_frames, n)
+    Kc = 9 * args.n_frames * 16 + 16 + 4640 + 73792            # conv columns of a Jacobian row
+    G = snk.DeviceArray((n, n), np.float32)
+
+    def sync():
+        _lib.call("snk_synchronize")
+        if dist is not None:
+            dist.barrier()
+
+    if world == 1:
+        snk.jacobian_gram(model, rb, n, out=G, host=False)   # workspace allocation + first launch
+        sync()
+        t0 = time.perf_counter()
+        _, ms = snk.jacobian_gram(model, rb, n, out=G, host=False)
+        wall = time.perf_counter() - t0
+        t_gather = 0.0
+    else:
+        import torch
+        comm = snk.Comm(world, rank, snk.dist.broadcast_bytes(dist, snk.Comm.unique_id() if rank == 0 else None,
+                                                               rank))
+        G.zero()
+        snk.jacobian_gram_shard(model, rb, n, rank, world, G)     # warm-up
+        sync()
+        t0 = time.perf_counter()
+        ms = snk.jacobian_gram_shard(model, rb, n, rank, world, G)
+        sync()
+        wall = time.perf_counter() - t0
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+        t0 = time.perf_counter()
+        snk.jacobian_gram_gather(comm, n, G, 0)
+        sync()
+        t_gather = time.perf_counter() - t0
+        del comm
+    T = (n + 127) // 128
+    tiles = len(snk.gram_tiles(n, rank, world))
+    flop_gram = float(n) * (n + 1) * Kc * tiles / (T * (T + 1) // 2)   # this rank's share, 2 flop / MAC
+    tf = flop_gram / (ms[2] * 1e-3) / 1e12
+    speak = PEAK_BF16_TFLOPS / H3_PRODUCTS
+    res = {"d_build_sec": wall + t_gather,
+           "d_build": {"kind": "per-sample Jacobian Gram G = J J' (n x n, fp32-accurate fp16 h3 split MFMA, "
+                               "fp64 accumulation)" + (f", {world} shards of the lower-triangle tiles + RCCL "
+                                                        f"send/recv gather to rank 0" if world > 1 else ""),
+                       "n_samples": n, "n_params": model.P, "conv_columns": Kc, "ranks": world,
+                       "shard_sec_max_over_ranks": wall, "gather_sec": t_gather,
+                       "phase_ms": {"forward_and_data_grads": ms[0], "per_sample_conv_jacobians": ms[1],
+                                    "conv_gram": ms[2], "dense_terms_and_mirror": ms[3]},
+                       "naive_flop": 2.0 * n * n * model.P, "executed_gram_flop_this_rank": flop_gram,
+                       "roofline": {"bound": "mfma",
+                                    "kernel": "h3_rows_kernel + syrk_h3_kernel (fp16 h3 split, LDS-DMA staged), "
+                                              "conv-column Gram",
+                                    "achieved": tf, "peak": speak, "unit": "TFLOP/s (fp32-equivalent)",
+                                    "frac": tf / speak, "avg_launch_ms": ms[2], "flop_per_launch": flop_gram,
+                                    "traffic": None, "half_mfma_tflops_executed": tf * H3_PRODUCTS,
+                                    "mfma_utilization": tf * H3_PRODUCTS / PEAK_BF16_TFLOPS,
+                                    "fp32_mfma_peak": PEAK_FP32_TFLOPS}}}
+    del G, rb
+    return res
+
+
 def d_build(args, snk, tr) -> dict:
     """The two Laplace D builds, after the timed region, on rank 0.
 
@@ -120,39 +208,8 @@ def d_build(args, snk, tr) -> dict:
     import numpy as np
     from snake_amd import _lib
 
-    n = args.d_samples or len(tr.buffer)
-    Kc = 9 * args.n_frames * 16 + 16 + 4640 + 73792            # conv columns of a Jacobian row
-    G = snk.DeviceArray((n, n), np.float32)
-    snk.jacobian_gram(tr.model, tr.buffer, n, out=G, host=False)   # workspace allocation + first launch
-    _lib.call("snk_synchronize")
-    t0 = time.perf_counter()
-    _, ms = snk.jacobian_gram(tr.model, tr.buffer, n, out=G, host=False)
-    wall = time.perf_counter() - t0
-    flop_gram = float(n) * (n + 1) * Kc                          # lower triangle incl. diagonal, 2 flop / MAC
-    tf = flop_gram / (ms[2] * 1e-3) / 1e12
+    res = d_build_gram(args, snk, tr.model, None, 0, 1)
     P = tr.model.P
-    # default: syrk_h3_kernel, the fp32 products as 3 fp16 products of per-row-scaled
-    # parts (SNK_SYRK=x6: 6 bf16 split products; =fp32: native f32 MFMA)
-    mode = os.environ.get("SNK_SYRK", "h3")
-    nprod = {"h3": H3_PRODUCTS, "x6": X6_PRODUCTS}.get(mode)
-    speak = PEAK_BF16_TFLOPS / nprod if nprod else PEAK_FP32_TFLOPS
-    kname = {"h3": "h3_rows_kernel + syrk_h3_kernel (fp16 h3 split, LDS-DMA staged)",
-             "x6": "syrk_kernel (bf16 x6 split)"}.get(mode, "syrk_kernel (f32 MFMA)")
-    res = {"d_build_sec": wall,
-           "d_build": {"kind": "per-sample Jacobian Gram G = J J' (n x n, fp32-accurate "
-                               + {"h3": "fp16 h3 split MFMA", "x6": "bf16x6 split MFMA"}.get(mode, "f32 MFMA")
-                               + ", fp64 accumulation)",
-                       "n_samples": n, "n_params": P, "conv_columns": Kc,
-                       "phase_ms": {"forward_and_data_grads": ms[0], "per_sample_conv_jacobians": ms[1],
-                                    "conv_gram": ms[2], "dense_terms_and_mirror": ms[3]},
-                       "naive_flop": 2.0 * n * n * P, "executed_gram_flop": flop_gram,
-                       "roofline": {"bound": "mfma", "kernel": kname + ", conv-column Gram", "achieved": tf,
-                                    "peak": speak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / speak,
-                                    "avg_launch_ms": ms[2], "flop_per_launch": flop_gram, "traffic": None,
-                                    "half_mfma_tflops_executed": tf * nprod if nprod else None,
-                                    "mfma_utilization": tf * nprod / PEAK_BF16_TFLOPS if nprod else tf / PEAK_FP32_TFLOPS,
-                                    "fp32_mfma_peak": PEAK_FP32_TFLOPS}}}
-    del G
     K = args.d_snapshots
     if K > 1:
         lap = snk.LaplaceD(P, K)
@@ -349,8 +406,14 @@ def main():
             del gl, rl, al
         except Exception as e:   # report, do not fail the headline line
             out["step_kernel_large"] = {"error": str(e)}
-    if rank == 0 and world == 1 and not args.no_dbuild:   # single-GPU measurements (configs[4])
-        out.update(d_build(args, snk, tr))
+    if not args.no_dbuild:
+        if world == 1:      # D(50k) + compute_D's snapshot Gram + laplace_sampling! (configs[4])
+            if rank == 0:
+                out.update(d_build(args, snk, tr))
+        else:               # D(50k) across the ranks
+            r = d_build_gram(args, snk, tr.model, dist, rank, world)
+            if rank == 0:
+                out.update(r)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

@@ -272,6 +272,20 @@ int snk_jacobian(snk_dqn m, snk_replay rb, const int64_t *slots_dev, int64_t n, 
  * gradients, per-sample conv Jacobians, conv Gram, dense terms + mirror. */
 int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_dev, float *ms_out);
 
+/* D(50k) across ranks: the n x n Gram's 128 x 128 lower-triangle
+ * tiles are split into nranks contiguous runs of the XCD-aware tile order; each
+ * rank computes every Jacobian row (cheap) and only its own tiles (+ their
+ * mirror) into G_dev, leaving the rest untouched. ms_out as snk_jacobian_gram. */
+int snk_jacobian_gram_shard(snk_dqn m, snk_replay rb, int64_t n, int32_t rank, int32_t nranks, float *G_dev,
+                            float *ms_out);
+/* the tiles of shard rank / nranks: count, and (optional) their top-left
+ * (row, col) element pairs, tiles_host [2 * count] (host only, no device) */
+int snk_gram_tiles(int64_t n, int32_t rank, int32_t nranks, int32_t *tiles_host, int64_t *count_out);
+/* every rank's shard tiles onto root's G_dev (point-to-point over RCCL: each
+ * rank packs its tiles and sends them on its own link; root unpacks and
+ * mirrors). Collective: every rank of c calls it after its shard. */
+int snk_jacobian_gram_gather(snk_comm c, int64_t n, float *G_dev, int32_t root);
+
 /* ---------------------------------------------------------------- Laplace sampling
  * la_utils.jl:83-118. D, mean and var are the handle's (after
  * snk_laplace_fit_center: the centred deviation matrix and its Welford

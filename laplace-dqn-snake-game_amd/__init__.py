@@ -15,8 +15,9 @@ from ._lib import SNK_NET_GRAD, SNK_NET_OPT_STATE, SNK_NET_Q, SNK_NET_TARGET  # 
 from .qnet import DQNModel, nparams, update_target_net_  # noqa: F401
 from .dist import Comm, aggregate_throughput, dist_attach, dist_detach  # noqa: F401
 from .trainer import Trainer, epsilon_greedy, fill_buffer_, play_episode, train_  # noqa: F401
-from .laplace import (LaplaceD, compute_D, jacobian, jacobian_gram, laplace_normals,  # noqa: F401
-                      laplace_sampling_, sample_model)
+from .laplace import (LaplaceD, compute_D, gram_tiles, jacobian, jacobian_gram,  # noqa: F401
+                      jacobian_gram_gather, jacobian_gram_shard, laplace_normals, laplace_sampling_,
+                      sample_model)
 from .bsonio import load_trainer, read_trainer  # noqa: F401
 
 __version__ = "1.0.0"

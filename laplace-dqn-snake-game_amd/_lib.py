@@ -125,6 +125,9 @@ _PROTOS = {
     "snk_laplace_gram": [vp, P(f32)],
     "snk_jacobian": [vp, vp, vp, i64, vp],
     "snk_jacobian_gram": [vp, vp, i64, vp, P(f32)],
+    "snk_jacobian_gram_shard": [vp, vp, i64, i32, i32, vp, P(f32)],
+    "snk_gram_tiles": [i64, i32, i32, vp, P(i64)],
+    "snk_jacobian_gram_gather": [vp, i64, vp, i32],
     "snk_laplace_normals": [u64, i64, i32, i64, i64, vp],
     "snk_laplace_sample_params": [vp, vp, u64, i64, vp],
     "snk_laplace_sampling": [vp, vp, vp, i64, u64, i64, P(f32), P(i64), vp, vp],

@@ -76,6 +76,21 @@ void comm_broadcast(snk_comm h, float *buf, int64_t n, int root, hipStream_t s) 
     SNK_NCCL(ncclBroadcast(buf, buf, (size_t)n, ncclFloat32, root, h->comm, s));
 }
 int comm_size(snk_comm h) { return h->nranks; }
+int comm_rank(snk_comm h) { return h->rank; }
+// point-to-point gather: every rank but root sends its n_send floats, root
+// receives rank r's n_recv[r] into recv[r]. On xGMI each sender has its own
+// link to root, so the transfers run side by side (one group).
+void comm_gather_to_root(snk_comm h, const float *send, int64_t n_send, float *const *recv, const int64_t *n_recv,
+                         int root, hipStream_t s) {
+    SNK_NCCL(ncclGroupStart());
+    if (h->rank == root) {
+        for (int r = 0; r < h->nranks; ++r)
+            if (r != root && n_recv[r] > 0) SNK_NCCL(ncclRecv(recv[r], (size_t)n_recv[r], ncclFloat32, r, h->comm, s));
+    } else if (n_send > 0) {
+        SNK_NCCL(ncclSend(send, (size_t)n_send, ncclFloat32, root, h->comm, s));
+    }
+    SNK_NCCL(ncclGroupEnd());
+}
 }  // namespace snk
 
 extern "C" int snk_comm_allreduce_mean(snk_comm h, float *buf_dev, int64_t n) {

@@ -17,6 +17,7 @@
 //     the 79k conv columns of J go through the big MFMA Gram.
 #include <cstring>
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "snk_dqn.hpp"
@@ -114,6 +115,56 @@ __global__ __launch_bounds__(256) void mirror_kernel(float *__restrict__ G, int 
     }
 }
 
+// the same for the 128 x 128 lower tiles [t0, t0 + gridDim.x) of a tile order:
+// (bi, bj) -> (bj, bi), strictly-lower elements only
+__global__ __launch_bounds__(256) void mirror_tiles_kernel(float *__restrict__ G, int N, int64_t ld,
+                                                           const int2 *__restrict__ tiles, int64_t t0) {
+    __shared__ float t[64][65];
+    const int2 tb = tiles[t0 + blockIdx.x];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int q = 0; q < 4; ++q) {   // four 64 x 64 quarters of the tile
+        const int si = tb.x * 128 + (q >> 1) * 64, sj = tb.y * 128 + (q & 1) * 64;
+        if (sj > si) continue;      // upper quarter of a diagonal tile
+        __syncthreads();
+        for (int r = ty; r < 64; r += 4) {
+            const int i = si + r, j = sj + tx;
+            t[r][tx] = (i < N && j < N) ? G[(int64_t)i * ld + j] : 0.0f;
+        }
+        __syncthreads();
+        for (int r = ty; r < 64; r += 4) {
+            const int j = sj + r, i = si + tx;
+            if (i < N && j < N && i > j) G[(int64_t)j * ld + i] = t[tx][r];
+        }
+    }
+}
+
+// shard tiles [t0, t0 + gridDim.x) of G <-> a packed [tile][128][128] buffer
+// (unpack also writes the mirrored upper half)
+__global__ __launch_bounds__(256) void gram_pack_kernel(const float *__restrict__ G, int N, int64_t ld,
+                                                        const int2 *__restrict__ tiles, int64_t t0,
+                                                        float *__restrict__ buf) {
+    const int2 tb = tiles[t0 + blockIdx.x];
+    float *o = buf + (int64_t)blockIdx.x * 128 * 128;
+    for (int e = threadIdx.x; e < 128 * 128; e += 256) {
+        const int i = tb.x * 128 + (e >> 7), j = tb.y * 128 + (e & 127);
+        o[e] = (i < N && j < N) ? G[(int64_t)i * ld + j] : 0.0f;
+    }
+}
+__global__ __launch_bounds__(256) void gram_unpack_kernel(float *__restrict__ G, int N, int64_t ld,
+                                                          const int2 *__restrict__ tiles, int64_t t0,
+                                                          const float *__restrict__ buf) {
+    const int2 tb = tiles[t0 + blockIdx.x];
+    const float *p = buf + (int64_t)blockIdx.x * 128 * 128;
+    for (int e = threadIdx.x; e < 128 * 128; e += 256) {
+        const int i = tb.x * 128 + (e >> 7), j = tb.y * 128 + (e & 127);
+        if (i < N && j < N && j <= i) {
+            const float v = p[e];
+            G[(int64_t)i * ld + j] = v;
+            G[(int64_t)j * ld + i] = v;
+        }
+    }
+}
+
 __global__ void iota_kernel(int64_t *__restrict__ v, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = i;
@@ -132,10 +183,7 @@ __global__ void jac_permute_kernel(const float *__restrict__ Jp, int64_t ldp, co
 // columns, so the ~32 workgroups an XCD runs at once (syrk_xcd_remap hands
 // each XCD a contiguous run of this list) share 8 + 4 row blocks in its L2
 // instead of 1 + 32 in plain row-major order. One device table per N, kept.
-static const int2 *syrk_tile_order(int N) {
-    static std::vector<std::pair<int, int2 *>> cache;
-    for (auto &c : cache)
-        if (c.first == N) return c.second;
+static std::vector<int2> syrk_tile_order_host(int N) {
     const int T = (int)ceil_div(N, SY_T);
     std::vector<int2> t;
     t.reserve((size_t)T * (T + 1) / 2);
@@ -145,18 +193,39 @@ static const int2 *syrk_tile_order(int N) {
             for (int i = i0; i < std::min(T, i0 + SI); ++i)
                 for (int j = j0; j < std::min(j0 + SJ, i + 1); ++j) t.push_back(int2{i, j});
     SNK_CHECK((int64_t)t.size() == (int64_t)T * (T + 1) / 2, SNK_ERR_INTERNAL, "syrk tile order");
+    return t;
+}
+static const int2 *syrk_tile_order(int N) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<int, int>, int2 *>> cache;   // (N, device) -> table
+    int dev = 0;
+    SNK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &c : cache)
+        if (c.first.first == N && c.first.second == dev) return c.second;
+    const std::vector<int2> t = syrk_tile_order_host(N);
     int2 *d = nullptr;
     SNK_HIP(hipMalloc(&d, t.size() * sizeof(int2)));
     SNK_HIP(hipMemcpy(d, t.data(), t.size() * sizeof(int2), hipMemcpyHostToDevice));
-    cache.emplace_back(N, d);
+    cache.emplace_back(std::make_pair(N, dev), d);
     return d;
 }
 
-static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s) {
+// lower-triangle tiles [t0, t1) of syrk_tile_order(N) for shard `rank` of `nranks`
+// (contiguous runs of the supertile order: each shard keeps its L2 locality)
+static void gram_tile_range(int64_t N, int rank, int nranks, int64_t &t0, int64_t &t1) {
+    const int64_t T = ceil_div(N, SY_T), tot = T * (T + 1) / 2;
+    t0 = tot * rank / nranks;
+    t1 = tot * (rank + 1) / nranks;
+}
+
+static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s, int rank = 0, int nranks = 1) {
     SyrkArgs a = a0;
-    const int64_t T = ceil_div(a.N, SY_T);
-    a.ntiles = T * (T + 1) / 2;
-    a.tiles = T < 16 ? nullptr : syrk_tile_order(a.N);   // XCD-aware supertile order
+    int64_t t1 = 0;
+    gram_tile_range(a.N, rank, nranks, a.t0, t1);
+    a.ntiles = t1 - a.t0;
+    a.tiles = syrk_tile_order(a.N);   // XCD-aware supertile order
+    if (a.ntiles == 0) return;
     SNK_CHECK(a.K % 4 == 0 && a.ld % 4 == 0 && a.kchunk % 4 == 0, SNK_ERR_INTERNAL, "syrk: K/ld not multiples of 4");
     SNK_CHECK(a.ntiles < (int64_t)1 << 31 && z <= 65535, SNK_ERR_INVALID, "syrk: problem too large");
     dim3 grid((unsigned)a.ntiles, (unsigned)z);
@@ -355,9 +424,13 @@ extern "C" int snk_jacobian(snk_dqn m, snk_replay rb, const int64_t *slots_dev, 
     });
 }
 
-extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_dev, float *ms_out) {
-    return guard([&] {
-        SNK_CHECK(m && rb && G_dev && n > 0, SNK_ERR_INVALID, "bad argument");
+// G = J J' tiles of shard rank / nranks (all: 0 / 1), mirrored; the Jacobian
+// rows of all n samples are computed by every shard (29 ms at 50k)
+static void jacobian_gram_tiles(snk_dqn m, snk_replay rb, int64_t n, float *G_dev, float *ms_out, int rank,
+                                int nranks) {
+    {
+        SNK_CHECK(m && rb && G_dev && n > 0 && nranks >= 1 && rank >= 0 && rank < nranks, SNK_ERR_INVALID,
+                  "bad argument");
         const ReplayDev &R = replay_dev(rb);
         SNK_CHECK(R.bs == m->L.bs && R.C == m->L.C, SNK_ERR_INVALID, "replay geometry differs from the model");
         int64_t len = 0;
@@ -397,15 +470,24 @@ extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_d
             launch_check("h3_rows_kernel");
             a.xh = m->jplanes; a.xe = m->jexp; a.ldh = ldh;
         }
-        syrk_launch(SYRK_F32, a, 1, s);
+        syrk_launch(SYRK_F32, a, 1, s, rank, nranks);
         if (ms_out) SNK_HIP(hipEventRecord(ev[3], s));
         SyrkArgs d{};
         d.x = m->jw.a3; d.ld = L.K1; d.K = L.K1; d.kchunk = L.K1; d.N = (int)n; d.g32 = G_dev; d.ldg = n;
         d.z = m->jw.dz1; d.hh = m->jw.h1; d.act = m->jact; d.ldz = 64;
-        syrk_launch(SYRK_DENSE_ADD, d, 1, s);
-        const unsigned nb = (unsigned)ceil_div(n, 64);
-        mirror_kernel<<<dim3(nb, nb), 256, 0, s>>>(G_dev, (int)n, n);
-        launch_check("mirror_kernel");
+        syrk_launch(SYRK_DENSE_ADD, d, 1, s, rank, nranks);
+        if (nranks == 1) {
+            const unsigned nb = (unsigned)ceil_div(n, 64);
+            mirror_kernel<<<dim3(nb, nb), 256, 0, s>>>(G_dev, (int)n, n);
+            launch_check("mirror_kernel");
+        } else {
+            int64_t t0, t1;
+            gram_tile_range(n, rank, nranks, t0, t1);
+            if (t1 > t0) {
+                mirror_tiles_kernel<<<(unsigned)(t1 - t0), 256, 0, s>>>(G_dev, (int)n, n, syrk_tile_order((int)n), t0);
+                launch_check("mirror_tiles_kernel");
+            }
+        }
         if (ms_out) {
             SNK_HIP(hipEventRecord(ev[4], s));
             SNK_HIP(hipEventSynchronize(ev[4]));
@@ -414,6 +496,81 @@ extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_d
         } else {
             SNK_HIP(hipStreamSynchronize(s));
         }
+    }
+}
+
+extern "C" int snk_jacobian_gram(snk_dqn m, snk_replay rb, int64_t n, float *G_dev, float *ms_out) {
+    return guard([&] { jacobian_gram_tiles(m, rb, n, G_dev, ms_out, 0, 1); });
+}
+
+extern "C" int snk_jacobian_gram_shard(snk_dqn m, snk_replay rb, int64_t n, int32_t rank, int32_t nranks,
+                                       float *G_dev, float *ms_out) {
+    return guard([&] { jacobian_gram_tiles(m, rb, n, G_dev, ms_out, rank, nranks); });
+}
+
+extern "C" int snk_gram_tiles(int64_t n, int32_t rank, int32_t nranks, int32_t *tiles_host, int64_t *count_out) {
+    return guard([&] {
+        SNK_CHECK(n > 0 && nranks >= 1 && rank >= 0 && rank < nranks && count_out, SNK_ERR_INVALID, "bad argument");
+        int64_t t0, t1;
+        gram_tile_range(n, rank, nranks, t0, t1);
+        *count_out = t1 - t0;
+        if (!tiles_host) return;
+        const std::vector<int2> order = syrk_tile_order_host((int)n);
+        for (int64_t t = t0; t < t1; ++t) {
+            tiles_host[2 * (t - t0)] = order[t].x * SY_T;
+            tiles_host[2 * (t - t0) + 1] = order[t].y * SY_T;
+        }
+    });
+}
+
+namespace snk {
+void comm_gather_to_root(snk_comm h, const float *send, int64_t n_send, float *const *recv, const int64_t *n_recv,
+                         int root, hipStream_t s);
+int comm_rank(snk_comm h);
+int comm_size(snk_comm h);
+}
+
+extern "C" int snk_jacobian_gram_gather(snk_comm c, int64_t n, float *G_dev, int32_t root) {
+    return guard([&] {
+        SNK_CHECK(c && G_dev && n > 0, SNK_ERR_INVALID, "bad argument");
+        const int R = comm_size(c), me = comm_rank(c);
+        SNK_CHECK(root >= 0 && root < R, SNK_ERR_INVALID, "bad root");
+        if (R == 1) return;
+        hipStream_t s = stream();
+        const int2 *tiles = syrk_tile_order((int)n);
+        constexpr int64_t TF = 128 * 128;
+        int64_t t0, t1;
+        if (me != root) {
+            gram_tile_range(n, me, R, t0, t1);
+            DevBuf<float> buf((size_t)std::max<int64_t>(t1 - t0, 1) * TF);
+            if (t1 > t0) {
+                gram_pack_kernel<<<(unsigned)(t1 - t0), 256, 0, s>>>(G_dev, (int)n, n, tiles, t0, buf);
+                launch_check("gram_pack_kernel");
+            }
+            comm_gather_to_root(c, buf, (t1 - t0) * TF, nullptr, nullptr, root, s);
+            SNK_HIP(hipStreamSynchronize(s));
+            return;
+        }
+        std::vector<DevBuf<float>> bufs(R);
+        std::vector<float *> rp(R, nullptr);
+        std::vector<int64_t> rn(R, 0);
+        for (int r = 0; r < R; ++r) {
+            if (r == root) continue;
+            gram_tile_range(n, r, R, t0, t1);
+            bufs[r] = DevBuf<float>((size_t)std::max<int64_t>(t1 - t0, 1) * TF);
+            rp[r] = bufs[r];
+            rn[r] = (t1 - t0) * TF;
+        }
+        comm_gather_to_root(c, nullptr, 0, rp.data(), rn.data(), root, s);
+        for (int r = 0; r < R; ++r) {
+            if (r == root) continue;
+            gram_tile_range(n, r, R, t0, t1);
+            if (t1 > t0) {
+                gram_unpack_kernel<<<(unsigned)(t1 - t0), 256, 0, s>>>(G_dev, (int)n, n, tiles, t0, rp[r]);
+                launch_check("gram_unpack_kernel");
+            }
+        }
+        SNK_HIP(hipStreamSynchronize(s));
     });
 }
 

@@ -321,7 +321,8 @@ struct SyrkArgs {
     const float *x;
     int64_t ld, K, kchunk;   // reduction range of split z: [z*kchunk, min(K, (z+1)*kchunk))
     int N;
-    int64_t ntiles;
+    int64_t ntiles;          // tiles of this launch: [t0, t0 + ntiles) of the order
+    int64_t t0;
     const int2 *tiles;       // optional tile order (bi, bj), indexed by the XCD remap; null: row-major
     float *g32;              // SYRK_F32 / SYRK_DENSE_ADD: G [N][ldg]
     double *g64;             // SYRK_SLAB64: slab [z][N][N]
@@ -396,7 +397,7 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
     __shared__ __attribute__((aligned(16))) uint16_t lds[SH_BUF * 2 * 2 * SY_T * SH_ROW];   // 128 KB
     int bi, bj;
     {
-        const int64_t t = syrk_xcd_remap(blockIdx.x, a.ntiles);
+        const int64_t t = a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
         if (a.tiles) {
             const int2 tb = a.tiles[t];
             bi = tb.x;
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
     SyrkLds &s = sm.f32;
     int bi, bj;
     {
-        const int64_t t = syrk_xcd_remap(blockIdx.x, a.ntiles);
+        const int64_t t = a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
         if (a.tiles) {
             const int2 tb = a.tiles[t];
             bi = tb.x;

@@ -199,6 +199,32 @@ def jacobian_gram(model: DQNModel, buf: ReplayBuffer, n: int | None = None, *, o
     return (G.numpy() if host else G), t
 
 
+def gram_tiles(n: int, rank: int = 0, nranks: int = 1) -> np.ndarray:
+    """The 128 x 128 lower-triangle tiles of the n x n Gram that shard
+    rank / nranks computes: [count, 2] top-left (row, col) elements, a
+    contiguous run of the XCD-aware supertile order (host only)."""
+    cnt = C.c_int64(0)
+    call("snk_gram_tiles", int(n), int(rank), int(nranks), None, C.byref(cnt))
+    out = np.zeros((cnt.value, 2), np.int32)
+    call("snk_gram_tiles", int(n), int(rank), int(nranks), _lib.ptr(out), C.byref(cnt))
+    return out
+
+
+def jacobian_gram_shard(model: DQNModel, buf: ReplayBuffer, n: int, rank: int, nranks: int,
+                        out: DeviceArray) -> list:
+    """This rank's tiles (and their mirror) of G = J J' over slots 0..n-1
+    written into `out` (a device [n, n] float32 array; other entries are left
+    as they are). Returns the 4 phase times (ms)."""
+    ms = (C.c_float * 4)()
+    call("snk_jacobian_gram_shard", model.handle, buf.handle, int(n), int(rank), int(nranks), out.ptr, ms)
+    return [float(v) for v in ms]
+
+
+def jacobian_gram_gather(comm, n: int, out: DeviceArray, root: int = 0) -> None:
+    """Collective: every rank's shard tiles onto root's `out` (RCCL send/recv)."""
+    call("snk_jacobian_gram_gather", comm.handle, int(n), out.ptr, int(root))
+
+
 def d_build_seconds(ms) -> float:
     """Wall time of one Jacobian-Gram D build from its phase times."""
     return sum(ms) / 1e3 if ms else math.nan

@@ -300,3 +300,34 @@ def test_laplace_sampling_wraps_small_buffer(snk):
     got = snk.stack_exp(small.buffer, slots)
     for k in ("states", "next_states", "actions", "rewards", "dones", "suicidal_mask"):
         assert np.array_equal(got[k], ref[k]), k
+
+
+def test_jacobian_gram_shards_reassemble_bitexact(snk):
+    """D(50k) across ranks, one device: the three shards of a 3-rank split,
+    each into its own zeroed G, hold disjoint tiles (+ mirror) whose sum is
+    the single-launch Gram bit for bit (a tile's arithmetic does not depend on
+    which launch computes it); n = 700 leaves a partial last tile row."""
+    bs, C, n = 12, 2, 700
+    _, rb = _replay(snk, bs, C)
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=29)
+    G, _ = snk.jacobian_gram(m, rb, n)
+    total = np.zeros((n, n), np.float64)
+    nz = np.zeros((n, n), np.int32)
+    for r in range(3):
+        Gr = snk.DeviceArray((n, n), np.float32)
+        Gr.zero()
+        snk.jacobian_gram_shard(m, rb, n, r, 3, Gr)
+        h = Gr.numpy()
+        total += h
+        nz += (h != 0)
+        for i0, j0 in snk.gram_tiles(n, r, 3):
+            blk = h[i0:i0 + 128, j0:j0 + 128]
+            assert np.array_equal(blk, G[i0:i0 + 128, j0:j0 + 128])
+    assert nz.max() <= 1
+    assert np.array_equal(total.astype(np.float32), G)
+    # a one-rank communicator's gather is the identity
+    comm = snk.Comm(1, 0, snk.Comm.unique_id())
+    Gd = snk.DeviceArray((n, n), np.float32)
+    Gd.upload(G)
+    snk.jacobian_gram_gather(comm, n, Gd, 0)
+    assert np.array_equal(Gd.numpy(), G)
