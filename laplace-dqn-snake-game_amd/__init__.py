@@ -19,5 +19,6 @@ from .laplace import (LaplaceD, compute_D, gram_tiles, jacobian, jacobian_gram, 
                       jacobian_gram_gather, jacobian_gram_shard, laplace_normals, laplace_sampling_,
                       sample_model)
 from .bsonio import load_trainer, read_trainer  # noqa: F401
+from . import gif  # noqa: F401
 
 __version__ = "1.0.0"
