@@ -137,6 +137,21 @@ typedef struct snk_dqn_s *snk_dqn;
  * counter RNG seeded by init_seed; RMSProp(lr, rho, eps) = (5e-4, 0.9, 1e-8). */
 int snk_dqn_create(snk_dqn *out, int32_t board_size, int32_t n_frames, float lr, float rho, float eps,
                    uint64_t init_seed);
+/* BASELINE.json configs[2]: the deeper conv Q-net in bf16 (builder-defined; the
+ * reference has none). It extends structs.jl:127-139 by one more 3x3 convolution
+ * and wider channels:
+ *   Conv(3,3,C=>32,relu;pad=1) Conv(3,3,32=>32,relu;pad=1) Conv(3,3,32=>64,relu;pad=1)
+ *   Conv(6,6,64=>64,relu) flatten Dense((bs-5)^2*64=>64,relu) Dense(64=>3)
+ * with conv / Dense1 weights and every conv activation in bf16, fp32 sums,
+ * fp32 master weights, RMSProp and head. board_size 10, 12 or 20.
+ * The handle answers every DQNModel and trainer entry point below except the
+ * Jacobian / Laplace ones and snk_dqn_time_act_layers / snk_dqn_last_q. */
+int snk_dqn_create_deep(snk_dqn *out, int32_t board_size, int32_t n_frames, float lr, float rho, float eps,
+                        uint64_t init_seed);
+/* measurement: average ms per launch of each layer of the deep net's
+ * epsilon_greedy forward over env's batch, ms_out[6] = L0 (VALU conv), L1, L2,
+ * L3 (bf16 MFMA convs), Dense1, head (HIP events on the library stream) */
+int snk_dqn_time_deep_layers(snk_dqn m, snk_env env, int32_t reps, double *ms_out);
 int snk_dqn_destroy(snk_dqn m);
 int snk_dqn_nparams(snk_dqn m, int64_t *P_out);
 /* Flux.destructure / restructure: which = SNK_NET_* */

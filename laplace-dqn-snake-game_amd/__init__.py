@@ -12,7 +12,7 @@ from .env import (ALL_ACTIONS, D, L, NULL_ACTION, R, U, SnakeGame, assemble_stat
 from .replay import (ReplayBuffer, empty_buffer_, isfull, isready, sample, stack_exp,  # noqa: F401
                      store_)
 from ._lib import SNK_NET_GRAD, SNK_NET_OPT_STATE, SNK_NET_Q, SNK_NET_TARGET  # noqa: F401
-from .qnet import DQNModel, nparams, update_target_net_  # noqa: F401
+from .qnet import DQNModel, deep_nparams, nparams, update_target_net_  # noqa: F401
 from .dist import Comm, aggregate_throughput, dist_attach, dist_detach  # noqa: F401
 from .trainer import Trainer, epsilon_greedy, fill_buffer_, play_episode, train_  # noqa: F401
 from .laplace import (LaplaceD, compute_D, gram_tiles, jacobian, jacobian_gram,  # noqa: F401

@@ -86,6 +86,8 @@ _PROTOS = {
     "snk_replay_gather": [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp],
     "snk_dqn_create": [P(vp), i32, i32, f32, f32, f32, u64],
     "snk_dqn_destroy": [vp],
+    "snk_dqn_create_deep": [P(vp), i32, i32, f32, f32, f32, u64],
+    "snk_dqn_time_deep_layers": [vp, vp, i32, vp],
     "snk_dqn_nparams": [vp, P(i64)],
     "snk_dqn_set_params": [vp, i32, vp],
     "snk_dqn_get_params": [vp, i32, vp],

@@ -1,0 +1,429 @@
+// snk_deep.hpp — the deeper bf16 Q-net of BASELINE.json configs[2] on gfx950.
+//
+// configs[2] names "65536 envs, 20x20 grid, deeper conv Q-net, bf16" with no
+// reference counterpart (builder-defined). The net extends
+// structs.jl:127-139 by one more 3x3 convolution and wider channels, with the
+// same Flux conventions (true convolution, column-major flatten):
+//   L0 Conv(3,3,C=>32,relu;pad=1)  L1 Conv(3,3,32=>32,relu;pad=1)
+//   L2 Conv(3,3,32=>64,relu;pad=1) L3 Conv(6,6,64=>64,relu)
+//   flatten -> Dense((bs-5)^2*64 => 64, relu) -> Dense(64 => 3)
+// bf16 semantics (oracle/snake_oracle.c restates them exactly): conv and
+// Dense1 weight matrices are used rounded to bf16, every conv output (after
+// bias + relu) is stored as bf16, sums accumulate in fp32 on the matrix cores;
+// biases, Dense2, the TD target / Huber head and RMSProp stay fp32 (fp64 for
+// the target, as the reference). Backward: native bf16 MFMA products with the
+// relu-masked gradient rounded to bf16 as the operand, fp32 accumulation.
+//
+// Forward kernels (activations [sample][position p = i + j*H][channel] bf16):
+//   deep_conv0_kernel  L0 on VALU (K = 9C): boards -> bf16
+//   deep_conv_kernel   L1..L3: one sample per workgroup, its whole input
+//                      staged in LDS inside a zero border, the layer's weights
+//                      streamed per kernel offset through a double-buffered
+//                      LDS tile, v_mfma_f32_16x16x32_bf16
+//   deep_dense1_kernel Dense1 on v_mfma_f32_16x16x32_bf16, K-split slabs the
+//                      shared head kernel sums (snk_qnet.hip head_launch)
+// Backward: gemm_bf16_kernel, the snk_gemm.hpp engine on
+//   v_mfma_f32_32x32x16_bf16 with the snk_loaders.hpp implicit-im2col loaders.
+#pragma once
+#include "snk_conv_x6.hpp"
+#include "snk_loaders.hpp"
+
+namespace snk {
+
+// ---------------------------------------------------------------- bf16
+__host__ __device__ inline uint16_t f2bf(float f) {   // round to nearest even
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+__host__ __device__ inline float bf2f(uint16_t b) {
+    const uint32_t u = (uint32_t)b << 16;
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+}
+
+// ---------------------------------------------------------------- layout
+struct DeepLayout {
+    int bs, C, Wo, K1;                         // K1 = Wo^2 * 64 (Dense1 fan-in)
+    int cin[4], cout[4], ks[4], pad[4];
+    int64_t off_w[4], off_b[4], off_d1w, off_d1b, off_d2w, off_d2b, P;
+    // bf16 weight image: conv L1..L3 [kk][co][ci], Dense1 [o][f]; L0 as
+    // bf16-rounded fp32 [9C][32] (VALU)
+    int64_t img_w[4], img_d1, img_n;
+    int64_t img0_n;                            // floats of the L0 image
+};
+DeepLayout deep_layout(int bs, int C);
+// a QLayout whose head offsets (off_d1b, off_d2w, off_d2b) and P are the deep
+// net's: what the shared head / Dense2-gradient kernels read
+QLayout deep_head_layout(const DeepLayout &D);
+void deep_packed_to_flux(const DeepLayout &D, int32_t *perm);
+
+// ---------------------------------------------------------------- weight image
+__global__ void deep_image_kernel(const float *__restrict__ th, uint16_t *__restrict__ img,
+                                  float *__restrict__ img0, DeepLayout D) {
+    const int64_t n = D.img_n + D.img0_n;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        if (t >= D.img_n) {   // L0: [9C][32] weights then 32 biases, weights bf16-rounded
+            const int64_t u = t - D.img_n;
+            const int64_t nw = 9LL * D.C * 32;
+            img0[u] = u < nw ? bf2f(f2bf(th[D.off_w[0] + u])) : th[D.off_b[0] + (u - nw)];
+            continue;
+        }
+        if (t >= D.img_d1) {   // Dense1 [o][f] <- packed W[f][o]
+            const int64_t u = t - D.img_d1;
+            const int64_t o = u / D.K1, f = u - o * D.K1;
+            img[t] = f2bf(th[D.off_d1w + f * 64 + o]);
+            continue;
+        }
+        int l = 1;
+        while (l < 3 && t >= D.img_w[l + 1]) ++l;
+        const int64_t u = t - D.img_w[l];
+        const int CI = D.cin[l], CO = D.cout[l];
+        const int64_t kk = u / (CI * CO);
+        const int r = (int)(u - kk * CI * CO);
+        const int co = r / CI, ci = r - co * CI;
+        img[t] = f2bf(th[D.off_w[l] + (kk * CI + ci) * CO + co]);   // packed W[(kk*CI + ci)*CO + co]
+    }
+}
+
+// ---------------------------------------------------------------- L0 (VALU)
+// 3x3, C -> 32, pad 1: NS samples per workgroup staged as floats inside a zero
+// border; one thread per output position, 32 accumulators, bf16 out (4 x 16 B).
+template <int C>
+__global__ __launch_bounds__(256) void deep_conv0_kernel(BoardSrc src, const float *__restrict__ img0,
+                                                         uint16_t *__restrict__ y, int64_t S, int bs, int NS) {
+    extern __shared__ __attribute__((aligned(16))) float d0sm[];
+    float *sw = d0sm;                       // [9C][32] + [32]
+    float *sx = d0sm + 9 * C * 32 + 32;     // [NS][C][(bs+2)^2]
+    const int bp = bs + 2, plane = bp * bp, nc = bs * bs;
+    for (int i = threadIdx.x; i < 9 * C * 32 + 32; i += blockDim.x) sw[i] = img0[i];
+    const int64_t s0 = (int64_t)blockIdx.x * NS;
+    const int ns = (int)min((int64_t)NS, S - s0);
+    for (int i = threadIdx.x; i < NS * C * plane; i += blockDim.x) sx[i] = 0.0f;
+    __syncthreads();
+    for (int e = threadIdx.x; e < ns * C * nc; e += blockDim.x) {
+        const int sc = e / nc, cell = e - sc * nc;
+        const int sl = sc / C, c = sc - sl * C;
+        const int jj = cell / bs, ii = cell - jj * bs;
+        sx[sc * plane + (ii + 1) + (jj + 1) * bp] = src.load(s0 + sl, c, cell);
+    }
+    __syncthreads();
+    const float4 *sw4 = reinterpret_cast<const float4 *>(sw);
+    for (int q = threadIdx.x; q < ns * nc; q += blockDim.x) {
+        const int sl = q / nc, p = q - sl * nc;
+        const int j = p / bs, i = p - j * bs;
+        float acc[32];
+#pragma unroll
+        for (int v4 = 0; v4 < 8; ++v4) {
+            const float4 b4 = sw4[9 * C * 8 + v4];
+            acc[4 * v4] = b4.x; acc[4 * v4 + 1] = b4.y; acc[4 * v4 + 2] = b4.z; acc[4 * v4 + 3] = b4.w;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 9; ++kk) {
+            const int du = kk % 3, dv = kk / 3;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const float v = sx[(sl * C + c) * plane + (i + du) + (j + dv) * bp];
+#pragma unroll
+                for (int v4 = 0; v4 < 8; ++v4) {
+                    const float4 w4 = sw4[(kk * C + c) * 8 + v4];
+                    acc[4 * v4] = __builtin_fmaf(v, w4.x, acc[4 * v4]);
+                    acc[4 * v4 + 1] = __builtin_fmaf(v, w4.y, acc[4 * v4 + 1]);
+                    acc[4 * v4 + 2] = __builtin_fmaf(v, w4.z, acc[4 * v4 + 2]);
+                    acc[4 * v4 + 3] = __builtin_fmaf(v, w4.w, acc[4 * v4 + 3]);
+                }
+            }
+        }
+        u32x4 o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t w[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a = fmaxf(acc[8 * k + 2 * e], 0.f), b = fmaxf(acc[8 * k + 2 * e + 1], 0.f);
+                w[e] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+            }
+            o[k] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+        u32x4 *dst = reinterpret_cast<u32x4 *>(y + ((s0 + sl) * nc + p) * 32);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k] = o[k];
+    }
+}
+
+// ---------------------------------------------------------------- L1..L3 (MFMA)
+// One workgroup = one sample, NW waves. LDS: the sample's input [HB][HB][CIN]
+// bf16 at a CST = CIN + 8 position stride (16-byte A reads of 16 consecutive
+// positions land on distinct banks), the zero border written explicitly; the
+// weights of one kernel offset [COUT][CIN + 8] double buffered, the next
+// offset's tile loaded into registers during this offset's MFMAs (one barrier
+// per offset). Wave w owns row tiles w, w + NW, ... of the HO^2 output
+// positions, all COUT / 16 column tiles: per offset and 32-channel chunk one
+// B fragment per column tile, then per row tile one A fragment and COUT / 16
+// MFMAs. Epilogue: bias + relu + bf16, straight to [S][HO^2][COUT].
+template <int CIN, int COUT, int KS, int PAD, int H>
+struct DeepConvShape {
+    static constexpr int HB = H + 2 * PAD, HO = H + 2 * PAD - KS + 1, CST = CIN + 8, BST = CIN + 8;
+    static constexpr int M = HO * HO, TILES = (M + 15) / 16, NT = COUT / 16, KC = CIN / 32;
+    static constexpr int A_ELEMS = HB * HB * CST, B_ELEMS = COUT * BST;
+    static constexpr int LDS = (A_ELEMS + 2 * B_ELEMS) * 2;
+    static constexpr int BCH = COUT * CIN / 8;   // 16-byte chunks of one offset's weights
+};
+
+template <int CIN, int COUT, int KS, int PAD, int H, int NW>
+__global__ __launch_bounds__(64 * NW) void deep_conv_kernel(const uint16_t *__restrict__ x,
+                                                            const uint16_t *__restrict__ wimg,
+                                                            const float *__restrict__ bias,
+                                                            uint16_t *__restrict__ y) {
+    using Sh = DeepConvShape<CIN, COUT, KS, PAD, H>;
+    constexpr int HB = Sh::HB, HO = Sh::HO, CST = Sh::CST, BST = Sh::BST, M = Sh::M, NT = Sh::NT, KC = Sh::KC;
+    constexpr int TPW = (Sh::TILES + NW - 1) / NW;
+    constexpr int NTH = 64 * NW, BPT = (Sh::BCH + NTH - 1) / NTH;
+    extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
+    uint16_t *As = dsm;
+    uint16_t *Bs = dsm + Sh::A_ELEMS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t s = blockIdx.x;
+    // ---- stage the input (interior) and zero the border positions
+    {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(x + s * (int64_t)H * H * CIN);
+        constexpr int NCH = H * H * CIN / 8, CPP = CIN / 8;
+        for (int q = tid; q < NCH; q += NTH) {
+            const int p = q / CPP, part = q - p * CPP;
+            const int jj = p / H, ii = p - jj * H;
+            *reinterpret_cast<u32x4 *>(As + ((ii + PAD) + (jj + PAD) * HB) * CST + part * 8) = src[q];
+        }
+        if constexpr (PAD > 0) {
+            constexpr int NB = HB * HB - H * H;   // border positions
+            const u32x4 z = {0u, 0u, 0u, 0u};
+            for (int q = tid; q < NB * CPP; q += NTH) {
+                const int b = q / CPP, part = q - b * CPP;
+                int bi, bj;   // b enumerates the top row, the bottom row, then the left/right columns
+                if (b < HB) { bi = b; bj = 0; }
+                else if (b < 2 * HB) { bi = b - HB; bj = HB - 1; }
+                else { const int t = b - 2 * HB; bj = 1 + (t >> 1); bi = (t & 1) ? HB - 1 : 0; }
+                *reinterpret_cast<u32x4 *>(As + (bi + bj * HB) * CST + part * 8) = z;
+            }
+        }
+    }
+    // ---- stage offset 0's weights
+    u32x4 breg[BPT];
+    auto bload = [&](int kk) {
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(wimg + (int64_t)kk * COUT * CIN);
+#pragma unroll
+        for (int u = 0; u < BPT; ++u) {
+            const int q = tid + u * NTH;
+            if (q < Sh::BCH) breg[u] = src[q];
+        }
+    };
+    auto bstore = [&](int buf) {
+        uint16_t *dst = Bs + buf * Sh::B_ELEMS;
+#pragma unroll
+        for (int u = 0; u < BPT; ++u) {
+            const int q = tid + u * NTH;
+            if (q < Sh::BCH) {
+                const int co = q / (CIN / 8), part = q - co * (CIN / 8);
+                *reinterpret_cast<u32x4 *>(dst + co * BST + part * 8) = breg[u];
+            }
+        }
+    };
+    bload(0);
+    bstore(0);
+    // ---- per row tile: bordered base position of this lane's A row
+    int abase[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        int row = (wave + t * NW) * 16 + r;
+        row = row < M ? row : M - 1;
+        const int j = row / HO, i = row - j * HO;
+        abase[t] = (i + j * HB) * CST + g * 8;
+    }
+    f32x4 acc[TPW][NT];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    for (int kk = 0; kk < KS * KS; ++kk) {
+        if (kk + 1 < KS * KS) bload(kk + 1);
+        const int du = kk % KS, dv = kk / KS;
+        const int koff = (du + dv * HB) * CST;
+        const uint16_t *Bc = Bs + (kk & 1) * Sh::B_ELEMS + r * BST + g * 8;
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+            bf16x8 bf[NT];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) bf[nt] = as_bf(*reinterpret_cast<const u32x4 *>(Bc + nt * 16 * BST + c * 32));
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                if ((wave + t * NW) < Sh::TILES) {
+                    const bf16x8 a = as_bf(*reinterpret_cast<const u32x4 *>(As + abase[t] + koff + c * 32));
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bf[nt], acc[t][nt], 0, 0, 0);
+                }
+            }
+        }
+        if (kk + 1 < KS * KS) bstore((kk + 1) & 1);
+        __syncthreads();
+    }
+    // ---- epilogue: C[row 4g + e][col nt*16 + r]
+    uint16_t *ys = y + s * (int64_t)M * COUT;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int col = nt * 16 + r;
+        const float b = bias[col];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = (wave + t * NW) * 16 + 4 * g + e;
+                if (row < M) ys[row * COUT + col] = f2bf(fmaxf(acc[t][nt][e] + b, 0.f));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- Dense1
+// slab[z][s][o] = sum_{f in split z} a4[s][f] * W1[f][o]; 4 waves x 16 samples
+// per workgroup, all 64 outputs (4 column tiles); A and B fragments straight
+// from global (the 1.8 MB bf16 image stays L2-resident), two k-steps in flight.
+__global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__restrict__ a4,
+                                                          const uint16_t *__restrict__ w1img, int64_t S, int K1,
+                                                          int kchunk, float *__restrict__ slab) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t row0 = (int64_t)blockIdx.x * 64 + wave * 16;
+    const int64_t srow = min(row0 + r, S - 1);
+    const int k0 = blockIdx.y * kchunk, k1 = min(K1, k0 + kchunk);
+    const uint16_t *pa = a4 + srow * K1 + g * 8;
+    const uint16_t *pb = w1img + (int64_t)r * K1 + g * 8;
+    f32x4 acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int k = k0;
+    for (; k + 64 <= k1; k += 64) {
+        u32x4 a[2], b[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            a[u] = *reinterpret_cast<const u32x4 *>(pa + k + 32 * u);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) b[u][nt] = *reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + k + 32 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+                acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a[u]), as_bf(b[u][nt]), acc[nt], 0, 0, 0);
+    }
+    for (; k < k1; k += 32) {
+        const u32x4 a = *reinterpret_cast<const u32x4 *>(pa + k);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                as_bf(a), as_bf(*reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + k)), acc[nt], 0, 0, 0);
+    }
+    float *o = slab + (int64_t)blockIdx.y * S * 64;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t row = row0 + 4 * g + e;
+            if (row < S) o[row * 64 + nt * 16 + r] = acc[nt][e];
+        }
+}
+
+// ---------------------------------------------------------------- backward engine (bf16)
+// gemm_body (snk_gemm.hpp) on v_mfma_f32_32x32x16_bf16: lane (r = l & 31,
+// h = l >> 5) holds A[row r][k + 8h + j] and B[k + 8h + j][col r], j < 8;
+// every loaded operand is rounded to bf16 (RNE), sums accumulate in fp32.
+// KW waves split K and sum through LDS; grid.z K-splits write slabs (EpSlab).
+template <int NT, int KW, class AL, class BL, class EP>
+__global__ __launch_bounds__(64 * KW) void gemm_bf16_kernel(AL al, BL bl, EP ep, int M, int K, int kchunk) {
+    __shared__ float red[KW > 1 ? KW * NT * 16 * 64 : 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int m0 = blockIdx.x * 32;
+    const int r = lane & 31, h = lane >> 5;
+    const int n0 = blockIdx.y * (NT * 32);
+    const int kb = blockIdx.z * kchunk;
+    const int ke = min(K, kb + kchunk);
+    const int sub = (((ke - kb) + KW - 1) / KW + 15) & ~15;
+    const int wb = kb + wave * sub;
+    const int we = min(ke, wb + sub);
+    f32x16 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[nt][e] = 0.0f;
+    const auto ctx = al.row(m0 + r, M);
+    for (int k = wb; k < we; k += 16) {
+        uint32_t aw[4], bw[NT][4];
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+            const int k0 = k + 8 * h + j, k1 = k0 + 1;
+            const float a0 = k0 < we ? al.load(ctx, k0, we) : 0.0f, a1 = k1 < we ? al.load(ctx, k1, we) : 0.0f;
+            aw[j / 2] = (uint32_t)f2bf(a0) | ((uint32_t)f2bf(a1) << 16);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int n = n0 + nt * 32 + r;
+                const float b0 = k0 < we ? bl.load(k0, n, we) : 0.0f, b1 = k1 < we ? bl.load(k1, n, we) : 0.0f;
+                bw[nt][j / 2] = (uint32_t)f2bf(b0) | ((uint32_t)f2bf(b1) << 16);
+            }
+        }
+        const bf16x8 av = as_bf(u32x4{aw[0], aw[1], aw[2], aw[3]});
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, as_bf(u32x4{bw[nt][0], bw[nt][1], bw[nt][2], bw[nt][3]}),
+                                                             acc[nt], 0, 0, 0);
+    }
+    if (KW > 1) {
+        float *dst = red + wave * NT * 16 * 64;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) dst[(nt * 16 + e) * 64 + lane] = acc[nt][e];
+        __syncthreads();
+        if (m0 >= M) return;
+        for (int e = threadIdx.x; e < NT * 16 * 64; e += 64 * KW) {
+            float v = red[e];
+#pragma unroll
+            for (int w = 1; w < KW; ++w) v += red[w * NT * 16 * 64 + e];
+            const int nt = e >> 10, gg = (e >> 6) & 15, ln = e & 63;
+            ep.store1(v, m0 + acc_row(gg, ln), n0 + nt * 32 + (ln & 31), (int)blockIdx.z);
+        }
+        return;
+    }
+    if (m0 >= M) return;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) ep.store(acc[nt], m0, n0 + nt * 32, lane, (int)blockIdx.z);
+}
+
+struct EpReluMaskB {  // y = (bf16 act > 0) ? acc : 0
+    float *y;
+    const uint16_t *act;
+    int64_t M;
+    int N;
+    __device__ void store1(float v, int row, int col, int) const {
+        if (row >= M || col >= N) return;
+        const int64_t o = (int64_t)row * N + col;
+        y[o] = bf2f(act[o]) > 0.0f ? v : 0.0f;
+    }
+    __device__ void store(const f32x16 &acc, int m0, int c0, int lane, int) const {
+        const int col = c0 + (lane & 31);
+        if (col >= N) return;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int row = m0 + acc_row(e, lane);
+            if (row < M) {
+                const int64_t o = (int64_t)row * N + col;
+                y[o] = bf2f(act[o]) > 0.0f ? acc[e] : 0.0f;
+            }
+        }
+    }
+};
+
+}  // namespace snk

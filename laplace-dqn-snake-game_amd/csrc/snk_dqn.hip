@@ -43,6 +43,10 @@ void dqn_permute(snk_dqn_s *h, const float *src, float *dst, bool to_packed, hip
 }
 
 void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, hipStream_t s) {
+    if (h->deep) {
+        deep_sync_target(h, counter, rate, s);
+        return;
+    }
     copy_if_due_kernel<<<(unsigned)std::min<int64_t>(ceil_div(h->L.P, 256), 2048), 256, 0, s>>>(
         h->theta_q, h->theta_t, h->L.P, counter, rate);
     launch_check("copy_if_due_kernel");
@@ -57,7 +61,12 @@ void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, 
     }
 }
 
-void dqn_q_changed(snk_dqn_s *h, hipStream_t s) { transpose_fwd_launch(h->L, h->theta_q, h->wt_q, h->wtb_q, s); }
+void dqn_q_changed(snk_dqn_s *h, hipStream_t s) {
+    if (h->deep)
+        deep_q_changed(h, s);
+    else
+        transpose_fwd_launch(h->L, h->theta_q, h->wt_q, h->wtb_q, s);
+}
 
 static const float *which_wt(snk_dqn_s *h, int32_t which) {
     return which == SNK_NET_TARGET ? h->wt_t : h->wt_q;
@@ -98,6 +107,11 @@ BoardSrc src_float(const QLayout &L, const float *x) {
 // target forward on s', online forward on s with the Huber head, backward.
 void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, const HeadArgs &meta, int64_t B,
                    double gamma, hipStream_t s, const LossOpts &o) {
+    if (h->deep) {   // the deeper bf16 net finishes its gradient itself (o.defer unused)
+        deep_loss_grad(h, s_src, sn_src, meta, B, gamma, s, o.loss_mean);
+        if (o.defer) *o.defer = GradSlabs{};
+        return;
+    }
     qwork_ensure(h->tgt, h->L, B, false);
     qwork_ensure(h->trn, h->L, B, true);
     const int64_t need = qnet_backward_slab_floats(h->L, B);
@@ -215,6 +229,7 @@ extern "C" int snk_dqn_destroy(snk_dqn h) {
     return guard([&] {
         if (!h) return;
         (void)hipStreamSynchronize(stream());
+        deep_free(h);
         qwork_free(h->act);
         qwork_free(h->tgt);
         qwork_free(h->trn);
@@ -254,7 +269,12 @@ extern "C" int snk_dqn_set_params(snk_dqn h, int32_t which, const float *flux_ho
         SNK_HIP(hipMemcpyAsync(h->tmp, flux_host, h->L.P * 4, hipMemcpyHostToDevice, s));
         dqn_permute(h, h->tmp, dst, true, s);
         if (which == SNK_NET_Q) dqn_q_changed(h, s);
-        if (which == SNK_NET_TARGET) transpose_fwd_launch(h->L, h->theta_t, h->wt_t, h->wtb_t, s);
+        if (which == SNK_NET_TARGET) {
+            if (h->deep)
+                deep_t_changed(h, s);
+            else
+                transpose_fwd_launch(h->L, h->theta_t, h->wt_t, h->wtb_t, s);
+        }
         SNK_HIP(hipStreamSynchronize(s));
     });
 }
@@ -289,6 +309,11 @@ extern "C" int snk_dqn_forward(snk_dqn h, int32_t which, const float *x_dev, int
         SNK_CHECK(h && x_dev && q_dev && B > 0, SNK_ERR_INVALID, "bad forward arguments");
         SNK_CHECK(which == SNK_NET_Q || which == SNK_NET_TARGET, SNK_ERR_INVALID, "forward needs q or target net");
         hipStream_t s = stream();
+        if (h->deep) {
+            const float *q = deep_forward(h, which, src_float(h->L, x_dev), B, HEAD_Q, HeadArgs{}, s);
+            SNK_HIP(hipMemcpyAsync(q_dev, q, B * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+            return;
+        }
         qwork_ensure(h->act, h->L, B, false);
         qnet_forward(h->L, which_buf(h, which), which_wt(h, which), src_float(h->L, x_dev), B, h->act, HEAD_Q,
                      HeadArgs{}, s, -1, which_wtb(h, which));
@@ -302,6 +327,11 @@ extern "C" int snk_dqn_forward_env(snk_dqn h, int32_t which, snk_env env, float 
         const EnvDev &E = env_dev(env);
         SNK_CHECK(E.bs == h->L.bs && E.C == h->L.C, SNK_ERR_INVALID, "env/model geometry mismatch");
         hipStream_t s = stream();
+        if (h->deep) {
+            const float *q = deep_forward(h, which, src_env(E), E.n, HEAD_Q, HeadArgs{}, s);
+            SNK_HIP(hipMemcpyAsync(q_dev, q, E.n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s));
+            return;
+        }
         qwork_ensure(h->act, h->L, E.n, false);
         qnet_forward(h->L, which_buf(h, which), which_wt(h, which), src_env(E), E.n, h->act, HEAD_Q, HeadArgs{}, s,
                      -1, which_wtb(h, which));
@@ -315,12 +345,16 @@ extern "C" int snk_dqn_act(snk_dqn h, snk_env env, float epsilon, uint64_t seed,
         const EnvDev &E = env_dev(env);
         SNK_CHECK(E.bs == h->L.bs && E.C == h->L.C, SNK_ERR_INVALID, "env/model geometry mismatch");
         hipStream_t s = stream();
-        qwork_ensure(h->act, h->L, E.n, false);
         HeadArgs ha;
         ha.act = act_dev;
         ha.epsilon = epsilon;
         ha.seed = seed;
         ha.tptr = &E.ctl->t;
+        if (h->deep) {
+            deep_forward(h, SNK_NET_Q, src_env(E), E.n, HEAD_ACT, ha, s);
+            return;
+        }
+        qwork_ensure(h->act, h->L, E.n, false);
         qnet_forward(h->L, h->theta_q, h->wt_q, src_env(E), E.n, h->act, HEAD_ACT, ha, s, -1, h->wtb_q);
     });
 }
@@ -328,6 +362,7 @@ extern "C" int snk_dqn_act(snk_dqn h, snk_env env, float epsilon, uint64_t seed,
 extern "C" int snk_dqn_time_act_layers(snk_dqn h, snk_env env, int32_t reps, double *ms_out) {
     return guard([&] {
         SNK_CHECK(h && env && ms_out && reps > 0, SNK_ERR_INVALID, "bad time_act_layers arguments");
+        SNK_CHECK(!h->deep, SNK_ERR_INVALID, "deep net: use snk_dqn_time_deep_layers");
         const EnvDev &E = env_dev(env);
         SNK_CHECK(E.bs == h->L.bs && E.C == h->L.C, SNK_ERR_INVALID, "env/model geometry mismatch");
         hipStream_t s = stream();
@@ -370,7 +405,7 @@ extern "C" int snk_dqn_time_act_layers(snk_dqn h, snk_env env, int32_t reps, dou
 
 extern "C" int snk_dqn_last_q(snk_dqn h, float *q_host, int64_t n) {
     return guard([&] {
-        SNK_CHECK(h && q_host && n >= 0 && n <= h->act.cap, SNK_ERR_INVALID, "bad last_q arguments");
+        SNK_CHECK(h && q_host && n >= 0 && n <= h->act.cap && !h->deep, SNK_ERR_INVALID, "bad last_q arguments");
         SNK_HIP(hipMemcpyAsync(q_host, h->act.q, n * 3 * sizeof(float), hipMemcpyDeviceToHost, stream()));
         SNK_HIP(hipStreamSynchronize(stream()));
     });
@@ -427,6 +462,10 @@ extern "C" int snk_dqn_loss_grad_batch(snk_dqn h, const float *states, const int
 extern "C" int snk_dqn_apply_grad(snk_dqn h) {
     return guard([&] {
         SNK_CHECK(h, SNK_ERR_INVALID, "NULL argument");
+        if (h->deep) {
+            deep_apply(h, nullptr, 1, stream());
+            return;
+        }
         const UpdateTarget u = dqn_update_target(h, nullptr, 1);   // RMSProp + forward image, one pass
         grad_update_launch(h->L, nullptr, h->grad, &u, stream());
     });

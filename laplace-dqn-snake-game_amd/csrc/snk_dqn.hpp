@@ -2,6 +2,10 @@
 #pragma once
 #include "snk_qnet.hpp"
 
+namespace snk {
+struct DeepNet;   // the configs[2] bf16 net (snk_deep.hip)
+}
+
 struct snk_dqn_s {
     snk::QLayout L{};
     float lr = 5e-4f, rho = 0.9f, eps = 1e-8f;
@@ -25,6 +29,8 @@ struct snk_dqn_s {
     int64_t jplanes_halves = 0, jexp_cap = 0;
     int64_t *jidx = nullptr;
     uint8_t *jact = nullptr;
+    // snk_dqn_create_deep: the deeper bf16 net; L then holds its head offsets and P only
+    snk::DeepNet *deep = nullptr;
 };
 
 namespace snk {
@@ -49,6 +55,26 @@ void dqn_sync_target_launch(snk_dqn_s *h, const int64_t *counter, int64_t rate, 
 void dqn_permute(snk_dqn_s *h, const float *src, float *dst, bool to_packed, hipStream_t s);
 // q_net parameters changed: rebuild its forward weight image
 void dqn_q_changed(snk_dqn_s *h, hipStream_t s);
+// ---- the deeper bf16 net (snk_deep.hip), dispatched to when h->deep is set
+void deep_create(snk_dqn_s *h, int bs, int C, uint64_t seed);
+void deep_free(snk_dqn_s *h);
+int64_t deep_ws_gen(const snk_dqn_s *h);
+void deep_q_changed(snk_dqn_s *h, hipStream_t s);
+void deep_t_changed(snk_dqn_s *h, hipStream_t s);
+void deep_sync_target(snk_dqn_s *h, const int64_t *counter, int64_t rate, hipStream_t s);
+// workspaces for an acting batch of S_act and / or a training batch of B (0: none)
+void deep_prepare(snk_dqn_s *h, int64_t S_act, int64_t B);
+// forward + head of q_net / t_net over S samples; returns the device Q [S][3]
+const float *deep_forward(snk_dqn_s *h, int32_t which, const BoardSrc &src, int64_t S, HeadMode mode,
+                          const HeadArgs &ha, hipStream_t s);
+void deep_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, const HeadArgs &meta, int64_t B,
+                    double gamma, hipStream_t s, bool loss_mean);
+const double *deep_batch_losses(snk_dqn_s *h);
+// RMSProp on the finished gradient, weight images, update_target_net! when *counter % rate == 0
+void deep_apply(snk_dqn_s *h, const int64_t *counter, int64_t rate, hipStream_t s);
+
 // generation of every buffer a captured trainer graph points into
-inline int64_t dqn_ws_gen(const snk_dqn_s *h) { return h->act.gen + h->tgt.gen + h->trn.gen + h->slab_gen; }
+inline int64_t dqn_ws_gen(const snk_dqn_s *h) {
+    return h->act.gen + h->tgt.gen + h->trn.gen + h->slab_gen + deep_ws_gen(h);
+}
 }  // namespace snk

@@ -162,6 +162,15 @@ struct UpdateTarget {
 void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
                         hipStream_t s);
 int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S);
+// raw launchers shared with the deeper net (snk_deep.hip): the head kernels read
+// only L.off_d1b / off_d2w / off_d2b; slab = ks partial Dense1 pre-activations [ks][S][64]
+void head_launch(const QLayout &L, const float *th, const float *slab, int ks, int64_t S, float *h1, float *q,
+                 HeadMode mode, const HeadArgs &ha, hipStream_t s);
+void head_pair_launch(const QLayout &L, const float *th_t, const float *slab_t, float *h1_t, float *q_t,
+                      const float *th_q, const float *slab_q, float *h1_q, float *q_q, int ks, int64_t S,
+                      const HeadArgs &ha, hipStream_t s);
+void d2_grad_launch(const float *dq, const float *h1, int64_t S, const QLayout &L, float *grad, hipStream_t s);
+void slab_reduce_launch(const float *slab, int ks, int64_t MN, float *out, hipStream_t s);
 // per-sample Jacobian rows J[s] = dQ(x_s)[a_s]/dtheta (packed order, row
 // stride ldJ), a_s = act[idx[s]] % 3 (written to act_out). The conv sections
 // [0, off_d1w) always; the Dense sections only with dense = true. ev_chain

@@ -158,7 +158,10 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     ha.seed = h->cfg.seed;
     ha.tptr = &E.ctl->t;
     ha.eps_dev = &h->stats->epsilon;
-    qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q);
+    if (q->deep)
+        deep_forward(q, SNK_NET_Q, src_env(E), E.n, HEAD_ACT, ha, s);
+    else
+        qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q);
     env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s);
     episode_stats_kernel<<<1, 1024, 0, s>>>(E.out_done, E.out_ep_reward, E.out_score, E.n, h->stats, E.ctl,
                                             R.count);
@@ -177,17 +180,22 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
         lo.defer = &pend;
         lo.loss_mean = false;
         dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s, lo);
-        // one pass: finish the gradient, RMSProp, forward image, update_target_net! when nb % rate == 0
-        const UpdateTarget ut = dqn_update_target(q, &h->stats->nb, h->cfg.target_update_rate);
-        if (h->comm) {   // data-parallel replicas: mean gradient before the step
-            grad_update_launch(q->L, &pend, q->grad, nullptr, s);
-            comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
-            grad_update_launch(q->L, nullptr, q->grad, &ut, s);
+        if (q->deep) {   // the deeper bf16 net: finished gradient, [mean over ranks], RMSProp + images + target
+            if (h->comm) comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
+            deep_apply(q, &h->stats->nb, h->cfg.target_update_rate, s);
         } else {
-            grad_update_launch(q->L, &pend, q->grad, &ut, s);
+            // one pass: finish the gradient, RMSProp, forward image, update_target_net! when nb % rate == 0
+            const UpdateTarget ut = dqn_update_target(q, &h->stats->nb, h->cfg.target_update_rate);
+            if (h->comm) {   // data-parallel replicas: mean gradient before the step
+                grad_update_launch(q->L, &pend, q->grad, nullptr, s);
+                comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
+                grad_update_launch(q->L, nullptr, q->grad, &ut, s);
+            } else {
+                grad_update_launch(q->L, &pend, q->grad, &ut, s);
+            }
         }
-        post_update_kernel<<<1, 256, 0, s>>>(h->stats, q->trn.loss, h->B, q->loss_dev, h->loss_log, h->log_cap,
-                                             h->cfg.decay, h->cfg.epsilon_end);
+        post_update_kernel<<<1, 256, 0, s>>>(h->stats, q->deep ? deep_batch_losses(q) : q->trn.loss, h->B, q->loss_dev,
+                                             h->loss_log, h->log_cap, h->cfg.decay, h->cfg.epsilon_end);
         launch_check("post_update_kernel");
     }
 }
@@ -227,10 +235,14 @@ extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, sn
         SNK_HIP(hipMemsetAsync(h->act, 0, E.n, s));
         SNK_HIP(hipMemsetAsync(h->idx, 0, h->B * sizeof(int64_t), s));
         // every workspace the iteration touches is allocated now (graph capture)
-        qwork_ensure(dqn->act, dqn->L, E.n, false);
-        qwork_ensure(dqn->tgt, dqn->L, h->B, false);
-        qwork_ensure(dqn->trn, dqn->L, h->B, true);
-        const int64_t need = qnet_backward_slab_floats(dqn->L, h->B);
+        if (dqn->deep) {
+            deep_prepare(dqn, E.n, h->B);
+        } else {
+            qwork_ensure(dqn->act, dqn->L, E.n, false);
+            qwork_ensure(dqn->tgt, dqn->L, h->B, false);
+            qwork_ensure(dqn->trn, dqn->L, h->B, true);
+        }
+        const int64_t need = dqn->deep ? 0 : qnet_backward_slab_floats(dqn->L, h->B);
         if (need > dqn->slab_cap) {
             dfree(dqn->slab);
             dqn->slab = dalloc<float>(need);
@@ -258,9 +270,13 @@ extern "C" int snk_trainer_destroy(snk_trainer h) {
 // workspaces. Re-size what the iteration touches and drop stale graphs.
 static void trainer_refresh(snk_trainer_s *h) {
     snk_dqn_s *q = h->dqn;
-    qwork_ensure(q->act, q->L, env_dev(h->env).n, false);
-    qwork_ensure(q->tgt, q->L, h->B, false);
-    qwork_ensure(q->trn, q->L, h->B, true);
+    if (q->deep) {
+        deep_prepare(q, env_dev(h->env).n, h->B);
+    } else {
+        qwork_ensure(q->act, q->L, env_dev(h->env).n, false);
+        qwork_ensure(q->tgt, q->L, h->B, false);
+        qwork_ensure(q->trn, q->L, h->B, true);
+    }
     const int64_t gen = dqn_ws_gen(q);
     if (gen != h->ws_gen) {
         SNK_HIP(hipStreamSynchronize(stream()));

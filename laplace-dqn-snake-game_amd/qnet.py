@@ -15,6 +15,13 @@ from . import _lib
 from ._lib import DeviceArray, call, ptr, vp
 
 
+def deep_nparams(board_size: int, n_frames: int) -> int:
+    """Parameter count of the configs[2] net: 1,097,731 at bs=20, 2 frames."""
+    wo = board_size - 5
+    return ((9 * n_frames * 32 + 32) + (9 * 32 * 32 + 32) + (9 * 32 * 64 + 64) + (36 * 64 * 64 + 64)
+            + (wo * wo * 64 * 64 + 64) + (64 * 3 + 3))
+
+
 def nparams(board_size: int, n_frames: int) -> int:
     """Q-net parameter count: 279,699 at bs=12, 2 frames."""
     wo = board_size - 5
@@ -29,13 +36,17 @@ class DQNModel:
     a copy of q_net; RMSProp(lr, rho=0.9, eps=1e-8)."""
 
     def __init__(self, board_size: int = 10, n_actions: int = 3, *, n_frames: int = 2, lr: float = 0.0005,
-                 rho: float = 0.9, eps: float = 1e-8, seed: int = 1234):
+                 rho: float = 0.9, eps: float = 1e-8, seed: int = 1234, deep: bool = False):
+        """deep=True: the deeper bf16 conv Q-net of BASELINE configs[2]
+        (include/snakehip.h snk_dqn_create_deep; board side 10, 12 or 20)."""
         if n_actions != 3:
             raise ValueError("the reference Q-net has 3 outputs (structs.jl:134)")
         self.board_size, self.n_frames, self.n_actions = int(board_size), int(n_frames), 3
         self.lr, self.rho, self.eps = float(lr), float(rho), float(eps)
+        self.deep = bool(deep)
         h = vp()
-        call("snk_dqn_create", C.byref(h), self.board_size, self.n_frames, self.lr, self.rho, self.eps, int(seed))
+        call("snk_dqn_create_deep" if self.deep else "snk_dqn_create", C.byref(h), self.board_size, self.n_frames,
+             self.lr, self.rho, self.eps, int(seed))
         self._h = h
         n = C.c_int64(0)
         call("snk_dqn_nparams", h, C.byref(n))

@@ -40,12 +40,12 @@ class Trainer:
                  epsilon_end: float = 0.05, decay: float = 1e-6, save: bool = False, game: SnakeGame | None = None,
                  model: DQNModel | None = None, n_envs: int = 1, board_size: int = 10, n_frames: int = 2,
                  capacity: int = 50000, batch_size: int = 64, updates_per_iter: int = 1, gamma: float = 0.97,
-                 seed: int = 1234, loss_log_capacity: int = 1 << 20, graph_unroll: int = 0):
+                 seed: int = 1234, loss_log_capacity: int = 1 << 20, graph_unroll: int = 0, deep: bool = False):
         self.game = game if game is not None else SnakeGame(board_size, n_frames, n_envs=n_envs, autoreset=True)
         if not self.game.autoreset:
             raise ValueError("the batched trainer needs auto-reset games")
         bs, nf = self.game.board_size, self.game.n_frames
-        self.model = model if model is not None else DQNModel(bs, 3, n_frames=nf, seed=seed)
+        self.model = model if model is not None else DQNModel(bs, 3, n_frames=nf, seed=seed, deep=deep)
         self.buffer = ReplayBuffer(capacity, board_size=bs, n_frames=nf, batch_size=batch_size)
         self.n_batches, self.target_update_rate = int(n_batches), int(target_update_rate)
         self.epsilon, self.epsilon_end, self.decay = float(epsilon), float(epsilon_end), float(decay)

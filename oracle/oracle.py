@@ -61,6 +61,13 @@ def lib():
     L.orc_dqn_loss_grad.restype = C.c_double
     L.orc_dqn_loss_grad.argtypes = [C.c_int, C.c_int, F32P, F32P, C.c_int, F64P, I32P, F32P, F64P,
                                     U8P, U8P, C.c_double, F64P, F64P]
+    L.orc_deep_nparams.restype = C.c_int64
+    L.orc_deep_nparams.argtypes = [C.c_int, C.c_int]
+    L.orc_deep_forward.argtypes = [C.c_int, C.c_int, F32P, C.c_int, F64P, F64P]
+    L.orc_deep_backward.argtypes = [C.c_int, C.c_int, F32P, C.c_int, F64P, F64P, F64P]
+    L.orc_deep_loss_grad.restype = C.c_double
+    L.orc_deep_loss_grad.argtypes = [C.c_int, C.c_int, F32P, F32P, C.c_int, F64P, I32P, F32P, F64P,
+                                     U8P, U8P, C.c_double, F64P, F64P]
     L.orc_rmsprop.argtypes = [C.c_int64, F32P, F32P, F32P, C.c_float, C.c_float, C.c_float]
     L.orc_welford_center.argtypes = [C.c_int64, C.c_int, F64P, F64P, F64P]
     L.orc_gram.argtypes = [C.c_int64, C.c_int, F64P, F64P]
@@ -175,6 +182,34 @@ def dqn_loss_grad(bs, C, q_params, t_params, s, a_idx, r, s_next, done, mask3, g
                                    np.ascontiguousarray(s_next, np.float64).reshape(B, -1),
                                    np.ascontiguousarray(done, np.uint8),
                                    np.ascontiguousarray(mask3, np.uint8).reshape(B, 3), gamma, g, tgt)
+    return loss, g, tgt
+
+
+# ---------------------------------------------------------------- deeper bf16 Q-net (configs[2])
+def deep_nparams(bs: int, C: int) -> int:
+    return int(lib().orc_deep_nparams(bs, C))
+
+
+def deep_forward(bs: int, C: int, params: np.ndarray, x: np.ndarray) -> np.ndarray:
+    """The configs[2] net with the device's bf16 rounding points, fp64 sums."""
+    x = np.ascontiguousarray(x, np.float64).reshape(-1, C * bs * bs)
+    B = x.shape[0]
+    q = np.zeros((B, 3), np.float64)
+    lib().orc_deep_forward(bs, C, np.ascontiguousarray(params, np.float32), B, x, q)
+    return q
+
+
+def deep_loss_grad(bs, C, q_params, t_params, s, a_idx, r, s_next, done, mask3, gamma=0.97):
+    s = np.ascontiguousarray(s, np.float64).reshape(-1, C * bs * bs)
+    B = s.shape[0]
+    g = np.zeros(len(q_params), np.float64)
+    tgt = np.zeros(B, np.float64)
+    loss = lib().orc_deep_loss_grad(bs, C, np.ascontiguousarray(q_params, np.float32),
+                                    np.ascontiguousarray(t_params, np.float32), B, s,
+                                    np.ascontiguousarray(a_idx, np.int32), np.ascontiguousarray(r, np.float32),
+                                    np.ascontiguousarray(s_next, np.float64).reshape(B, -1),
+                                    np.ascontiguousarray(done, np.uint8),
+                                    np.ascontiguousarray(mask3, np.uint8).reshape(B, 3), gamma, g, tgt)
     return loss, g, tgt
 
 

@@ -504,6 +504,180 @@ double orc_dqn_loss_grad(int bs, int C, const float *qp, const float *tp, int B,
     return loss;
 }
 
+/* ======================= deeper bf16 Q-net (configs[2]) =====================
+ * BASELINE.json configs[2] names a "deeper conv Q-net, bf16" with no reference
+ * counterpart (builder-defined). It extends structs.jl:127-139
+ * by one more 3x3 convolution and wider channels, same Flux conventions:
+ *   Conv(3,3,C=>32,relu;pad=1) Conv(3,3,32=>32,relu;pad=1) Conv(3,3,32=>64,relu;pad=1)
+ *   Conv(6,6,64=>64,relu) flatten Dense((bs-5)^2*64=>64,relu) Dense(64=>3)
+ * bf16 semantics of the device path, restated here exactly:
+ *   - conv and Dense1 weight matrices are used rounded to bf16 (RNE); biases
+ *     and Dense2 stay fp32;
+ *   - every conv output (after bias + relu) is rounded to bf16;
+ *   - backward: the relu-masked gradient entering each conv / Dense1 layer is
+ *     rounded to bf16 before it is multiplied (both the weight- and the data-
+ *     gradient products); Dense2 and the TD/Huber head stay fp32/fp64.
+ * Sums are fp64 here (fp32 on the device). */
+static float bf16r(double v) {
+    float f = (float)v;
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u) return f;
+    u += 0x7fffu + ((u >> 16) & 1u);
+    u &= 0xffff0000u;
+    memcpy(&f, &u, 4);
+    return f;
+}
+typedef struct { int cin[4], cout[4], ks[4], pad[4]; int off_w[4], off_b[4], off_d1w, off_d1b, off_d2w, off_d2b, P, F1, Wo; } dlayout;
+static dlayout deep_layout(int bs, int C) {
+    dlayout L; int o = 0;
+    const int ci[4] = {C, 32, 32, 64}, co[4] = {32, 32, 64, 64}, ks[4] = {3, 3, 3, 6}, pd[4] = {1, 1, 1, 0};
+    for (int l = 0; l < 4; l++) {
+        L.cin[l] = ci[l]; L.cout[l] = co[l]; L.ks[l] = ks[l]; L.pad[l] = pd[l];
+        L.off_w[l] = o; o += ks[l] * ks[l] * ci[l] * co[l];
+        L.off_b[l] = o; o += co[l];
+    }
+    L.Wo = bs - 5; L.F1 = L.Wo * L.Wo * 64;
+    L.off_d1w = o; o += 64 * L.F1; L.off_d1b = o; o += 64;
+    L.off_d2w = o; o += 3 * 64; L.off_d2b = o; o += 3;
+    L.P = o;
+    return L;
+}
+int64_t orc_deep_nparams(int bs, int C) { return deep_layout(bs, C).P; }
+
+/* params with the conv / Dense1 weight matrices rounded to bf16 */
+static float *deep_rounded(const dlayout *L, const float *p) {
+    float *r = (float *)malloc(sizeof(float) * L->P);
+    memcpy(r, p, sizeof(float) * L->P);
+    for (int l = 0; l < 4; l++)
+        for (int i = L->off_w[l]; i < L->off_b[l]; i++) r[i] = bf16r(p[i]);
+    for (int i = L->off_d1w; i < L->off_d1b; i++) r[i] = bf16r(p[i]);
+    return r;
+}
+typedef struct { double *a[4], *h1; } dacts;
+static dacts dacts_alloc(int bs) {
+    dacts A; const int Wo = bs - 5;
+    A.a[0] = (double *)malloc(sizeof(double) * bs * bs * 32);
+    A.a[1] = (double *)malloc(sizeof(double) * bs * bs * 32);
+    A.a[2] = (double *)malloc(sizeof(double) * bs * bs * 64);
+    A.a[3] = (double *)malloc(sizeof(double) * Wo * Wo * 64);
+    A.h1 = (double *)malloc(sizeof(double) * 64);
+    return A;
+}
+static void dacts_free(dacts *A) { for (int l = 0; l < 4; l++) free(A->a[l]); free(A->h1); }
+static void deep_fwd_one(const dlayout *L, int bs, const float *pr, const double *x, dacts *A, double *q) {
+    const double *in = x;
+    int H = bs;
+    for (int l = 0; l < 4; l++) {
+        conv_fwd(H, L->cin[l], L->cout[l], L->ks[l], L->pad[l], pr + L->off_w[l], pr + L->off_b[l], in, A->a[l]);
+        const int Ho = H + 2 * L->pad[l] - L->ks[l] + 1, n = Ho * Ho * L->cout[l];
+        for (int i = 0; i < n; i++) A->a[l][i] = bf16r(A->a[l][i]);
+        in = A->a[l];
+        H = Ho;
+    }
+    for (int o = 0; o < 64; o++) {
+        double s = pr[L->off_d1b + o];
+        for (int f = 0; f < L->F1; f++) s += (double)pr[L->off_d1w + o + f * 64] * A->a[3][f];
+        A->h1[o] = s > 0 ? s : 0;
+    }
+    for (int a = 0; a < 3; a++) {
+        double s = pr[L->off_d2b + a];
+        for (int o = 0; o < 64; o++) s += (double)pr[L->off_d2w + a + o * 3] * A->h1[o];
+        q[a] = s;
+    }
+}
+void orc_deep_forward(int bs, int C, const float *params, int B, const double *x, double *q) {
+    dlayout L = deep_layout(bs, C);
+    float *pr = deep_rounded(&L, params);
+    dacts A = dacts_alloc(bs);
+    for (int b = 0; b < B; b++) deep_fwd_one(&L, bs, pr, x + (size_t)b * C * bs * bs, &A, q + 3 * b);
+    dacts_free(&A);
+    free(pr);
+}
+/* conv_bwd with the masked gradient rounded to bf16 first (the device's MFMA operand) */
+static void conv_bwd_bf16(int H, int Cin, int Cout, int K, int pad, const float *w, const double *x,
+                          const double *y, const double *dy, double *dw, double *db, double *dx) {
+    const int Ho = H + 2 * pad - K + 1, n = Ho * Ho * Cout;
+    double *dr = (double *)malloc(sizeof(double) * n);
+    for (int i = 0; i < n; i++) dr[i] = y[i] > 0 ? (double)bf16r(dy[i]) : 0.0;
+    /* conv_bwd skips y <= 0 itself; feed it the rounded values */
+    conv_bwd(H, Cin, Cout, K, pad, w, x, y, dr, dw, db, dx);
+    free(dr);
+}
+void orc_deep_backward(int bs, int C, const float *p, int B, const double *x, const double *dq, double *g) {
+    dlayout L = deep_layout(bs, C);
+    float *pr = deep_rounded(&L, p);
+    dacts A = dacts_alloc(bs);
+    const int Wo = L.Wo;
+    double *dh1 = (double *)malloc(sizeof(double) * 64);
+    double *da[4];
+    da[0] = (double *)malloc(sizeof(double) * bs * bs * 32);
+    da[1] = (double *)malloc(sizeof(double) * bs * bs * 32);
+    da[2] = (double *)malloc(sizeof(double) * bs * bs * 64);
+    da[3] = (double *)malloc(sizeof(double) * Wo * Wo * 64);
+    double q[3];
+    for (int b = 0; b < B; b++) {
+        const double *xb = x + (size_t)b * C * bs * bs;
+        const double *d = dq + 3 * b;
+        deep_fwd_one(&L, bs, pr, xb, &A, q);
+        for (int a = 0; a < 3; a++) {
+            g[L.off_d2b + a] += d[a];
+            for (int o = 0; o < 64; o++) g[L.off_d2w + a + o * 3] += d[a] * A.h1[o];
+        }
+        for (int o = 0; o < 64; o++) {
+            double s = 0;
+            for (int a = 0; a < 3; a++) s += d[a] * (double)p[L.off_d2w + a + o * 3];
+            dh1[o] = A.h1[o] > 0 ? (double)bf16r(s) : 0;
+        }
+        memset(da[3], 0, sizeof(double) * L.F1);
+        for (int o = 0; o < 64; o++) {
+            if (dh1[o] == 0) continue;
+            g[L.off_d1b + o] += dh1[o];
+            for (int f = 0; f < L.F1; f++) {
+                g[L.off_d1w + o + f * 64] += dh1[o] * A.a[3][f];
+                da[3][f] += dh1[o] * (double)pr[L.off_d1w + o + f * 64];
+            }
+        }
+        for (int l = 3; l >= 0; l--) {
+            const int H = l == 3 ? bs : bs;   /* every conv input is bs x bs */
+            const double *xin = l == 0 ? xb : A.a[l - 1];
+            conv_bwd_bf16(H, L.cin[l], L.cout[l], L.ks[l], L.pad[l], pr + L.off_w[l], xin, A.a[l], da[l],
+                          g + L.off_w[l], g + L.off_b[l], l == 0 ? NULL : da[l - 1]);
+        }
+    }
+    free(dh1);
+    for (int l = 0; l < 4; l++) free(da[l]);
+    dacts_free(&A);
+    free(pr);
+}
+double orc_deep_loss_grad(int bs, int C, const float *qp, const float *tp, int B, const double *s,
+                          const int32_t *a_idx, const float *r, const double *s_next, const uint8_t *done,
+                          const uint8_t *mask3, double gamma, double *grad, double *target_out) {
+    double *qn = (double *)malloc(sizeof(double) * 3 * B);
+    double *qs = (double *)malloc(sizeof(double) * 3 * B);
+    double *dq = (double *)calloc((size_t)3 * B, sizeof(double));
+    orc_deep_forward(bs, C, tp, B, s_next, qn);
+    orc_deep_forward(bs, C, qp, B, s, qs);
+    double loss = 0;
+    for (int b = 0; b < B; b++) {
+        double mx = -INFINITY;
+        for (int a = 0; a < 3; a++) {
+            /* the device keeps Q in fp32: the masked max is over fp32 values */
+            double v = mask3[3 * b + a] ? -100.0 : (double)(float)qn[3 * b + a];
+            if (v > mx) mx = v;
+        }
+        double tgt = (double)r[b] + gamma * mx * (double)(1 - done[b]);
+        if (target_out) target_out[b] = tgt;
+        double e = qs[3 * b + a_idx[b]] - tgt, ae = fabs(e);
+        loss += ae < 1.0 ? 0.5 * e * e : (ae - 0.5);
+        dq[3 * b + a_idx[b]] = (ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / B;
+    }
+    loss /= B;
+    if (grad) orc_deep_backward(bs, C, qp, B, s, dq, grad);
+    free(qn); free(qs); free(dq);
+    return loss;
+}
+
 /* Optimisers.jl RMSProp apply! (non-centred), Float32:
  *   quad = rho*quad + (1-rho)*dx^2 ; x -= dx*eta/(sqrt(quad)+eps) */
 void orc_rmsprop(int64_t P, float *theta, float *acc, const float *grad, float eta, float rho, float eps) {

@@ -99,6 +99,15 @@ double orc_dqn_loss_grad(int bs, int C, const float *q_params, const float *t_pa
                          const double *s, const int32_t *a_idx, const float *r,
                          const double *s_next, const uint8_t *done, const uint8_t *mask3,
                          double gamma, double *grad, double *target_out);
+/* ---- deeper bf16 Q-net (BASELINE configs[2], builder-defined; see the .c) -- */
+int64_t orc_deep_nparams(int bs, int C);
+void orc_deep_forward(int bs, int C, const float *params, int B, const double *x, double *q);
+void orc_deep_backward(int bs, int C, const float *params, int B, const double *x, const double *dq,
+                       double *grad);
+double orc_deep_loss_grad(int bs, int C, const float *q_params, const float *t_params, int B,
+                          const double *s, const int32_t *a_idx, const float *r, const double *s_next,
+                          const uint8_t *done, const uint8_t *mask3, double gamma, double *grad,
+                          double *target_out);
 /* Optimisers.RMSProp apply! in Float32 (utils.jl:429,466) */
 void orc_rmsprop(int64_t P, float *theta, float *acc, const float *grad,
                  float eta, float rho, float eps);
