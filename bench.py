@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--repeats", type=int, default=5,
+                   help="timed windows of --steps steps each; value and ms_per_step are the median window's")
     p.add_argument("--n-envs", type=int, default=4096)
     p.add_argument("--board-size", type=int, default=12)
     p.add_argument("--n-frames", type=int, default=2)
@@ -66,6 +68,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip per-kernel timing")
     p.add_argument("--no-dbuild", action="store_true", help="skip the Laplace D builds")
+    p.add_argument("--no-configs2", action="store_true", help="skip the configs[2] deep bf16 net line")
     p.add_argument("--d-samples", type=int, default=0, help="Jacobian Gram rows (0 = the whole replay buffer)")
     p.add_argument("--d-snapshots", type=int, default=1000, help="K of the snapshot D (compute_D.jl:51)")
     return p.parse_args()
@@ -106,6 +109,82 @@ def cpu_baseline(args) -> dict:
             "sample": (f"oracle C restatement, 1 thread: Q forward on {nf} of {n} states (scaled x{n // nf}), "
                        f"3 lockstep steps of {n} envs, one B=64 loss+grad+RMSProp; per-iteration "
                        f"fwd {t_fwd:.2f}s + step {t_step:.3f}s + update {t_upd:.2f}s")}
+
+
+def configs2(args, snk, graph) -> dict:
+    """BASELINE.json configs[2]: 65,536 lockstep 20x20 envs with the deeper
+    bf16 conv Q-net (snk_dqn_create_deep), one trainer
+    iteration per step as the headline (act forward, step + store, one B=64
+    update), median of 3 windows of 10 steps; per-layer times of the act
+    forward and the roofline of its dominant kernel (bf16 MFMA peak)."""
+    import numpy as np
+    from snake_amd import _lib
+    n, bs, C = 65536, 20, args.n_frames
+    tr = snk.Trainer(n_envs=n, board_size=bs, n_frames=C, capacity=args.capacity, batch_size=64,
+                     epsilon=args.epsilon, epsilon_end=args.epsilon, decay=0.0, updates_per_iter=1, seed=4321,
+                     deep=True)
+    snk.fill_buffer_(tr, graph=graph)
+    tr.run(2, learn=True, graph=graph)
+    steps, windows = 10, []
+    for _ in range(3):
+        _lib.call("snk_synchronize")
+        t0 = time.perf_counter()
+        tr.run(steps, learn=True, graph=graph)
+        _lib.call("snk_synchronize")
+        windows.append(time.perf_counter() - t0)
+    el = float(np.median(windows))
+    ms = np.zeros(6, np.float64)
+    _lib.call("snk_dqn_time_deep_layers", tr.model.handle, tr.game.handle, 5, _lib.ptr(ms))
+    wo, nc = bs - 5, bs * bs
+    flop = [2.0 * n * nc * 32 * 9 * C, 2.0 * n * nc * 32 * 288, 2.0 * n * nc * 64 * 288,
+            2.0 * n * wo * wo * 64 * 2304, 2.0 * n * wo * wo * 64 * 64, 2.0 * n * 64 * 3]
+    names = ["L0 conv 3x3 C->32 (deep_conv0_kernel, VALU)", "L1 conv 3x3 32->32 (deep_conv_kernel, bf16 MFMA)",
+             "L2 conv 3x3 32->64 (deep_conv_kernel, bf16 MFMA)", "L3 conv 6x6 64->64 (deep_conv_kernel, bf16 MFMA)",
+             "Dense1 (deep_dense1_kernel, bf16 MFMA)", "head (Dense2 + epsilon-greedy)"]
+    d = int(np.argmax(ms[1:5])) + 1
+    tf = flop[d] / (ms[d] * 1e-3) / 1e12
+    fwd_flop = sum(flop)
+    st = tr.stats()
+    return {"workload": f"configs[2]: {n} lockstep {bs}x{bs} envs, {C}-frame deeper conv Q-net (bf16): eps-greedy "
+                        f"forward + step!/virtual_step + store! + 1 B=64 update per step",
+            "value": n * steps / el, "unit": "env-steps/s", "ms_per_step": 1000.0 * el / steps,
+            "windows_ms": [1000.0 * w for w in windows], "steps": steps, "dtype": "bf16",
+            "n_params": tr.model.P, "forward_flop_per_env_step": fwd_flop / n,
+            "act_forward_ms": {nm: float(t) for nm, t in zip(names, ms)},
+            "act_forward_total_ms": float(ms.sum()),
+            "act_forward_tflops": fwd_flop / (ms.sum() * 1e-3) / 1e12,
+            "roofline": {"bound": "mfma", "kernel": names[d], "achieved": tf, "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s (bf16)", "frac": tf / PEAK_BF16_TFLOPS, "avg_launch_ms": float(ms[d]),
+                         "flop_per_launch": flop[d], "traffic": None},
+            "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"]}}
+
+
+def reference_ratio(args, snk, graph, episodes_per_env_step) -> dict:
+    """The reference's own ratio of updates to play: one update per finished
+    episode (utils.jl:434-481). At the headline workload about
+    episodes_per_env_step x 4096 episodes end per lockstep step, so this runs
+    that many B=64 updates per step: updates/s and env-steps/s of an
+    update-bound loop, and the time of one update from the difference with
+    the 1-update step."""
+    import numpy as np
+    from snake_amd import _lib
+    n, bs, C = args.n_envs, args.board_size, args.n_frames
+    U = max(2, int(round(episodes_per_env_step * n)))
+    tr = snk.Trainer(n_envs=n, board_size=bs, n_frames=C, capacity=args.capacity, batch_size=64,
+                     epsilon=args.epsilon, epsilon_end=args.epsilon, decay=0.0, updates_per_iter=U, seed=99,
+                     graph_unroll=1)
+    snk.fill_buffer_(tr, graph=graph)
+    tr.run(1, learn=True, graph=graph)
+    steps, windows = 3, []
+    for _ in range(3):
+        _lib.call("snk_synchronize")
+        t0 = time.perf_counter()
+        tr.run(steps, learn=True, graph=graph)
+        _lib.call("snk_synchronize")
+        windows.append(time.perf_counter() - t0)
+    el = float(np.median(windows))
+    return {"updates_per_step": U, "updates_per_s": U * steps / el, "env_steps_per_s": n * steps / el,
+            "ms_per_step": 1000.0 * el / steps, "ms_per_update": 1000.0 * el / steps / U}
 
 
 def d_buffer(snk, bs, C, n):
@@ -288,16 +367,20 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    barrier()
-    t0 = time.perf_counter()
-    tr.run(args.steps, learn=True, graph=graph)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    windows = []
+    for _ in range(max(1, args.repeats)):
+        barrier()
+        t0 = time.perf_counter()
+        tr.run(args.steps, learn=True, graph=graph)
+        barrier()
+        w = time.perf_counter() - t0
+        if dist is not None:
+            import torch
+            t = torch.tensor([w], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            w = float(t.item())
+        windows.append(w)
+    elapsed = float(np.median(windows))   # median of the timed windows
     st = tr.stats()
     faults = tr.game.check_faults()
     if comm is not None:
@@ -315,6 +398,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
+        "windows_ms": [1000.0 * w for w in windows],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -406,6 +490,20 @@ def main():
             del gl, rl, al
         except Exception as e:   # report, do not fail the headline line
             out["step_kernel_large"] = {"error": str(e)}
+    if rank == 0 and world == 1 and not args.no_extras:
+        eps_rate = st["episodes"] / max(1, st["env_steps"])
+        try:
+            out["reference_ratio"] = reference_ratio(args, snk, graph, eps_rate)
+            out["reference_ratio"]["ms_per_update_marginal"] = (
+                (out["reference_ratio"]["ms_per_step"] - out["ms_per_step"]) / (out["reference_ratio"]["updates_per_step"] - 1))
+        except Exception as e:   # report, do not fail the headline line
+            out["reference_ratio"] = {"error": str(e)}
+        out["updates_per_s"] = args.updates_per_iter * args.steps / elapsed
+    if rank == 0 and world == 1 and not args.no_configs2:
+        try:
+            out["configs2"] = configs2(args, snk, graph)
+        except Exception as e:
+            out["configs2"] = {"error": str(e)}
     if not args.no_dbuild:
         if world == 1:      # D(50k) + compute_D's snapshot Gram + laplace_sampling! (configs[4])
             if rank == 0:
