@@ -74,41 +74,53 @@ def parse():
     return p.parse_args()
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args) -> dict:
-    """The CPU oracle (oracle/liboracle.so, plain C, 1 thread) timed on this
-    host on a bounded sample of the same workload, extrapolated to one full
-    iteration: Q forward of 4096 states (timed on 128, scaled), 4096 env steps
-    (timed on all 4096 for 3 steps), one 64-sample DQN update (timed once)."""
+    """The CPU baseline: oracle/cpu_fast.cpp, an optimised
+    C++ restatement of the same iteration (O(1)-collision env, fp32
+    im2col + blocked GEMM Q-net and update, OpenMP), timed on this host for
+    whole iterations: act forward over every env, env step + store, one B=64
+    DQN update. 1 thread, then the CPU share of this job (OMP_NUM_THREADS, else
+    every core). Plus the D(50k) Gram on a 2,000-row sample of Jacobian-sized
+    rows, extrapolated by the n(n+1)/2 tile count (labelled)."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
+    L = oracle.fast()
     bs, C, n = args.board_size, args.n_frames, args.n_envs
-    rng = np.random.default_rng(0)
-    P = oracle.qnet_nparams(bs, C)
-    params = (rng.standard_normal(P) * 0.05).astype(np.float32)
-    nf = 128
-    x = rng.integers(-1, 3, size=(nf, C, bs * bs)).astype(np.float64)
-    t0 = time.perf_counter()
-    oracle.qnet_forward(bs, C, params, x)
-    t_fwd = (time.perf_counter() - t0) / nf * n
-    ob = oracle.OracleBatch(n, bs, C)
-    t0 = time.perf_counter()
-    for t in range(3):
-        ob.step(oracle.synth_actions(7, n, t), want_frames=True)
-    t_step = (time.perf_counter() - t0) / 3
-    B = 64
-    s = rng.integers(-1, 3, size=(B, C, bs * bs))
-    sn = rng.integers(-1, 3, size=(B, C, bs * bs))
-    t0 = time.perf_counter()
-    _, g, _ = oracle.dqn_loss_grad(bs, C, params, params, s, rng.integers(0, 3, B), np.zeros(B, np.float32), sn,
-                                   np.zeros(B, np.uint8), np.zeros((B, 3), np.uint8))
-    oracle.rmsprop(params, np.zeros_like(params), g.astype(np.float32))
-    t_upd = (time.perf_counter() - t0) * args.updates_per_iter
-    it = t_fwd + t_step + t_upd
-    return {"value": n / it, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle C restatement, 1 thread: Q forward on {nf} of {n} states (scaled x{n // nf}), "
-                       f"3 lockstep steps of {n} envs, one B=64 loss+grad+RMSProp; per-iteration "
-                       f"fwd {t_fwd:.2f}s + step {t_step:.3f}s + update {t_upd:.2f}s")}
+    food, _ = oracle.food_list(bs)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    t1, tn = np.zeros(4), np.zeros(4)
+    v1 = L.cpuf_bench(n, bs, C, 1, 0, 1, args.updates_per_iter, args.capacity, food, len(food), t1)
+    vn = L.cpuf_bench(n, bs, C, threads, 1, 3, args.updates_per_iter, args.capacity, food, len(food), tn)
+    ns, Kc = 2000, 9 * C * 16 + 16 + 4640 + 73792
+    X = np.random.default_rng(0).standard_normal((ns, Kc)).astype(np.float32)
+    G = np.zeros((ns, ns), np.float32)
+    tg = L.cpuf_gram(ns, Kc, X, G, threads)
+    N = args.d_samples or 50_000
+    return {"value": vn, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": (f"oracle/cpu_fast.cpp (optimised C++ restatement, OpenMP, x86-64-v3): whole iterations of "
+                       f"{n} envs ({bs}x{bs}, {C} frames): act forward + step/store + {args.updates_per_iter} B=64 "
+                       f"update(s); {threads} threads: 3 iterations (fwd {tn[0]:.2f}s, step {tn[1]:.3f}s, "
+                       f"update {tn[2]:.2f}s); 1 thread: 1 iteration (fwd {t1[0]:.2f}s, step {t1[1]:.3f}s, "
+                       f"update {t1[2]:.2f}s)"),
+            "single_thread": {"value": v1, "cores": 1},
+            "d_build_gram_sec_extrapolated": tg * (N * (N + 1.0)) / (ns * (ns + 1.0)),
+            "d_build_gram_sample": f"G = X X' of {ns} rows x {Kc} conv columns in {tg:.2f}s on {threads} threads "
+                                   f"({2.0 * ns * (ns + 1) / 2 * Kc / tg / 1e9:.0f} GFLOP/s), scaled by the "
+                                   f"n(n+1)/2 ratio to n = {N}; Jacobian rows and the dense terms (<2% of the "
+                                   f"work) not included"}
 
 
 def configs2(args, snk, graph) -> dict:

@@ -75,6 +75,38 @@ def lib():
     return L
 
 
+_FAST = None
+
+
+def fast():
+    """libcpufast.so (cpu_fast.cpp): the optimised multi-threaded CPU
+    restatement bench.py times as cpu_baseline. Same test-only status."""
+    global _FAST
+    if _FAST is not None:
+        return _FAST
+    path = os.path.join(_HERE, "libcpufast.so")
+    if not os.path.exists(path) or os.path.getmtime(os.path.join(_HERE, "cpu_fast.cpp")) > os.path.getmtime(path):
+        subprocess.run(["make", "-C", _HERE, "-s", "libcpufast.so"], check=True)
+    L = C.CDLL(path)
+    L.cpuf_env_create.restype = C.c_void_p
+    L.cpuf_env_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, I32P, C.c_int]
+    L.cpuf_env_destroy.argtypes = [C.c_void_p]
+    L.cpuf_env_step.argtypes = [C.c_void_p, U8P, F32P, U8P, U8P, C.c_int]
+    L.cpuf_env_boards.argtypes = [C.c_void_p, I8P]
+    L.cpuf_qnet_forward.argtypes = [C.c_int, C.c_int, F32P, C.c_int, F32P, F32P, C.c_int]
+    L.cpuf_loss_grad.restype = C.c_double
+    L.cpuf_loss_grad.argtypes = [C.c_int, C.c_int, F32P, F32P, C.c_int, F32P, I32P, F32P, F32P, U8P, U8P, F32P,
+                                 C.c_int]
+    L.cpuf_bench.restype = C.c_double
+    L.cpuf_bench.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, I32P, C.c_int,
+                             F64P]
+    L.cpuf_gram.restype = C.c_double
+    L.cpuf_gram.argtypes = [C.c_int, C.c_int, F32P, F32P, C.c_int]
+    L.cpuf_max_threads.restype = C.c_int
+    _FAST = L
+    return L
+
+
 # ---------------------------------------------------------------- RNG / food
 def xoshiro_seed(seed: int = 42) -> np.ndarray:
     st = np.zeros(5, np.uint64)
