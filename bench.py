@@ -171,6 +171,35 @@ def configs2(args, snk, graph) -> dict:
             "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"]}}
 
 
+def step_kernel_point(snk, n, bs, C, store):
+    """The fused step!/virtual_step(/store!) kernel alone, back-to-back launches
+    between one HIP event pair (snk_env_time_step). Algorithmic bytes per
+    env-step: the current board read + the new one written (2 * pitch), 16 B
+    state read + 16 B written, 12 B of step outputs, the action byte; with the
+    store also b_{t-1} read and the C + 1 replay frames written + 9 B of replay
+    metadata: (C + 4) * pitch + 57 at C = 2, 2 * pitch + 45 without."""
+    import ctypes
+    import numpy as np
+    from snake_amd import _lib
+    g = snk.SnakeGame(bs, C, n_envs=n, autoreset=True)
+    rb = snk.ReplayBuffer(n * 2, board_size=bs, n_frames=C, batch_size=64) if store else None
+    a = snk.DeviceArray(n, np.uint8)
+    for t in range(20):   # boards into play
+        snk.synth_actions_dev(g, 7 + t, a)
+        snk.step_indices_dev(g, a.ptr, replay=rb)
+    snk.synth_actions_dev(g, 99, a)
+    ms = _lib.f64(0)
+    _lib.call("snk_env_time_step", g.handle, rb.handle if rb else None, a.ptr, 50, ctypes.byref(ms))
+    pitch = (bs * bs + 15) // 16 * 16
+    bpe = (C + 4) * pitch + 57 if store else 2 * pitch + 45
+    gbs = n * bpe / (ms.value * 1e-3) / 1e9
+    mall = n * (3 * pitch + 2 * bs * bs + 40) < 256e6
+    return {"n_envs": n, "board": bs, "store": store,
+            "residency": "MALL (working set < 256 MB Infinity Cache)" if mall else "HBM",
+            "avg_launch_ms": ms.value, "bytes_per_env_step": bpe, "achieved_GBs": gbs,
+            "frac_hbm": gbs / PEAK_HBM_GBS, "env_steps_per_s": n / (ms.value * 1e-3)}
+
+
 def reference_ratio(args, snk, graph, episodes_per_env_step) -> dict:
     """The reference's own ratio of updates to play: one update per finished
     episode (utils.jl:434-481). At the headline workload about
@@ -482,26 +511,14 @@ def main():
         out["step_kernel"] = {"avg_launch_ms": sms.value, "bytes_per_env_step": step_bytes,
                               "achieved_GBs": gbs, "frac_hbm": gbs / PEAK_HBM_GBS,
                               "env_steps_per_s": n / (sms.value * 1e-3)}
-        # configs[2]-scale step kernel (65,536 envs, 20x20, replay store fused): the HBM-bound case
-        try:
-            gl = snk.SnakeGame(20, C, n_envs=65536, autoreset=True)
-            rl = snk.ReplayBuffer(65536 * 4, board_size=20, n_frames=C, batch_size=64)
-            al = snk.DeviceArray(65536, np.uint8)
-            for t in range(20):
-                snk.synth_actions_dev(gl, 7 + t, al)
-                snk.step_indices_dev(gl, al.ptr, replay=rl)
-            snk.synth_actions_dev(gl, 99, al)
-            lms = _lib.f64(0)
-            _lib.call("snk_env_time_step", gl.handle, rl.handle, al.ptr, 50, ctypes.byref(lms))
-            lb = (C + 4) * 400 + 57
-            lg = 65536 * lb / (lms.value * 1e-3) / 1e9
-            out["step_kernel_large"] = {"config": "65536 envs, 20x20, store fused (configs[2] env scale)",
-                                        "avg_launch_ms": lms.value, "bytes_per_env_step": lb,
-                                        "achieved_GBs": lg, "frac_hbm": lg / PEAK_HBM_GBS,
-                                        "env_steps_per_s": 65536 / (lms.value * 1e-3)}
-            del gl, rl, al
-        except Exception as e:   # report, do not fail the headline line
-            out["step_kernel_large"] = {"error": str(e)}
+        # configs[2]-scale step kernel (20x20 boards): 65,536 envs (working set inside the 256 MB
+        # Infinity Cache) and 262,144 envs (HBM-resident), pure step and with the replay store fused
+        out["step_kernel_large"] = []
+        for ln, store in ((65536, True), (262144, False), (262144, True)):
+            try:
+                out["step_kernel_large"].append(step_kernel_point(snk, ln, 20, C, store))
+            except Exception as e:   # report, do not fail the headline line
+                out["step_kernel_large"].append({"n_envs": ln, "store": store, "error": str(e)})
     if rank == 0 and world == 1 and not args.no_extras:
         eps_rate = st["episodes"] / max(1, st["env_steps"])
         try:

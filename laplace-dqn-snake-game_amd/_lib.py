@@ -13,7 +13,8 @@ import re
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsnakehip.so")
+# SNK_LIB: an alternative build of the same library (tools/ profiling variants)
+LIB_PATH = os.environ.get("SNK_LIB") or os.path.join(_HERE, "libsnakehip.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "snakehip.h")
 
 SNK_OK = 0

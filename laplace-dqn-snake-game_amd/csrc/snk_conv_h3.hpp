@@ -69,10 +69,11 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // partial max |w| of w[0, n): block b (256 threads) covers a grid-stride share; part[b]
+// block blockIdx.x of nblk scanning blocks (a launch may hold other workgroups too)
 __device__ __forceinline__ void wmax_block(const float *__restrict__ w, int64_t n, float *__restrict__ part,
-                                           float *red4) {
+                                           float *red4, int nblk) {
     float m = 0.0f;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)nblk * 256)
         m = fmaxf(m, fabsf(w[i]));
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
@@ -83,7 +84,7 @@ __device__ __forceinline__ void wmax_block(const float *__restrict__ w, int64_t 
 static __global__ __launch_bounds__(256) void wmax_scan_kernel(const float *__restrict__ w, int64_t n,
                                                         float *__restrict__ part) {
     __shared__ float red4[4];
-    wmax_block(w, n, part, red4);
+    wmax_block(w, n, part, red4, (int)gridDim.x);
 }
 
 // conv3 (CK = 32 -> CN = 64, pad 0, EPI_BIAS_RELU) on the h3 split; ConvArgs:

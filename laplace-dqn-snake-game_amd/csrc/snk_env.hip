@@ -3,21 +3,30 @@
 // One fused kernel per lockstep step of n envs implements step!
 // (utils.jl:100-109: move_wrapper! -> grow_maybe! -> sample_food! /
 // remove_tail! -> check_collision -> update_board!) plus virtual_step's
-// suicidal mask (utils.jl:112-132), auto-reset (utils.jl:199 `SnakeGame()`)
-// and, optionally, store! of the transition into the replay ring
-// (utils.jl:267-277).
+// suicidal mask (utils.jl:112-132), auto-reset (utils.jl:199 `SnakeGame()`),
+// optionally store! of the transition into the replay ring (utils.jl:267-277)
+// and the trainer's episode statistics (utils.jl:478).
 //
-// Mapping: a workgroup is ONE wave of 64 lanes that owns 64 envs.
-//   Phase A  the wave streams the 64 current boards (16-byte pieces,
-//            consecutive lanes -> consecutive bytes) HBM -> LDS;
-//   Phase B  lane e runs env e's scalar logic against its LDS board: O(1)
-//            collision test (board[new_head] lookup replaces the reference's
-//            O(L) count over the body), food-list probe, in-place edits of
-//            the <= 3 cells that change, next-state suicidal mask;
-//   Phase C  the wave streams the new boards LDS -> HBM frame ring, and the
-//            b_{t-C}..b_t frames into the replay slot.
-// Per env-step HBM traffic is 2*pitch + 32 B of state/outputs (+ (C+1)*pitch
-// when storing): the board is touched once in each direction.
+// Mapping: a workgroup of 4 waves owns 64 envs (NE).
+//   Phase A  all 256 threads stream the 64 current boards (16-byte pieces,
+//            consecutive threads -> consecutive bytes) HBM -> LDS; wave 0
+//            first issues its lanes' state / action / body-ring loads so their
+//            latency hides under the board stream;
+//   Phase B  wave 0, lane e = env e, runs the scalar logic against the
+//            UNMODIFIED LDS board: O(1) collision (board[new_head] replaces the
+//            reference's O(L) body scan), food-list probe, next-state suicidal
+//            mask. The <= 3 changed cells (tail -> 0, head -> 1, food -> 2) are
+//            recorded as patches, and the logic reads the new board through them;
+//   Phase C  all threads write the new boards (LDS piece + patches) to the frame
+//            ring and, when storing, b_{t-C}..b_t into the replay slot (b_{t-1}
+//            read from HBM in the same pass).
+// LDS is the boards only (64 * pitch), so 4-wave workgroups keep 6 (20x20) to 8
+// (12x12) workgroups = 24-32 waves per CU streaming. Per env-step HBM traffic is
+// 2 * pitch + 45 B (+ (C + 1) * pitch written and (C - 1) * pitch read when
+// storing): every board byte is touched once in each direction.
+// The last workgroup to arrive (agent-scope ticket) advances the step counter
+// and the replay count, and reduces the per-workgroup episode partials in
+// workgroup order (deterministic), so a step is ONE launch.
 #include <algorithm>
 #include <vector>
 
@@ -25,57 +34,159 @@
 
 namespace snk {
 
-__device__ __forceinline__ int food_search(const int8_t *b, const int16_t *food, int n_food,
-                                           uint64_t used) {
-    // utils.jl:25-34: first list entry (in list order) whose cell is empty
+constexpr int ENV_NE = 64, ENV_NT = 256;
+// Profiling builds only (make clocks): per-workgroup phase timestamps (100 MHz realtime
+// counter) into a debug buffer, read back by snk_env_debug_clocks.
+#ifdef SNK_ENV_CLOCKS
+__device__ uint64_t *g_env_clk;
+#define ENV_CLK(slot) \
+    do { if (threadIdx.x == 0 && g_env_clk) g_env_clk[(int64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define ENV_CLK1(slot) \
+    do { if (threadIdx.x == 64 && g_env_clk) g_env_clk[(int64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define ENV_CLK(slot) do { } while (0)
+#define ENV_CLK1(slot) do { } while (0)
+#endif
+typedef int i32x4 __attribute__((ext_vector_type(4)));   // native vector: register arrays stay in VGPRs
+
+// utils.jl:25-34: first list entry (in list order) whose cell is empty
+template <class Cell>
+__device__ __forceinline__ int food_search(const Cell &cell, const int16_t *food, int n_food, uint64_t used) {
     for (int k = 0; k < n_food; ++k)
-        if (!((used >> k) & 1ull) && b[food[k]] == 0) return k;
+        if (!((used >> k) & 1ull) && cell(food[k]) == 0) return k;
     return -1;
 }
-__device__ __forceinline__ bool has_empty(const int8_t *b, int ncell) {
+template <class Cell>
+__device__ __forceinline__ bool has_empty(const Cell &cell, int ncell) {
     for (int c = 0; c < ncell; ++c)
-        if (b[c] == 0) return true;
+        if (cell(c) == 0) return true;
     return false;
 }
 
+// the 16 board bytes [base, base + 16) with patch p (cell pc[p], value p) applied, p ascending
+__device__ __forceinline__ i32x4 patch16(i32x4 v, int base, const int16_t *pc) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const int off = pc[p] - base;
+        if ((unsigned)off < 16u) {
+            const int w = off >> 2, sh = (off & 3) * 8;
+            const int keep = ~(0xff << sh), val = p << sh;
+            v[0] = w == 0 ? (v[0] & keep) | val : v[0];
+            v[1] = w == 1 ? (v[1] & keep) | val : v[1];
+            v[2] = w == 2 ? (v[2] & keep) | val : v[2];
+            v[3] = w == 3 ? (v[3] & keep) | val : v[3];
+        }
+    }
+    return v;
+}
+
+__device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// workgroups per CU the LDS admits (6 at most: 85 VGPRs): the register budget is sized for them
 template <int PITCH>
-__global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *__restrict__ act,
-                                                      int act_mode, ReplayDev R, int store) {
-    __shared__ __attribute__((aligned(16))) int8_t sb[64 * PITCH];
-    __shared__ uint8_t s_flag[64];  // bit0 stepped, bit1 reset
-    constexpr int NCH = PITCH / 16;
-    const int lane = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * 64;
-    const int ne = (int)min((int64_t)64, E.n - e0);
+constexpr int env_wg_per_cu() {
+    return (160 * 1024) / (ENV_NE * PITCH + 1024) < 6 ? (160 * 1024) / (ENV_NE * PITCH + 1024) : 6;
+}
+
+template <int PITCH>
+__global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kernel(EnvDev E, const uint8_t *__restrict__ act, int act_mode,
+                                                          ReplayDev R, int store, EpisodeAcc acc, int with_acc) {
+    constexpr int NCH = PITCH / 16, NPT = (ENV_NE * NCH + ENV_NT - 1) / ENV_NT;
+    __shared__ __attribute__((aligned(16))) int8_t sb[ENV_NE * PITCH];
+    __shared__ __attribute__((aligned(8))) int16_t s_pc[ENV_NE * 4];   // patch cells (tail, head, food), -1 = none
+    __shared__ uint8_t s_flag[ENV_NE];                                  // bit0 stepped, bit1 reset
+    __shared__ int16_t s_food[64];
+    __shared__ float s_epr[ENV_NE];   // finished episodes: reward (NaN = not finished), score
+    __shared__ uint8_t s_score[ENV_NE];
+    ENV_CLK(0);
+    const int tid = threadIdx.x;
+    const bool w0 = tid < 64;
+    const int lane = tid & 63;
+    const int64_t e0 = (int64_t)blockIdx.x * ENV_NE;
+    const int ne = (int)min((int64_t)ENV_NE, E.n - e0);
     const int64_t t = E.ctl->t;
     const int cur = (int)(t % 3), nxt = (int)((t + 1) % 3), prv = (int)((t + 2) % 3);
     const int64_t rc = store ? *R.count : 0;
+    const int bs = E.bs, cap = E.ring_cap;
+
+    // ---- wave 0: per-env scalar loads first (state -> body ring cells) ----
+    const bool live = w0 && lane < ne;
+    const int64_t e = e0 + lane;
+    EnvState st{};
+    int a = 0, head_cell = 0, tail_cell = 0, tail_next = 0, tail_idx = 0;
+    float epr0 = 0.0f;
+    if (live) {
+        st = E.state[e];
+        a = act[e];
+        epr0 = E.ep_reward[e];
+        const uint16_t *ring = E.ring + e * cap;
+        tail_idx = (int)st.head + (int)st.len - 1;
+        if (tail_idx >= cap) tail_idx -= cap;
+        head_cell = (int)st.head_cell;
+        tail_cell = (int)st.tail_cell;
+        tail_next = ring[tail_idx == 0 ? cap - 1 : tail_idx - 1];   // the new tail unless the snake eats
+    }
+    if (w0 && lane < E.n_food) s_food[lane] = E.food[lane];
+    ENV_CLK(1);
 
     // ---- Phase A: current boards HBM -> LDS ------------------------------
-    for (int idx = lane; idx < ne * NCH; idx += 64) {
-        const int e = idx / NCH, c = idx - e * NCH;
-        const int4 v = *reinterpret_cast<const int4 *>(E.frames + ((e0 + e) * 3 + cur) * PITCH + c * 16);
-        *reinterpret_cast<int4 *>(sb + e * PITCH + c * 16) = v;
+    {
+        i32x4 v[NPT];
+#pragma clang loop unroll(full)
+        for (int k = 0; k < NPT; ++k) {
+            const int idx = tid + k * ENV_NT;
+            if (idx < ne * NCH) {
+                const int el = idx / NCH, c = idx - el * NCH;
+                v[k] = *reinterpret_cast<const i32x4 *>(E.frames + ((e0 + el) * 3 + cur) * PITCH + c * 16);
+            }
+        }
+#pragma clang loop unroll(full)
+        for (int k = 0; k < NPT; ++k) {
+            const int idx = tid + k * ENV_NT;
+            if (idx < ne * NCH) *reinterpret_cast<i32x4 *>(sb + idx * 16) = v[k];
+        }
     }
     __syncthreads();
+    ENV_CLK(2);
 
-    // ---- Phase B: per-env logic (lane = env) ------------------------------
-    uint8_t flag = 0;
-    if (lane < ne) {
-        const int64_t e = e0 + lane;
-        const int bs = E.bs, cap = E.ring_cap;
-        int8_t *b = sb + lane * PITCH;
-        EnvState st = E.state[e];
+    // ---- Phase B: per-env logic (wave 0, lane = env) ----------------------
+    bool done_out = false;
+    float epr_out = 0.0f;
+    int score_out = 0;
+    if (live) {
+        uint8_t flag = 0;
+        int16_t pc[3] = {-1, -1, -1};
+        const int8_t *b = sb + lane * PITCH;
         const int prev = st.flags & 3;
         if (!(st.flags & 4)) {
             flag = 1;
-            const int a = act[e];
             const int dir = act_mode == SNK_ACT_INDEX ? avail_action(prev, a % 3) : (a & 3);
             uint16_t *ring = E.ring + e * cap;
-            const int head_cell = ring[st.head];
-            int tail_idx = st.head + st.len - 1;
-            if (tail_idx >= cap) tail_idx -= cap;
-            const int tail_cell = ring[tail_idx];
             // grow_maybe! (utils.jl:66-81)
             const int nh = head_cell + dir_delta(bs, dir);
             const int old = b[nh];
@@ -85,14 +196,15 @@ __global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *_
             int food_cell = -1;
             bool fault = false;
             int score = st.score;
+            auto cell_old = [&](int c) { return (int)b[c]; };
             if (eat) {
                 score += 1;
-                const int k = food_search(b, E.food, E.n_food, used);  // pre-update board
+                const int k = food_search(cell_old, s_food, E.n_food, used);   // pre-update board
                 if (k >= 0) {
                     used |= 1ull << k;
-                    food_cell = E.food[k];
-                } else if (has_empty(b, bs * bs)) {
-                    fault = true;  // utils.jl:37 BoundsError in the reference
+                    food_cell = s_food[k];
+                } else if (has_empty(cell_old, bs * bs)) {
+                    fault = true;   // utils.jl:37 BoundsError in the reference
                 }
             }
             // check_collision (utils.jl:55-58) after the tail pop; truncation
@@ -101,15 +213,17 @@ __global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *_
             const int steps = st.steps + 1;
             const bool lost = old == -1 || body || dir == (prev ^ 1) || (E.C + steps - 1 > E.max_hist);
             if (lost) reward = -1.0f;
-            // update_board! (utils.jl:43-52) as cell edits
-            if (!eat) b[tail_cell] = 0;
-            b[nh] = 1;
-            if (food_cell >= 0) b[food_cell] = 2;
+            // update_board! (utils.jl:43-52) as patches, applied in this order
+            pc[0] = eat ? -1 : (int16_t)tail_cell;
+            pc[1] = (int16_t)nh;
+            pc[2] = (int16_t)food_cell;
+            auto cell_new = [&](int c) {
+                return c == food_cell ? 2 : c == nh ? 1 : (!eat && c == tail_cell) ? 0 : (int)b[c];
+            };
             const int nhead = st.head == 0 ? cap - 1 : st.head - 1;
             ring[nhead] = (uint16_t)nh;
             const int nlen = st.len + (eat ? 1 : 0);
-            const int ntail_idx = eat ? tail_idx : (tail_idx == 0 ? cap - 1 : tail_idx - 1);
-            const int ntail_cell = eat ? tail_cell : ring[ntail_idx];
+            const int ntail_cell = eat ? tail_cell : tail_next;
             // virtual_step (utils.jl:112-132): would each next action lose?
             uint8_t mask = 7;
             if (!lost) {
@@ -117,15 +231,15 @@ __global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *_
                 const bool trunc2 = E.C + steps > E.max_hist;
                 for (int k2 = 0; k2 < 3; ++k2) {
                     const int nh2 = nh + dir_delta(bs, avail_action(dir, k2));
-                    const int v = b[nh2];
+                    const int v = cell_new(nh2);
                     const bool veat = v == 2;
                     const bool vbody = v == 1 && !(!veat && nh2 == ntail_cell);
                     if (v == -1 || vbody || trunc2) mask |= (uint8_t)(1 << k2);
-                    if (veat && food_search(b, E.food, E.n_food, used) < 0 && has_empty(b, bs * bs))
-                        fault = true;  // the virtual step's sample_food! would throw too
+                    if (veat && food_search(cell_new, s_food, E.n_food, used) < 0 && has_empty(cell_new, bs * bs))
+                        fault = true;   // the virtual step's sample_food! would throw too
                 }
             }
-            const float epr = E.ep_reward[e] + reward;
+            const float epr = epr0 + reward;
             const uint8_t dirs = (uint8_t)(prev | (dir << 2) | ((lost ? 1 : 0) << 4));
             E.out_reward[e] = reward;
             E.out_done[e] = lost;
@@ -133,6 +247,9 @@ __global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *_
             E.out_dirs[e] = dirs;
             E.out_ep_reward[e] = epr;
             E.out_score[e] = (uint8_t)score;
+            done_out = lost;
+            epr_out = epr;
+            score_out = score;
             if (fault) atomicAdd(E.fault_count, 1u);
             if (store) {
                 const int64_t slot = (rc + e) % R.cap;
@@ -144,21 +261,21 @@ __global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *_
             }
             if (lost && E.autoreset) {
                 flag |= 2;
-                EnvState ns{};
-                ns.head = 0;
-                ns.len = 2;
-                ring[0] = (uint16_t)((bs - 3) + bs);  // structs.jl:47 (bs-2, 2)
-                ring[1] = (uint16_t)((bs - 2) + bs);  //              (bs-1, 2)
+                const EnvState ns = EnvState::fresh(bs);
+                ring[0] = (uint16_t)((bs - 3) + bs);   // structs.jl:47 (bs-2, 2)
+                ring[1] = (uint16_t)((bs - 2) + bs);   //              (bs-1, 2)
                 E.state[e] = ns;
                 E.ep_reward[e] = 0.0f;
             } else {
-                EnvState ns;
+                EnvState ns{};
                 ns.food_used = used;
                 ns.head = (uint16_t)nhead;
                 ns.len = (uint16_t)nlen;
                 ns.steps = (uint16_t)steps;
                 ns.flags = (uint8_t)(dir | (lost ? 4 : 0) | ((fault || (st.flags & 8)) ? 8 : 0));
                 ns.score = (uint8_t)score;
+                ns.head_cell = (uint64_t)nh;
+                ns.tail_cell = (uint64_t)ntail_cell;
                 E.state[e] = ns;
                 E.ep_reward[e] = epr;
             }
@@ -168,49 +285,149 @@ __global__ __launch_bounds__(64) void env_step_kernel(EnvDev E, const uint8_t *_
             E.out_done[e] = 1;
             E.out_mask[e] = 7;
             E.out_dirs[e] = (uint8_t)(prev | (prev << 2) | (1 << 4));
-            E.out_ep_reward[e] = E.ep_reward[e];
+            E.out_ep_reward[e] = epr0;
             E.out_score[e] = st.score;
+            done_out = true;
+            epr_out = epr0;
+            score_out = st.score;
         }
         s_flag[lane] = flag;
+        s_epr[lane] = done_out ? epr_out : __builtin_nanf("");
+        s_score[lane] = (uint8_t)score_out;
+        s_pc[lane * 4 + 0] = pc[0];
+        s_pc[lane * 4 + 1] = pc[1];
+        s_pc[lane * 4 + 2] = pc[2];
     }
     __syncthreads();
 
-    // ---- Phase C: LDS -> frame ring (+ replay slot) -----------------------
-    for (int idx = lane; idx < ne * NCH; idx += 64) {
-        const int e = idx / NCH, c = idx - e * NCH;
-        const int64_t ge = e0 + e;
-        const uint8_t f = s_flag[e];
-        const int4 vnew = *reinterpret_cast<const int4 *>(sb + e * PITCH + c * 16);
-        int8_t *fr = E.frames + ge * 3 * PITCH + c * 16;
-        if (store && (f & 1)) {
-            const int64_t slot = (rc + ge) % R.cap;
-            int8_t *rf = R.frames + slot * (int64_t)(R.C + 1) * PITCH + c * 16;
-            const int4 vcur = *reinterpret_cast<const int4 *>(fr + cur * PITCH);
-            if (R.C == 2) {
-                const int4 vprv = *reinterpret_cast<const int4 *>(fr + prv * PITCH);
-                *reinterpret_cast<int4 *>(rf) = vprv;
-                *reinterpret_cast<int4 *>(rf + PITCH) = vcur;
-                *reinterpret_cast<int4 *>(rf + 2 * PITCH) = vnew;
-            } else {
-                *reinterpret_cast<int4 *>(rf) = vcur;
-                *reinterpret_cast<int4 *>(rf + PITCH) = vnew;
+    ENV_CLK(3);
+    // ---- arrival (wave 1, which stored nothing yet): partials (write-through), ticket ----
+    // Every wave read ctl / R.count before the first barrier. Only the partial stores are
+    // drained before the ticket; the last arriver reduces after its share of phase C.
+    bool is_last = false;
+    if (tid >= 64 && tid < 128) {
+        if (with_acc) {
+            const bool d = lane < ne && !__builtin_isnan(s_epr[lane]);
+            const float er = d ? s_epr[lane] : 0.0f;
+            const int sc = d ? s_score[lane] : 0;
+            const int64_t cnt = wave_sum_i64(d ? 1 : 0);
+            const int64_t ssum = wave_sum_i64(sc);
+            const double rsum = wave_sum_f64((double)er);
+            const float rmax = wave_max_f32(d ? er : -INFINITY);
+            const int smax = wave_max_i32(sc);
+            if (lane < 4) {
+                const uint64_t word = lane == 0 ? (uint64_t)cnt
+                                    : lane == 1 ? (uint64_t)ssum
+                                    : lane == 2 ? (uint64_t)__double_as_longlong(rsum)
+                                                : ((uint64_t)(uint32_t)__float_as_uint(rmax) |
+                                                   ((uint64_t)(uint32_t)smax << 32));
+                st_sc1(E.part + (int64_t)blockIdx.x * 4 + lane, word);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        uint32_t prev_n = 0;
+        if (lane == 0) prev_n = __hip_atomic_fetch_add(E.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = __shfl(prev_n, 0, 64) == gridDim.x - 1;
+        ENV_CLK1(4);
+    }
+
+    // ---- Phase C: patched boards -> frame ring (+ replay slot) -----------
+    // in groups of PG pieces per thread: the b_{t-1} loads of a group go out together
+    constexpr int PG = 4;
+    const bool rd_prv = store && R.C == 2;
+    for (int k0 = 0; k0 < NPT; k0 += PG) {
+        i32x4 vp[PG];
+        if (rd_prv) {
+#pragma clang loop unroll(full)
+            for (int k = 0; k < PG; ++k) {
+                const int idx = tid + (k0 + k) * ENV_NT;
+                if (k0 + k < NPT && idx < ne * NCH) {
+                    const int el = idx / NCH, c = idx - el * NCH;
+                    vp[k] = *reinterpret_cast<const i32x4 *>(E.frames + ((e0 + el) * 3 + prv) * PITCH + c * 16);
+                }
             }
         }
-        if (f & 2) {
-            // auto-reset: next state is (b0, b0) (structs.jl:53 n_frames copies)
-            const int4 v0 = *reinterpret_cast<const int4 *>(E.init_board + c * 16);
-            *reinterpret_cast<int4 *>(fr + nxt * PITCH) = v0;
-            if (E.C == 2) *reinterpret_cast<int4 *>(fr + cur * PITCH) = v0;
-        } else {
-            *reinterpret_cast<int4 *>(fr + nxt * PITCH) = vnew;
+#pragma clang loop unroll(full)
+        for (int k = 0; k < PG; ++k) {
+            const int idx = tid + (k0 + k) * ENV_NT;
+            if (k0 + k < NPT && idx < ne * NCH) {
+                const int el = idx / NCH, c = idx - el * NCH;
+                const int64_t ge = e0 + el;
+                const uint8_t f = s_flag[el];
+                const i32x4 vcur = *reinterpret_cast<const i32x4 *>(sb + idx * 16);
+                const i32x4 vnew = (f & 1) ? patch16(vcur, c * 16, s_pc + el * 4) : vcur;
+                int8_t *fr = E.frames + ge * 3 * PITCH + c * 16;
+                if (store && (f & 1)) {
+                    const int64_t slot = (rc + ge) % R.cap;
+                    int8_t *rf = R.frames + slot * (int64_t)(R.C + 1) * PITCH + c * 16;
+                    if (rd_prv) {
+                        *reinterpret_cast<i32x4 *>(rf) = vp[k];
+                        *reinterpret_cast<i32x4 *>(rf + PITCH) = vcur;
+                        *reinterpret_cast<i32x4 *>(rf + 2 * PITCH) = vnew;
+                    } else {
+                        *reinterpret_cast<i32x4 *>(rf) = vcur;
+                        *reinterpret_cast<i32x4 *>(rf + PITCH) = vnew;
+                    }
+                }
+                if (f & 2) {
+                    // auto-reset: next state is (b0, b0) (structs.jl:53 n_frames copies)
+                    const i32x4 v0 = *reinterpret_cast<const i32x4 *>(E.init_board + c * 16);
+                    *reinterpret_cast<i32x4 *>(fr + nxt * PITCH) = v0;
+                    if (E.C == 2) *reinterpret_cast<i32x4 *>(fr + cur * PITCH) = v0;
+                } else {
+                    *reinterpret_cast<i32x4 *>(fr + nxt * PITCH) = vnew;
+                }
+            }
         }
     }
-}
 
-__global__ void env_advance_kernel(Ctl *ctl, int64_t *replay_count, int64_t n) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        ctl->t += 1;
-        if (replay_count) *replay_count += n;
+#ifdef SNK_ENV_CLOCKS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ENV_CLK(5);
+    ENV_CLK1(6);
+#endif
+    if (!is_last) return;
+    if (with_acc) {
+        int64_t cnt = 0, ssum = 0;
+        double rsum = 0.0;
+        float rmax = -INFINITY;
+        int smax = 0;
+        for (int g0 = 0; g0 < (int)gridDim.x; g0 += 64) {
+            const int g = g0 + lane;
+            int64_t c1 = 0, s1 = 0;
+            double r1 = 0.0;
+            float m1 = -INFINITY;
+            int sm1 = 0;
+            if (g < (int)gridDim.x) {
+                const uint64_t *p = E.part + (int64_t)g * 4;
+                c1 = (int64_t)ld_sc1(p);
+                s1 = (int64_t)ld_sc1(p + 1);
+                r1 = __longlong_as_double((long long)ld_sc1(p + 2));
+                const uint64_t w3 = ld_sc1(p + 3);
+                m1 = __uint_as_float((uint32_t)w3);
+                sm1 = (int)(uint32_t)(w3 >> 32);
+            }
+            cnt += wave_sum_i64(c1);
+            ssum += wave_sum_i64(s1);
+            rsum += wave_sum_f64(r1);
+            rmax = fmaxf(rmax, wave_max_f32(m1));
+            smax = max(smax, wave_max_i32(sm1));
+        }
+        if (lane == 0) {
+            *acc.episodes += cnt;
+            *acc.reward_sum += rsum;
+            *acc.score_sum += ssum;
+            if (cnt > 0) {
+                *acc.reward_max = fmaxf(*acc.reward_max, rmax);
+                *acc.score_max = max(*acc.score_max, smax);
+            }
+            *acc.env_steps += E.n;
+        }
+    }
+    if (lane == 0) {
+        E.ctl->t = t + 1;
+        if (store) *R.count = rc + E.n;
+        __hip_atomic_store(E.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -225,10 +442,7 @@ __global__ void env_reset_kernel(EnvDev E, const uint8_t *__restrict__ mask) {
     uint16_t *ring = E.ring + e * E.ring_cap;
     ring[0] = (uint16_t)((E.bs - 3) + E.bs);
     ring[1] = (uint16_t)((E.bs - 2) + E.bs);
-    EnvState ns{};
-    ns.head = 0;
-    ns.len = 2;
-    E.state[e] = ns;
+    E.state[e] = EnvState::fresh(E.bs);
     E.ep_reward[e] = 0.0f;
 }
 
@@ -253,35 +467,25 @@ __global__ void env_synth_kernel(EnvDev E, uint64_t seed, uint8_t *__restrict__ 
     act[e] = (uint8_t)((rng_hash(seed, (uint64_t)e, (uint64_t)E.ctl->t) >> 32) % 3);
 }
 
-void env_launch_step(const EnvDev &E, const uint8_t *act, int act_mode, const ReplayDev *R,
-                     hipStream_t s) {
+void env_launch_step(const EnvDev &E, const uint8_t *act, int act_mode, const ReplayDev *R, hipStream_t s,
+                     const EpisodeAcc *acc) {
     ReplayDev r{};
     if (R) r = *R;
-    const int grid = ceil_div(E.n, 64);
+    EpisodeAcc ea{};
+    if (acc) ea = *acc;
+    const int wa = acc ? 1 : 0;
+    const int grid = ceil_div(E.n, ENV_NE);
     const int store = R ? 1 : 0;
+#define SNK_ENV_CASE(P) \
+    case P: env_step_kernel<P><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, store, ea, wa); break;
     switch (E.pitch) {
-        case 48: env_step_kernel<48><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 64: env_step_kernel<64><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 96: env_step_kernel<96><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 112: env_step_kernel<112><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 128: env_step_kernel<128><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 144: env_step_kernel<144><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 176: env_step_kernel<176><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 208: env_step_kernel<208><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 240: env_step_kernel<240><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 256: env_step_kernel<256><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 304: env_step_kernel<304><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 336: env_step_kernel<336><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 368: env_step_kernel<368><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
-        case 400: env_step_kernel<400><<<grid, 64, 0, s>>>(E, act, act_mode, r, store); break;
+        SNK_ENV_CASE(48) SNK_ENV_CASE(64) SNK_ENV_CASE(96) SNK_ENV_CASE(112) SNK_ENV_CASE(128)
+        SNK_ENV_CASE(144) SNK_ENV_CASE(176) SNK_ENV_CASE(208) SNK_ENV_CASE(240) SNK_ENV_CASE(256)
+        SNK_ENV_CASE(304) SNK_ENV_CASE(336) SNK_ENV_CASE(368) SNK_ENV_CASE(400)
         default: SNK_CHECK(false, SNK_ERR_INVALID, "unsupported board pitch %d", E.pitch);
     }
+#undef SNK_ENV_CASE
     launch_check("env_step_kernel");
-}
-
-void env_launch_advance(const EnvDev &E, const ReplayDev *R, hipStream_t s) {
-    env_advance_kernel<<<1, 64, 0, s>>>(E.ctl, R ? R->count : nullptr, E.n);
-    launch_check("env_advance_kernel");
 }
 
 }  // namespace snk
@@ -352,6 +556,9 @@ extern "C" int snk_env_create(snk_env *out, int64_t n, int32_t bs, int32_t C, ui
         d.out_score = dalloc<uint8_t>(n);
         d.fault_count = dalloc<uint32_t>(1);
         d.ctl = dalloc<Ctl>(1);
+        d.ticket = dalloc<uint32_t>(1);
+        d.part = dalloc<uint64_t>((size_t)ceil_div(n, ENV_NE) * 4);
+        SNK_HIP(hipMemsetAsync(d.ticket, 0, sizeof(uint32_t), s));
         h->scratch = dalloc<uint8_t>(n);
         h->gather = dalloc<int8_t>((size_t)n * C * d.ring_cap);
         SNK_HIP(hipMemsetAsync(d.fault_count, 0, sizeof(uint32_t), s));
@@ -377,6 +584,7 @@ extern "C" int snk_env_destroy(snk_env h) {
         for (void *p : {(void *)d.frames, (void *)d.ring, (void *)d.state, (void *)d.ep_reward,
                         (void *)d.out_reward, (void *)d.out_done, (void *)d.out_mask, (void *)d.out_dirs,
                         (void *)d.out_ep_reward, (void *)d.out_score, (void *)d.fault_count, (void *)d.ctl,
+                        (void *)d.ticket, (void *)d.part,
                         (void *)h->init_board, (void *)h->food, (void *)h->scratch, (void *)h->gather})
             dfree(p);
         delete h;
@@ -405,7 +613,6 @@ extern "C" int snk_env_step(snk_env h, const uint8_t *act_dev, int32_t act_mode)
                   "bad act_mode %d", act_mode);
         hipStream_t s = stream();
         env_launch_step(h->d, act_dev, act_mode, nullptr, s);
-        env_launch_advance(h->d, nullptr, s);
     });
 }
 
@@ -525,3 +732,25 @@ extern "C" int snk_env_info(snk_env h, int64_t *n, int32_t *bs, int32_t *C, int6
 namespace snk {
 const EnvDev &env_dev(snk_env h) { return h->d; }
 }
+
+#ifdef SNK_ENV_CLOCKS
+// profiling builds: out[g][8] = the phase stamps of the LAST step launch (call after it)
+extern "C" int snk_env_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t arm) {
+    return guard([&] {
+        static uint64_t *buf = nullptr;
+        static int64_t cap = 0;
+        if (arm) {
+            if (n_wg > cap) {
+                dfree(buf);
+                buf = dalloc<uint64_t>(n_wg * 8);
+                cap = n_wg;
+            }
+            SNK_HIP(hipMemset(buf, 0, n_wg * 8 * sizeof(uint64_t)));
+            SNK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_env_clk), &buf, sizeof(buf)));
+            return;
+        }
+        SNK_HIP(hipDeviceSynchronize());
+        SNK_HIP(hipMemcpy(out_host, buf, n_wg * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    });
+}
+#endif

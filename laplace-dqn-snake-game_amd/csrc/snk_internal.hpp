@@ -15,12 +15,28 @@ namespace snk {
 enum Dir : int { DIR_U = 0, DIR_D = 1, DIR_L = 2, DIR_R = 3 };  // utils.jl:8 order
 
 struct alignas(16) EnvState {
-    uint64_t food_used;  // consumed entries of the shared food list (<= 64)
-    uint16_t head;       // ring index of the head (pushfirst! decrements)
-    uint16_t len;        // snake length
-    uint16_t steps;      // real steps of the current episode
-    uint8_t flags;       // bits 0-1 prev_dir, bit 2 lost, bit 3 faulted
-    uint8_t score;
+    // word 0
+    uint64_t food_used : 50;  // consumed entries of the shared food list (n_food = 50)
+    uint64_t head_cell : 9;   // board cell of the head   (= ring[head]; bs <= 20: cell < 400)
+    uint64_t flags : 4;       // bits 0-1 prev_dir, bit 2 lost, bit 3 faulted
+    uint64_t pad0 : 1;
+    // word 1
+    uint64_t head : 9;        // ring index of the head (pushfirst! decrements)
+    uint64_t len : 9;         // snake length (<= bs^2)
+    uint64_t steps : 16;      // real steps of the current episode (max_hist < 60000)
+    uint64_t score : 8;
+    uint64_t tail_cell : 9;   // board cell of the tail (= ring[head + len - 1])
+    uint64_t pad1 : 13;
+    // the head and tail cells ride in the state so a step reads one body-ring entry (the
+    // new tail when the snake does not eat) instead of three scattered ones
+    __host__ __device__ static EnvState fresh(int bs) {   // structs.jl:47 snake (bs-2, 2), (bs-1, 2)
+        EnvState s{};
+        s.head = 0;
+        s.len = 2;
+        s.head_cell = (uint64_t)((bs - 3) + bs);
+        s.tail_cell = (uint64_t)((bs - 2) + bs);
+        return s;
+    }
 };
 static_assert(sizeof(EnvState) == 16, "EnvState must be 16 bytes");
 
@@ -51,6 +67,17 @@ struct EnvDev {
     const int8_t *init_board;  // [pitch] SnakeGame() board b0
     uint32_t *fault_count;
     Ctl *ctl;
+    uint32_t *ticket;     // arrival counter of the step kernel's workgroups (0 between launches)
+    uint64_t *part;       // [ceil(n / 64)][4] per-workgroup episode statistics (EpisodeAcc)
+};
+
+// Trainer statistics the step kernel folds in (episode_stats, utils.jl:478): the
+// last workgroup to finish reduces the per-workgroup partials in workgroup order.
+struct EpisodeAcc {
+    int64_t *episodes, *score_sum, *env_steps;
+    double *reward_sum;
+    float *reward_max;
+    int32_t *score_max;
 };
 
 struct ReplayDev {
@@ -80,9 +107,37 @@ __host__ __device__ inline int avail_index(int prev_dir, int dir) {
     return dir - (dir > rev ? 1 : 0);
 }
 
-// Launch helpers implemented in the .hip files
+// sample(rpb) (utils.jl:280-287) for a batch of <= 64: Floyd's algorithm on the counter
+// stream, one wave (lane n draws t_n; a ballot finds an earlier equal pick)
+struct SampleRider {
+    const int64_t *count = nullptr;   // transitions stored so far (device)
+    int64_t cap = 0, pending = 0;     // pending: transitions the coming step stores
+    int32_t batch = 0;
+    uint64_t seed = 0, draw = 0;
+    const int64_t *draw_dev = nullptr;
+    int64_t *out = nullptr;           // [batch] slots; nullptr: no rider
+    int32_t *b_out = nullptr;
+};
+__device__ inline void sample_wave(const SampleRider &r) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t draw = r.draw_dev ? (uint64_t)*r.draw_dev : r.draw;
+    const int64_t len = min(*r.count + r.pending, r.cap);
+    const int B = (int)min((int64_t)r.batch, len);
+    const int64_t t = lane < B ? (int64_t)__umul64hi(rng_hash(r.seed, draw, (uint64_t)lane), (uint64_t)(len - B + lane + 1))
+                               : -1;
+    int64_t v = -2;
+    for (int n = 0; n < B; ++n) {
+        const int64_t tn = __shfl(t, n, 64);
+        const bool hit = __ballot(lane < n && v == tn) != 0;
+        if (lane == n) v = hit ? len - B + n : tn;
+    }
+    if (lane < B) r.out[lane] = v;
+    if (lane == 0 && r.b_out) *r.b_out = B;
+}
+// Launch helpers implemented in the .hip files. One launch is a whole lockstep
+// step: its last workgroup also advances ctl->t (and the replay count when
+// storing) and, with acc, folds the finished episodes into the trainer stats.
 void env_launch_step(const EnvDev &E, const uint8_t *act, int act_mode, const ReplayDev *R,
-                     hipStream_t s);
-void env_launch_advance(const EnvDev &E, const ReplayDev *R, hipStream_t s);
+                     hipStream_t s, const EpisodeAcc *acc = nullptr);
 
 }  // namespace snk

@@ -891,7 +891,6 @@ static void lap_rollout(snk_dqn m, const float *W, int64_t ldw, int64_t G, float
         lap_act_kernel<<<(unsigned)G, 256, lds, s>>>(L, W, ldw, src, fin, act, nullptr);
         launch_check("lap_act_kernel");
         env_launch_step(E, act, SNK_ACT_INDEX, &R, s);
-        env_launch_advance(E, &R, s);
         lap_track_kernel<<<(unsigned)ceil_div(G, 256), 256, 0, s>>>(E.out_done, E.out_ep_reward, G, t, fin, len_dev,
                                                                     rew_dev, nfin);
         launch_check("lap_track_kernel");

@@ -394,9 +394,14 @@ struct Conv1Args {
 };
 struct Conv1Pair {
     Conv1Args g[2];
+    SampleRider rider;   // rider.out: the last workgroup of grid.y = 0 runs the replay sample
 };
 template <int C>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S, int bs, int NS) {
+    if (cp.rider.out && blockIdx.x == gridDim.x - 1) {   // the rider workgroup: independent of conv1
+        if (blockIdx.y == 0 && threadIdx.x < 64) sample_wave(cp.rider);
+        return;
+    }
     const Conv1Args &ca = cp.g[blockIdx.y];
     const BoardSrc &src = ca.src;
     const float *__restrict__ w = ca.w;
@@ -418,7 +423,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
     for (int i = threadIdx.x; i < NS * C * plane; i += blockDim.x) sx[i] = 0.0f;
     if (ca.wscan) {   // block-uniform
         __shared__ float red4[4];
-        wmax_block(ca.wscan, ca.wscan_n, ca.wpart, red4);
+        wmax_block(ca.wscan, ca.wscan_n, ca.wpart, red4, (int)gridDim.x - (cp.rider.out ? 1 : 0));
     }
     __syncthreads();
     const int nel = ns * C * ncell;
@@ -850,7 +855,8 @@ bool qnet_fused23(const QLayout &L, const float *th, const float *wt, const uint
     return h3s_ok(L, &net, 1, S) && h3c2_on() && !w.has_train;
 }
 
-static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi) {
+static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi,
+                           const SampleRider *rider = nullptr) {
     const int bs = L.bs, nc = L.ncell;
     const bool h3 = h3s_ok(L, net, ng, S);
     // h3 also for conv2 (conv_h3c2_kernel): conv1 then writes fp32 a1 only. SNK_H3C2=0: x6 conv2.
@@ -861,9 +867,10 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         // 20 us against 25 at 8; 1 sample per workgroup costs the per-workgroup weight/board latency)
         constexpr int c1div = 1024;
         const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S * ng / c1div));
-        const dim3 grid((unsigned)ceil_div(S, ns), (unsigned)ng);
+        const dim3 grid((unsigned)(ceil_div(S, ns) + (rider ? 1 : 0)), (unsigned)ng);
         const size_t lds = (size_t)(9 * L.C * 16 + 16 + ((ns * L.C * (bs + 2) * (bs + 2) + 3) & ~3) + 256 * 24) * sizeof(float);
         Conv1Pair cp{};
+        if (rider) cp.rider = *rider;
         for (int g = 0; g < 2; ++g) {
             const FwdNet &n = net[g < ng ? g : 0];
             // x6: a1 also (acting: only) as bf16 planes for conv2
@@ -879,7 +886,7 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         launch_check("conv1_fwd_kernel");
         for (int g = 0; g < ng; ++g) {
             net[g].w->x0_valid = net[g].w->has_train ? 1 : 0;
-            net[g].w->wmax_n = h3 ? (int)grid.x : 0;
+            net[g].w->wmax_n = h3 ? (int)ceil_div(S, ns) : 0;
             net[g].w->wmax_img = h3 ? net[g].wt + L.off_t3 : nullptr;
         }
     }
@@ -954,10 +961,12 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
 }
 
 void qnet_forward(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
-                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only, const uint16_t *wtb) {
+                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only, const uint16_t *wtb,
+                  const SampleRider *rider) {
     const FwdNet net{th, wt, wtb, src, &w};
+    SNK_CHECK(!rider || (only < 0 && rider->batch <= 64), SNK_ERR_INTERNAL, "sample rider: full forward, batch <= 64");
     if (only < 0)
-        forward_layers(L, &net, 1, S, s, 0, 3);
+        forward_layers(L, &net, 1, S, s, 0, 3, rider);
     else if (only == QNET_ONLY_CONV23)
         forward_layers(L, &net, 1, S, s, 1, 2);
     else if (only < 4)
@@ -1225,8 +1234,10 @@ struct UpdArgs {
     GradSlabs g;
     float *grad;
     UpdateTarget u;
-    int finish, apply;
+    PostUpdate post;
+    int finish, apply, has_post;
 };
+
 
 // index of packed parameter i in the forward weight image, or -1; x6 = its
 // plane-0 index in the bf16 split image (planes CK*CN apart)
@@ -1300,43 +1311,60 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
             g = a.grad[i];
         }
         if (a.apply && t < 195) apply_one(a, L, i, g, due, omr);
-        return;
-    }
-    const int64_t nthreads = (int64_t)(gridDim.x - 1) * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L.off_d2w; i += nthreads) {
-        float g = a.grad[i];
-        if (a.finish) {
+    } else {
+        const int64_t nthreads = (int64_t)(gridDim.x - 1) * blockDim.x;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L.off_d2w; i += nthreads) {
+            float g = a.grad[i];
+            if (a.finish) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int64_t j = i - a.g.off[k];
-                if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
-                    // slab_reduce order; the loads of 8 slabs go out together
-                    const float *sl = a.g.slab[k] + j;
-                    const int64_t n = a.g.n[k];
-                    const int zc = a.g.z[k];
-                    float v = 0.0f;
-                    int z = 0;
-                    for (; z + 8 <= zc; z += 8) {
-                        float x[8];
+                for (int k = 0; k < 4; ++k) {
+                    const int64_t j = i - a.g.off[k];
+                    if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
+                        // slab_reduce order; the loads of 8 slabs go out together
+                        const float *sl = a.g.slab[k] + j;
+                        const int64_t n = a.g.n[k];
+                        const int zc = a.g.z[k];
+                        float v = 0.0f;
+                        int z = 0;
+                        for (; z + 8 <= zc; z += 8) {
+                            float x[8];
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) x[u] = sl[(int64_t)(z + u) * n];
+                            for (int u = 0; u < 8; ++u) x[u] = sl[(int64_t)(z + u) * n];
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) v += x[u];
+                            for (int u = 0; u < 8; ++u) v += x[u];
+                        }
+                        for (; z < zc; ++z) v += sl[(int64_t)z * n];
+                        g = v;
                     }
-                    for (; z < zc; ++z) v += sl[(int64_t)z * n];
-                    g = v;
                 }
+                a.grad[i] = g;
             }
-            a.grad[i] = g;
+            if (a.apply) apply_one(a, L, i, g, due, omr);
         }
-        if (a.apply) apply_one(a, L, i, g, due, omr);
     }
+    // every block read *counter (nb) above; the last to arrive advances it. The bookkeeping
+    // reads nothing another block of this launch wrote, so the ticket needs no fence.
+    if (!a.has_post) return;
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(a.post.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    post_update_block(a.post);
+    if (threadIdx.x == 0) __hip_atomic_store(a.post.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
-                        hipStream_t s) {
+                        hipStream_t s, const PostUpdate *post) {
     UpdArgs a{};
     a.L = L;
+    if (post) {
+        a.post = *post;
+        a.has_post = 1;
+    }
     if (pending) a.g = *pending;
     a.grad = grad;
     if (apply) a.u = *apply;

@@ -129,9 +129,11 @@ void qnet_head(const QLayout &L, const float *theta, int64_t S, QWork &w, HeadMo
 constexpr int QNET_ONLY_CONV23 = 12;
 // whether an act forward of S samples runs conv2 + conv3 fused (conv_h3f_kernel)
 bool qnet_fused23(const QLayout &L, const float *theta, const float *wt, const uint16_t *wtb, int64_t S, QWork &w);
-// wtb (optional): bf16 split planes of the image -> conv2/conv3/Dense1 on the x6 kernels
+// wtb (optional): bf16 split planes of the image -> conv2/conv3/Dense1 on the x6 kernels.
+// rider (optional): a replay sample run by one extra workgroup of the conv1 launch
 void qnet_forward(const QLayout &L, const float *theta, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
-                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1, const uint16_t *wtb = nullptr);
+                  HeadMode mode, const HeadArgs &ha, hipStream_t s, int only = -1, const uint16_t *wtb = nullptr,
+                  const SampleRider *rider = nullptr);
 // Weight-gradient sections a backward left as K-split partial slabs (z > 1),
 // plus Dense2's gradient (a reduction of dq x h1 over the batch): finished
 // inside the update kernel instead of by separate reduce launches.
@@ -159,8 +161,41 @@ struct UpdateTarget {
     int64_t rate;
     float lr, rho, eps;
 };
+// the trainer's bookkeeping after an update (utils.jl:456-481: track_loss!, epsilon decay,
+// nb += 1), done by the last workgroup of the update pass to arrive (ticket)
+struct PostUpdate {
+    const double *loss;    // [B] per-sample Huber losses
+    int64_t B;
+    double *loss_out, *last_loss, *log;
+    int64_t log_cap;
+    int64_t *updates, *nb;
+    float *epsilon;
+    float decay, eps_end;
+    uint32_t *ticket;      // 0 between launches
+};
+// tr.losses / epsilon decay / nb += 1 after an update (utils.jl:456-481), the Huber
+// mean over the batch in a fixed order (256-thread strided sums, then a tree)
+__device__ inline void post_update_block(const PostUpdate &p) {   // 256 threads
+    __shared__ double sh[256];
+    double v = 0.0;
+    for (int64_t i = threadIdx.x; i < p.B; i += 256) v += p.loss[i];
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const double l = sh[0] / (double)p.B;
+    *p.loss_out = l;
+    *p.last_loss = l;
+    if (p.log) p.log[*p.updates % p.log_cap] = l;      // track_loss! (utils.jl:404-406)
+    *p.epsilon = fmaxf(*p.epsilon - p.decay, p.eps_end);  // utils.jl:480
+    *p.updates += 1;
+    *p.nb += 1;
+}
 void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
-                        hipStream_t s);
+                        hipStream_t s, const PostUpdate *post = nullptr);
 int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S);
 // raw launchers shared with the deeper net (snk_deep.hip): the head kernels read
 // only L.off_d1b / off_d2w / off_d2b; slab = ks partial Dense1 pre-activations [ks][S][64]

@@ -88,26 +88,7 @@ __global__ __launch_bounds__(256) void replay_sample_kernel(const int64_t *__res
 // The same draw for B <= 64 in one wave: lane n holds candidate t_n; the serial
 // pass broadcasts t_n and asks all earlier lanes at once (ballot) whether it
 // was already chosen. Same output as the LDS-set version.
-__global__ __launch_bounds__(64) void replay_sample_wave_kernel(const int64_t *__restrict__ count, int64_t cap,
-                                                                int32_t batch, uint64_t seed, uint64_t draw,
-                                                                const int64_t *__restrict__ draw_dev,
-                                                                int64_t *__restrict__ out, int32_t *__restrict__ b_out,
-                                                                int64_t pending) {
-    const int lane = threadIdx.x;
-    if (draw_dev) draw = (uint64_t)*draw_dev;
-    const int64_t len = min(*count + pending, cap);
-    const int B = (int)min((int64_t)batch, len);
-    const int64_t t = lane < B ? (int64_t)__umul64hi(rng_hash(seed, draw, (uint64_t)lane), (uint64_t)(len - B + lane + 1))
-                               : -1;
-    int64_t v = -2;
-    for (int n = 0; n < B; ++n) {
-        const int64_t tn = __shfl(t, n, 64);
-        const bool hit = __ballot(lane < n && v == tn) != 0;
-        if (lane == n) v = hit ? len - B + n : tn;
-    }
-    if (lane < B) out[lane] = v;
-    if (lane == 0 && b_out) *b_out = B;
-}
+__global__ __launch_bounds__(64) void replay_sample_wave_kernel(SampleRider r) { sample_wave(r); }
 
 __global__ void replay_store_kernel(ReplayDev R, int64_t B, const int8_t *__restrict__ frames,
                                     const uint8_t *__restrict__ act, const float *__restrict__ rew,
@@ -204,7 +185,6 @@ extern "C" int snk_env_step_store(snk_env env, const uint8_t *act_dev, int32_t a
         SNK_CHECK(E.bs == rb->d.bs && E.C == rb->d.C, SNK_ERR_INVALID, "env/replay geometry mismatch");
         hipStream_t s = stream();
         env_launch_step(E, act_dev, act_mode, &rb->d, s);
-        env_launch_advance(E, &rb->d, s);
     });
 }
 
@@ -217,17 +197,16 @@ extern "C" int snk_env_time_step(snk_env env, snk_replay rb, const uint8_t *act_
         hipEvent_t a, b;
         SNK_HIP(hipEventCreate(&a));
         SNK_HIP(hipEventCreate(&b));
-        double total = 0.0;
-        for (int r = 0; r < reps; ++r) {
-            SNK_HIP(hipEventRecord(a, s));
-            env_launch_step(E, act_dev, SNK_ACT_INDEX, rb ? &rb->d : nullptr, s);
-            SNK_HIP(hipEventRecord(b, s));
-            env_launch_advance(E, rb ? &rb->d : nullptr, s);
-            SNK_HIP(hipEventSynchronize(b));
-            float ms = 0.0f;
-            SNK_HIP(hipEventElapsedTime(&ms, a, b));
-            total += ms;
-        }
+        // back-to-back launches between one event pair: the steady-state time per step
+        // (kernel + launch boundary), as the trainer's graph runs it
+        env_launch_step(E, act_dev, SNK_ACT_INDEX, rb ? &rb->d : nullptr, s);   // warm
+        SNK_HIP(hipEventRecord(a, s));
+        for (int r = 0; r < reps; ++r) env_launch_step(E, act_dev, SNK_ACT_INDEX, rb ? &rb->d : nullptr, s);
+        SNK_HIP(hipEventRecord(b, s));
+        SNK_HIP(hipEventSynchronize(b));
+        float ms = 0.0f;
+        SNK_HIP(hipEventElapsedTime(&ms, a, b));
+        const double total = ms;
         *ms_out = total / reps;
         (void)hipEventDestroy(a);
         (void)hipEventDestroy(b);
@@ -301,8 +280,12 @@ extern "C" int snk_replay_empty(snk_replay h) {
 namespace snk {
 void replay_launch_sample(const ReplayDev &d, int32_t batch, uint64_t seed, uint64_t draw,
                           const int64_t *draw_dev, int64_t *idx, int32_t *b_dev, hipStream_t s, int64_t pending) {
-    if (batch <= 64)
-        replay_sample_wave_kernel<<<1, 64, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev, pending);
+    if (batch <= 64) {
+        SampleRider r;
+        r.count = d.count; r.cap = d.cap; r.pending = pending; r.batch = batch; r.seed = seed; r.draw = draw;
+        r.draw_dev = draw_dev; r.out = idx; r.b_out = b_dev;
+        replay_sample_wave_kernel<<<1, 64, 0, s>>>(r);
+    }
     else
         replay_sample_kernel<<<1, 256, 0, s>>>(d.count, d.cap, batch, seed, draw, draw_dev, idx, b_dev, pending);
     launch_check("replay_sample_kernel");

@@ -32,79 +32,8 @@ struct alignas(16) TrainStats {
     int32_t pad;
 };
 
-__global__ __launch_bounds__(1024) void episode_stats_kernel(const uint8_t *__restrict__ done,
-                                                             const float *__restrict__ ep_reward,
-                                                             const uint8_t *__restrict__ score, int64_t n,
-                                                             TrainStats *st, Ctl *ctl, int64_t *replay_count) {
-    __shared__ double s_r[1024];
-    __shared__ int64_t s_n[1024], s_s[1024];
-    __shared__ float s_m[1024];
-    __shared__ int32_t s_sm[1024];
-    double r = 0.0;
-    int64_t cnt = 0, ssum = 0;
-    float mx = -INFINITY;
-    int32_t smx = 0;
-    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) {
-        if (done[e]) {
-            const float v = ep_reward[e];
-            r += (double)v;
-            cnt += 1;
-            ssum += score[e];
-            mx = fmaxf(mx, v);
-            smx = max(smx, (int32_t)score[e]);
-        }
-    }
-    const int t = threadIdx.x;
-    s_r[t] = r; s_n[t] = cnt; s_s[t] = ssum; s_m[t] = mx; s_sm[t] = smx;
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if (t < o) {
-            s_r[t] += s_r[t + o];
-            s_n[t] += s_n[t + o];
-            s_s[t] += s_s[t + o];
-            s_m[t] = fmaxf(s_m[t], s_m[t + o]);
-            s_sm[t] = max(s_sm[t], s_sm[t + o]);
-        }
-        __syncthreads();
-    }
-    if (t == 0) {
-        st->episodes += s_n[0];
-        st->reward_sum += s_r[0];
-        st->score_sum += s_s[0];
-        if (s_n[0] > 0) {
-            st->reward_max = fmaxf(st->reward_max, s_m[0]);
-            st->score_max = max(st->score_max, s_sm[0]);
-        }
-        st->env_steps += n;
-        // env_advance_kernel folded in: the step is complete
-        ctl->t += 1;
-        if (replay_count) *replay_count += n;
-    }
-}
-
-// tr.losses / epsilon decay / nb += 1 after an update (utils.jl:456-481), with
-// the Huber mean over the batch reduced here (loss_mean_kernel's order)
-__global__ __launch_bounds__(256) void post_update_kernel(TrainStats *st, const double *__restrict__ loss, int64_t B,
-                                                          double *loss_out, double *log, int64_t log_cap,
-                                                          float decay, float eps_end) {
-    __shared__ double sh[256];
-    double v = 0.0;
-    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) v += loss[i];
-    sh[threadIdx.x] = v;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
-        __syncthreads();
-    }
-    if (threadIdx.x != 0) return;
-    const double l = sh[0] / (double)B;
-    *loss_out = l;
-    st->last_loss = l;
-    if (log) log[st->updates % log_cap] = l;          // track_loss! (utils.jl:404-406)
-    st->epsilon = fmaxf(st->epsilon - decay, eps_end); // utils.jl:480
-    st->updates += 1;
-    st->nb += 1;
-}
+// the post-update bookkeeping as its own launch (the deeper net's update path)
+__global__ __launch_bounds__(256) void post_update_kernel(PostUpdate p) { post_update_block(p); }
 
 void comm_allreduce_mean(snk_comm h, float *buf, int64_t n, hipStream_t s);
 void comm_broadcast(snk_comm h, float *buf, int64_t n, int root, hipStream_t s);
@@ -125,6 +54,7 @@ struct snk_trainer_s {
     int64_t *idx = nullptr;
     double *loss_log = nullptr;
     int64_t log_cap = 0;
+    uint32_t *ticket = nullptr;   // grad_update_kernel's arrival counter (post-update fold)
     int32_t B = 64;
     // [2 * learn + unrolled]: one iteration, or `unroll` iterations back to back in one
     // graph (iterations only communicate through device counters, so a longer graph is
@@ -152,7 +82,16 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     snk_dqn_s *q = h->dqn;
     const bool upd = learn && n_upd > 0;
     const uint64_t sseed = h->cfg.seed ^ 0x5A4D504C45ULL;
-    if (upd) replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s, E.n);
+    // the first update's sample (counting the n transitions this step stores) rides in a
+    // spare workgroup of the act forward's conv1 launch (small net, batch <= 64)
+    const bool ride = upd && !q->deep && h->B <= 64;
+    SampleRider rider;
+    if (ride) {
+        rider.count = R.count; rider.cap = R.cap; rider.pending = E.n; rider.batch = h->B; rider.seed = sseed;
+        rider.draw_dev = &h->stats->updates; rider.out = h->idx;
+    } else if (upd) {
+        replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s, E.n);
+    }
     HeadArgs ha;
     ha.act = h->act;
     ha.seed = h->cfg.seed;
@@ -161,11 +100,12 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     if (q->deep)
         deep_forward(q, SNK_NET_Q, src_env(E), E.n, HEAD_ACT, ha, s);
     else
-        qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q);
-    env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s);
-    episode_stats_kernel<<<1, 1024, 0, s>>>(E.out_done, E.out_ep_reward, E.out_score, E.n, h->stats, E.ctl,
-                                            R.count);
-    launch_check("episode_stats_kernel");
+        qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q,
+                     ride ? &rider : nullptr);
+    // step! + virtual_step + store! + the episode statistics, one launch
+    const EpisodeAcc acc{&h->stats->episodes, &h->stats->score_sum, &h->stats->env_steps, &h->stats->reward_sum,
+                         &h->stats->reward_max, &h->stats->score_max};
+    env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s, &acc);
     if (!upd) return;
     for (int u = 0; u < n_upd; ++u) {
         if (u > 0) replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s);
@@ -180,23 +120,26 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
         lo.defer = &pend;
         lo.loss_mean = false;
         dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s, lo);
+        const PostUpdate post{q->deep ? deep_batch_losses(q) : q->trn.loss, h->B, q->loss_dev, &h->stats->last_loss,
+                              h->loss_log, h->log_cap, &h->stats->updates, &h->stats->nb, &h->stats->epsilon,
+                              h->cfg.decay, h->cfg.epsilon_end, h->ticket};
         if (q->deep) {   // the deeper bf16 net: finished gradient, [mean over ranks], RMSProp + images + target
             if (h->comm) comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
             deep_apply(q, &h->stats->nb, h->cfg.target_update_rate, s);
+            post_update_kernel<<<1, 256, 0, s>>>(post);
+            launch_check("post_update_kernel");
         } else {
-            // one pass: finish the gradient, RMSProp, forward image, update_target_net! when nb % rate == 0
+            // one pass: finish the gradient, RMSProp, forward image, update_target_net! when
+            // nb % rate == 0, and (last block to arrive) the post-update bookkeeping
             const UpdateTarget ut = dqn_update_target(q, &h->stats->nb, h->cfg.target_update_rate);
             if (h->comm) {   // data-parallel replicas: mean gradient before the step
                 grad_update_launch(q->L, &pend, q->grad, nullptr, s);
                 comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
-                grad_update_launch(q->L, nullptr, q->grad, &ut, s);
+                grad_update_launch(q->L, nullptr, q->grad, &ut, s, &post);
             } else {
-                grad_update_launch(q->L, &pend, q->grad, &ut, s);
+                grad_update_launch(q->L, &pend, q->grad, &ut, s, &post);
             }
         }
-        post_update_kernel<<<1, 256, 0, s>>>(h->stats, q->deep ? deep_batch_losses(q) : q->trn.loss, h->B, q->loss_dev,
-                                             h->loss_log, h->log_cap, h->cfg.decay, h->cfg.epsilon_end);
-        launch_check("post_update_kernel");
     }
 }
 
@@ -222,6 +165,8 @@ extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, sn
         h->act = dalloc<uint8_t>(E.n);
         h->idx = dalloc<int64_t>(h->B);
         h->loss_log = dalloc<double>(h->log_cap);
+        h->ticket = dalloc<uint32_t>(1);
+        SNK_HIP(hipMemsetAsync(h->ticket, 0, sizeof(uint32_t), s));
         // iterations per captured graph: they only communicate through device
         // counters, so a longer graph is the same launch sequence with the
         // graph launch gap paid once per `unroll` (measured 12.34 M env-steps/s
@@ -260,7 +205,8 @@ extern "C" int snk_trainer_destroy(snk_trainer h) {
         if (!h) return;
         (void)hipStreamSynchronize(stream());
         h->drop_graphs();
-        for (void *p : {(void *)h->stats, (void *)h->act, (void *)h->idx, (void *)h->loss_log}) dfree(p);
+        for (void *p : {(void *)h->stats, (void *)h->act, (void *)h->idx, (void *)h->loss_log, (void *)h->ticket})
+            dfree(p);
         delete h;
     });
 }

@@ -328,3 +328,38 @@ def test_train_episode_schedule(snk):
         eps = max(np.float32(eps - np.float32(0.05)), np.float32(0.6))
     assert np.float32(s0["epsilon"]) == eps
     assert s0["buffer_length"] == 300
+
+
+@pytest.mark.parametrize("n_envs", [4096, 200])
+def test_trainer_episode_stats_fold(snk, n_envs):
+    """The step kernel's last workgroup folds the finished episodes into the
+    trainer statistics (episode_stats, utils.jl:478) and advances the step and
+    replay counters. Checked iteration by iteration against the step's own
+    outputs accumulated on the host: episodes, score sum, reward max, score max
+    and env-steps exact; the Float64 reward sum within 1e-12 relative (the
+    device reduces per-workgroup partials in workgroup order). 200 envs leave a
+    partial last workgroup."""
+    tr = snk.Trainer(n_batches=10, n_envs=n_envs, board_size=12, n_frames=2, capacity=4 * n_envs, epsilon=1.0,
+                     decay=0.0, seed=3)
+    s0 = tr.stats()
+    t0 = tr.game.t
+    ep, ss, rs, rm, sm = 0, 0, 0.0, -np.inf, 0
+    for it in range(60):
+        tr.run(1, learn=False, graph=(it % 2 == 0))
+        o = tr.game.last("done", "ep_reward", "score")
+        d = o["done"].astype(bool)
+        ep += int(d.sum())
+        ss += int(o["score"][d].astype(np.int64).sum())
+        rs += float(o["ep_reward"][d].astype(np.float64).sum())
+        if d.any():
+            rm = max(rm, float(o["ep_reward"][d].max()))
+            sm = max(sm, int(o["score"][d].max()))
+    st = tr.stats()
+    assert ep > 0
+    assert st["episodes"] - s0["episodes"] == ep
+    assert st["score_sum"] - s0["score_sum"] == ss
+    assert st["env_steps"] - s0["env_steps"] == 60 * n_envs
+    assert np.float32(st["reward_max"]) == np.float32(rm) and st["score_max"] == sm
+    assert abs(st["reward_sum"] - rs) <= 1e-12 * max(1.0, abs(rs))
+    assert tr.game.t == t0 + 60
+    assert len(tr.buffer) == min(60 * n_envs, 4 * n_envs)
