@@ -7,23 +7,25 @@
 // optionally store! of the transition into the replay ring (utils.jl:267-277)
 // and the trainer's episode statistics (utils.jl:478).
 //
-// Mapping: a workgroup of 4 waves owns 64 envs (NE).
-//   Phase A  all 256 threads stream the 64 current boards (16-byte pieces,
-//            consecutive threads -> consecutive bytes) HBM -> LDS; wave 0
-//            first issues its lanes' state / action / body-ring loads so their
-//            latency hides under the board stream;
-//   Phase B  wave 0, lane e = env e, runs the scalar logic against the
-//            UNMODIFIED LDS board: O(1) collision (board[new_head] replaces the
+// Mapping: a workgroup of 2 waves owns 64 envs (NE).
+//   Phase A  all 128 threads stream the 64 current boards (16-byte pieces,
+//            consecutive threads -> consecutive bytes) HBM -> registers, where
+//            they stay until phase C; LDS gets a 2-bit copy (value + 1 per cell).
+//            Wave 0 first issues its lanes' state / action / episode-reward loads
+//            so their latency hides under the board stream;
+//   Phase B  wave 0, lane e = env e, runs the scalar logic against the packed
+//            UNMODIFIED board: O(1) collision (board[new_head] replaces the
 //            reference's O(L) body scan), food-list probe, next-state suicidal
 //            mask. The <= 3 changed cells (tail -> 0, head -> 1, food -> 2) are
 //            recorded as patches, and the logic reads the new board through them;
-//   Phase C  all threads write the new boards (LDS piece + patches) to the frame
-//            ring and, when storing, b_{t-C}..b_t into the replay slot (b_{t-1}
-//            read from HBM in the same pass).
-// LDS is the boards only (64 * pitch), so 4-wave workgroups keep 6 (20x20) to 8
-// (12x12) workgroups = 24-32 waves per CU streaming. Per env-step HBM traffic is
-// 2 * pitch + 45 B (+ (C + 1) * pitch written and (C - 1) * pitch read when
-// storing): every board byte is touched once in each direction.
+//   Phase C  every thread patches its register pieces and writes the new boards
+//            to the frame ring and, when storing, b_{t-C}..b_t into the replay
+//            slot (b_{t-1} read from HBM in the same pass).
+// The boards live in registers (13 pieces per thread at 20x20), so LDS (a 6.4 KB
+// packed copy) does not cap the envs in flight: 4-5 waves per SIMD = 512-640 envs
+// per CU. Per env-step HBM traffic is 2 * pitch + 45 B (+ (C + 1) * pitch written
+// and (C - 1) * pitch read when storing): every board byte is touched once in each
+// direction; the body ring is touched once (one entry read, one written).
 // The last workgroup to arrive (agent-scope ticket) advances the step counter
 // and the replay count, and reduces the per-workgroup episode partials in
 // workgroup order (deterministic), so a step is ONE launch.
@@ -34,7 +36,7 @@
 
 namespace snk {
 
-constexpr int ENV_NE = 64, ENV_NT = 256;
+constexpr int ENV_NE = 64, ENV_NT = 128;
 // Profiling builds only (make clocks): per-workgroup phase timestamps (100 MHz realtime
 // counter) into a debug buffer, read back by snk_env_debug_clocks.
 #ifdef SNK_ENV_CLOCKS
@@ -107,17 +109,35 @@ __device__ __forceinline__ int wave_max_i32(int v) {
     return v;
 }
 
-// workgroups per CU the LDS admits (6 at most: 85 VGPRs): the register budget is sized for them
-template <int PITCH>
-constexpr int env_wg_per_cu() {
-    return (160 * 1024) / (ENV_NE * PITCH + 1024) < 6 ? (160 * 1024) / (ENV_NE * PITCH + 1024) : 6;
+// board cell c from the packed LDS copy (2-bit codes, value + 1: -1 wall .. 2 food)
+__device__ __forceinline__ int cell_at(const uint32_t *bp, int c) {
+    return (int)((bp[c >> 4] >> ((c & 15) * 2)) & 3u) - 1;
+}
+// 16 board bytes -> 16 2-bit codes (byte + 1, carry-free per byte)
+__device__ __forceinline__ uint32_t pack16(const i32x4 v) {
+    uint32_t out = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t x = (uint32_t)v[w];
+        const uint32_t inc = (((x & 0x7f7f7f7fu) + 0x01010101u) ^ (x & 0x80808080u)) & 0x03030303u;
+        const uint32_t cmp = (inc | (inc >> 6) | (inc >> 12) | (inc >> 18)) & 0xffu;
+        out |= cmp << (8 * w);
+    }
+    return out;
 }
 
+// Boards stay in the registers of the thread that loaded them (NPT 16-byte pieces per
+// thread, 13 at 20x20); LDS holds only a 2-bit copy for the logic lanes (100 B per env at
+// 20x20), so LDS no longer caps the envs in flight: 2-wave workgroups, 5 per SIMD.
 template <int PITCH>
-__global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kernel(EnvDev E, const uint8_t *__restrict__ act, int act_mode,
-                                                          ReplayDev R, int store, EpisodeAcc acc, int with_acc) {
+constexpr int env_waves_per_simd() { return PITCH > 304 ? 4 : 5; }   // the register budget of NPT pieces
+
+template <int PITCH>
+__global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_kernel(EnvDev E, const uint8_t *__restrict__ act,
+                                                             int act_mode, ReplayDev R, int store, EpisodeAcc acc,
+                                                             int with_acc) {
     constexpr int NCH = PITCH / 16, NPT = (ENV_NE * NCH + ENV_NT - 1) / ENV_NT;
-    __shared__ __attribute__((aligned(16))) int8_t sb[ENV_NE * PITCH];
+    __shared__ uint32_t sbp[ENV_NE * NCH];                              // packed boards
     __shared__ __attribute__((aligned(8))) int16_t s_pc[ENV_NE * 4];   // patch cells (tail, head, food), -1 = none
     __shared__ uint8_t s_flag[ENV_NE];                                  // bit0 stepped, bit1 reset
     __shared__ int16_t s_food[64];
@@ -134,7 +154,7 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
     const int64_t rc = store ? *R.count : 0;
     const int bs = E.bs, cap = E.ring_cap;
 
-    // ---- wave 0: per-env scalar loads first (state -> body ring cells) ----
+    // ---- wave 0: per-env loads first (state, action, episode reward) ----
     const bool live = w0 && lane < ne;
     const int64_t e = e0 + lane;
     EnvState st{};
@@ -144,32 +164,31 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
         st = E.state[e];
         a = act[e];
         epr0 = E.ep_reward[e];
-        const uint16_t *ring = E.ring + e * cap;
-        tail_idx = (int)st.head + (int)st.len - 1;
-        if (tail_idx >= cap) tail_idx -= cap;
         head_cell = (int)st.head_cell;
         tail_cell = (int)st.tail_cell;
-        tail_next = ring[tail_idx == 0 ? cap - 1 : tail_idx - 1];   // the new tail unless the snake eats
+        tail_next = (int)st.tail_next;   // the new tail unless the snake eats
     }
     if (w0 && lane < E.n_food) s_food[lane] = E.food[lane];
     ENV_CLK(1);
 
-    // ---- Phase A: current boards HBM -> LDS ------------------------------
-    {
-        i32x4 v[NPT];
+    // ---- Phase A: current boards HBM -> registers (+ packed copy in LDS) ----
+    // slot-major ring: the workgroup's 64 boards of a slot are one contiguous 64 * PITCH run
+    const int8_t *fcur = E.frames + ((int64_t)cur * E.n + e0) * PITCH;
+    int8_t *fnxt = E.frames + ((int64_t)nxt * E.n + e0) * PITCH;
+    const int8_t *fprv = E.frames + ((int64_t)prv * E.n + e0) * PITCH;
+    i32x4 vcur[NPT];
 #pragma clang loop unroll(full)
-        for (int k = 0; k < NPT; ++k) {
-            const int idx = tid + k * ENV_NT;
-            if (idx < ne * NCH) {
-                const int el = idx / NCH, c = idx - el * NCH;
-                v[k] = *reinterpret_cast<const i32x4 *>(E.frames + ((e0 + el) * 3 + cur) * PITCH + c * 16);
-            }
+    for (int k = 0; k < NPT; ++k) {
+        const int idx = tid + k * ENV_NT;
+        if (idx < ne * NCH) {
+            const int el = idx / NCH, c = idx - el * NCH;
+            vcur[k] = *reinterpret_cast<const i32x4 *>(fcur + idx * 16);
         }
+    }
 #pragma clang loop unroll(full)
-        for (int k = 0; k < NPT; ++k) {
-            const int idx = tid + k * ENV_NT;
-            if (idx < ne * NCH) *reinterpret_cast<i32x4 *>(sb + idx * 16) = v[k];
-        }
+    for (int k = 0; k < NPT; ++k) {
+        const int idx = tid + k * ENV_NT;
+        if (idx < ne * NCH) sbp[idx] = pack16(vcur[k]);
     }
     __syncthreads();
     ENV_CLK(2);
@@ -181,22 +200,26 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
     if (live) {
         uint8_t flag = 0;
         int16_t pc[3] = {-1, -1, -1};
-        const int8_t *b = sb + lane * PITCH;
+        const uint32_t *bp = sbp + lane * NCH;
         const int prev = st.flags & 3;
         if (!(st.flags & 4)) {
             flag = 1;
             const int dir = act_mode == SNK_ACT_INDEX ? avail_action(prev, a % 3) : (a & 3);
             uint16_t *ring = E.ring + e * cap;
+            // the cell after the new tail (next step's tail_next), read now, used at the end
+            tail_idx = (int)st.head + (int)st.len - 1;
+            if (tail_idx >= cap) tail_idx -= cap;
+            const int ring2 = ring[tail_idx >= 2 ? tail_idx - 2 : tail_idx - 2 + cap];
             // grow_maybe! (utils.jl:66-81)
             const int nh = head_cell + dir_delta(bs, dir);
-            const int old = b[nh];
+            const int old = cell_at(bp, nh);
             const bool eat = old == 2;
             float reward = eat ? 1.0f : -0.01f;
             uint64_t used = st.food_used;
             int food_cell = -1;
             bool fault = false;
             int score = st.score;
-            auto cell_old = [&](int c) { return (int)b[c]; };
+            auto cell_old = [&](int c) { return cell_at(bp, c); };
             if (eat) {
                 score += 1;
                 const int k = food_search(cell_old, s_food, E.n_food, used);   // pre-update board
@@ -218,7 +241,7 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
             pc[1] = (int16_t)nh;
             pc[2] = (int16_t)food_cell;
             auto cell_new = [&](int c) {
-                return c == food_cell ? 2 : c == nh ? 1 : (!eat && c == tail_cell) ? 0 : (int)b[c];
+                return c == food_cell ? 2 : c == nh ? 1 : (!eat && c == tail_cell) ? 0 : cell_at(bp, c);
             };
             const int nhead = st.head == 0 ? cap - 1 : st.head - 1;
             ring[nhead] = (uint16_t)nh;
@@ -276,6 +299,7 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
                 ns.score = (uint8_t)score;
                 ns.head_cell = (uint64_t)nh;
                 ns.tail_cell = (uint64_t)ntail_cell;
+                ns.tail_next = (uint64_t)(eat ? tail_next : nlen == 2 ? nh : ring2);
                 E.state[e] = ns;
                 E.ep_reward[e] = epr;
             }
@@ -325,16 +349,36 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        uint32_t prev_n = 0;
-        if (lane == 0) prev_n = __hip_atomic_fetch_add(E.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = __shfl(prev_n, 0, 64) == gridDim.x - 1;
+        // with statistics: ONE counter (the partials' hand-off: release by the drained sc1
+        // stores above, acquire by the last arriver's sc1 loads). Without: shard k =
+        // blockIdx % 8 counts its workgroups, the last of a shard adds to the top counter
+        // (8 shards: no single word serialises 4096 arrivals)
+        const int nwg = (int)gridDim.x;
+        uint32_t last = 0;
+        if (lane == 0) {
+            if (with_acc) {
+                last = __hip_atomic_fetch_add(E.ticket + 8 * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       (uint32_t)(nwg - 1);
+            } else {
+                const int k = (int)(blockIdx.x & 7);
+                const uint32_t size_k = (uint32_t)((nwg - k + 7) >> 3);
+                if (__hip_atomic_fetch_add(E.ticket + k * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    size_k - 1) {
+                    __hip_atomic_store(E.ticket + k * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last = __hip_atomic_fetch_add(E.ticket + 8 * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                           (uint32_t)(min(nwg, 8) - 1);
+                }
+            }
+        }
+        is_last = __shfl(last, 0, 64) != 0;
         ENV_CLK1(4);
     }
 
     // ---- Phase C: patched boards -> frame ring (+ replay slot) -----------
     // in groups of PG pieces per thread: the b_{t-1} loads of a group go out together
-    constexpr int PG = 4;
+    constexpr int PG = 2;
     const bool rd_prv = store && R.C == 2;
+#pragma clang loop unroll(full)
     for (int k0 = 0; k0 < NPT; k0 += PG) {
         i32x4 vp[PG];
         if (rd_prv) {
@@ -342,8 +386,7 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
             for (int k = 0; k < PG; ++k) {
                 const int idx = tid + (k0 + k) * ENV_NT;
                 if (k0 + k < NPT && idx < ne * NCH) {
-                    const int el = idx / NCH, c = idx - el * NCH;
-                    vp[k] = *reinterpret_cast<const i32x4 *>(E.frames + ((e0 + el) * 3 + prv) * PITCH + c * 16);
+                    vp[k] = *reinterpret_cast<const i32x4 *>(fprv + idx * 16);
                 }
             }
         }
@@ -354,28 +397,27 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
                 const int el = idx / NCH, c = idx - el * NCH;
                 const int64_t ge = e0 + el;
                 const uint8_t f = s_flag[el];
-                const i32x4 vcur = *reinterpret_cast<const i32x4 *>(sb + idx * 16);
-                const i32x4 vnew = (f & 1) ? patch16(vcur, c * 16, s_pc + el * 4) : vcur;
-                int8_t *fr = E.frames + ge * 3 * PITCH + c * 16;
+                const i32x4 vc = vcur[k0 + k];
+                const i32x4 vnew = (f & 1) ? patch16(vc, c * 16, s_pc + el * 4) : vc;
                 if (store && (f & 1)) {
                     const int64_t slot = (rc + ge) % R.cap;
                     int8_t *rf = R.frames + slot * (int64_t)(R.C + 1) * PITCH + c * 16;
                     if (rd_prv) {
                         *reinterpret_cast<i32x4 *>(rf) = vp[k];
-                        *reinterpret_cast<i32x4 *>(rf + PITCH) = vcur;
+                        *reinterpret_cast<i32x4 *>(rf + PITCH) = vc;
                         *reinterpret_cast<i32x4 *>(rf + 2 * PITCH) = vnew;
                     } else {
-                        *reinterpret_cast<i32x4 *>(rf) = vcur;
+                        *reinterpret_cast<i32x4 *>(rf) = vc;
                         *reinterpret_cast<i32x4 *>(rf + PITCH) = vnew;
                     }
                 }
                 if (f & 2) {
                     // auto-reset: next state is (b0, b0) (structs.jl:53 n_frames copies)
                     const i32x4 v0 = *reinterpret_cast<const i32x4 *>(E.init_board + c * 16);
-                    *reinterpret_cast<i32x4 *>(fr + nxt * PITCH) = v0;
-                    if (E.C == 2) *reinterpret_cast<i32x4 *>(fr + cur * PITCH) = v0;
+                    *reinterpret_cast<i32x4 *>(fnxt + idx * 16) = v0;
+                    if (E.C == 2) *reinterpret_cast<i32x4 *>(E.frames + ((int64_t)cur * E.n + e0) * PITCH + idx * 16) = v0;
                 } else {
-                    *reinterpret_cast<i32x4 *>(fr + nxt * PITCH) = vnew;
+                    *reinterpret_cast<i32x4 *>(fnxt + idx * 16) = vnew;
                 }
             }
         }
@@ -427,7 +469,7 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
     if (lane == 0) {
         E.ctl->t = t + 1;
         if (store) *R.count = rc + E.n;
-        __hip_atomic_store(E.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(E.ticket + 8 * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -435,10 +477,11 @@ __global__ __launch_bounds__(ENV_NT, env_wg_per_cu<PITCH>()) void env_step_kerne
 __global__ void env_reset_kernel(EnvDev E, const uint8_t *__restrict__ mask) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E.n || (mask && !mask[e])) return;
-    int8_t *fr = E.frames + e * 3 * E.pitch;
-    for (int s = 0; s < 3; ++s)
+    for (int s = 0; s < 3; ++s) {
+        int8_t *fr = E.frames + ((int64_t)s * E.n + e) * E.pitch;
         for (int c = 0; c < E.pitch; c += 16)
-            *reinterpret_cast<int4 *>(fr + s * E.pitch + c) = *reinterpret_cast<const int4 *>(E.init_board + c);
+            *reinterpret_cast<int4 *>(fr + c) = *reinterpret_cast<const int4 *>(E.init_board + c);
+    }
     uint16_t *ring = E.ring + e * E.ring_cap;
     ring[0] = (uint16_t)((E.bs - 3) + E.bs);
     ring[1] = (uint16_t)((E.bs - 2) + E.bs);
@@ -457,7 +500,7 @@ __global__ void env_gather_kernel(EnvDev E, int nf, int8_t *__restrict__ out) {
         const int r = (int)(i - e * nf * ncell);
         const int f = r / ncell, c = r - f * ncell;
         const int slot = (int)((t + 3 - (nf - 1 - f)) % 3);
-        out[i] = E.frames[(e * 3 + slot) * E.pitch + c];
+        out[i] = E.frames[((int64_t)slot * E.n + e) * E.pitch + c];
     }
 }
 
@@ -556,9 +599,9 @@ extern "C" int snk_env_create(snk_env *out, int64_t n, int32_t bs, int32_t C, ui
         d.out_score = dalloc<uint8_t>(n);
         d.fault_count = dalloc<uint32_t>(1);
         d.ctl = dalloc<Ctl>(1);
-        d.ticket = dalloc<uint32_t>(1);
+        d.ticket = dalloc<uint32_t>(9 * 32);
         d.part = dalloc<uint64_t>((size_t)ceil_div(n, ENV_NE) * 4);
-        SNK_HIP(hipMemsetAsync(d.ticket, 0, sizeof(uint32_t), s));
+        SNK_HIP(hipMemsetAsync(d.ticket, 0, 9 * 32 * sizeof(uint32_t), s));
         h->scratch = dalloc<uint8_t>(n);
         h->gather = dalloc<int8_t>((size_t)n * C * d.ring_cap);
         SNK_HIP(hipMemsetAsync(d.fault_count, 0, sizeof(uint32_t), s));

@@ -1,7 +1,8 @@
 // snk_internal.hpp — device-side data layout of libsnakehip.
 //
 // HBM layout (all SoA, sized for 288 GB HBM3E):
-//   env frames  int8  [n][3][pitch]   ring of the last 3 boards per env
+//   env frames  int8  [3][n][pitch]   ring of the last 3 boards, slot-major (a slot of
+//                                     all envs is one contiguous stream)
 //   env ring    u16   [n][bs*bs]      snake body ring (head index moves down)
 //   env state   16 B  [n]             EnvState below (one 128-bit load/store)
 //   replay      int8  [cap][C+1][pitch] + SoA metadata [cap]
@@ -26,15 +27,18 @@ struct alignas(16) EnvState {
     uint64_t steps : 16;      // real steps of the current episode (max_hist < 60000)
     uint64_t score : 8;
     uint64_t tail_cell : 9;   // board cell of the tail (= ring[head + len - 1])
-    uint64_t pad1 : 13;
-    // the head and tail cells ride in the state so a step reads one body-ring entry (the
-    // new tail when the snake does not eat) instead of three scattered ones
+    uint64_t tail_next : 9;   // the cell the tail moves to (= ring[head + len - 2])
+    uint64_t pad1 : 4;
+    // head, tail and next-tail cells ride in the state: a step issues its one body-ring
+    // read (the tail's next-but-one, for the NEXT step) after the state has arrived and
+    // consumes it only when it writes the new state
     __host__ __device__ static EnvState fresh(int bs) {   // structs.jl:47 snake (bs-2, 2), (bs-1, 2)
         EnvState s{};
         s.head = 0;
         s.len = 2;
         s.head_cell = (uint64_t)((bs - 3) + bs);
         s.tail_cell = (uint64_t)((bs - 2) + bs);
+        s.tail_next = s.head_cell;
         return s;
     }
 };
@@ -52,7 +56,7 @@ struct alignas(16) Ctl {
 struct EnvDev {
     int64_t n;
     int bs, C, pitch, max_hist, autoreset, n_food, ring_cap;
-    int8_t *frames;       // [n][3][pitch]
+    int8_t *frames;       // [3][n][pitch]: slot (t % 3) of env e at (slot * n + e) * pitch
     uint16_t *ring;       // [n][ring_cap]
     EnvState *state;      // [n]
     float *ep_reward;     // [n] running episode reward (utils.jl:207)
@@ -67,7 +71,8 @@ struct EnvDev {
     const int8_t *init_board;  // [pitch] SnakeGame() board b0
     uint32_t *fault_count;
     Ctl *ctl;
-    uint32_t *ticket;     // arrival counter of the step kernel's workgroups (0 between launches)
+    uint32_t *ticket;     // arrival counters of the step kernel's workgroups, 0 between launches:
+                          // [k * 32] shard k = blockIdx % 8, [8 * 32] the top / single counter
     uint64_t *part;       // [ceil(n / 64)][4] per-workgroup episode statistics (EpisodeAcc)
 };
 

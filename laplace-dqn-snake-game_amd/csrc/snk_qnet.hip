@@ -19,6 +19,7 @@
 #include "snk_conv_x6.hpp"
 #include "snk_loaders.hpp"
 #include "snk_qnet.hpp"
+#include "snk_upd_fwd.hpp"
 
 namespace snk {
 
@@ -976,6 +977,52 @@ void qnet_forward(const QLayout &L, const float *th, const float *wt, const Boar
 }
 
 void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s) {
+    forward_layers(L, net, 2, S, s, 0, 3);
+}
+
+template <int HIN, int C>
+static void upd_fwd_launch_t(const UpdFwdArgs &a, hipStream_t s) {
+    constexpr size_t lds = (size_t)updf_lds_bytes(HIN, C);
+    static_assert(lds <= 160 * 1024, "upd_fwd LDS");
+    set_lds_limit((const void *)upd_fwd_kernel<HIN, C>, lds);
+    upd_fwd_kernel<HIN, C><<<dim3((unsigned)(2 * a.S), 2), 256, lds, s>>>(a);
+    launch_check("upd_fwd_kernel");
+}
+
+// board sides with an instantiated fused update forward (the others take the layer path)
+static bool upd_fwd_launch(const UpdFwdArgs &a, hipStream_t s) {
+#define SNK_UPDF(B)                                                             \
+    case B:                                                                     \
+        if (a.L.C == 1) upd_fwd_launch_t<B, 1>(a, s); else upd_fwd_launch_t<B, 2>(a, s); \
+        return true;
+    switch (a.L.bs) {
+        SNK_UPDF(8) SNK_UPDF(10) SNK_UPDF(12) SNK_UPDF(13) SNK_UPDF(16)
+        default: return false;
+    }
+#undef SNK_UPDF
+}
+
+void qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s) {
+    // the x6 weight planes of both nets are kept current by every theta change
+    if (net[0].wtb && net[1].wtb && (L.C == 1 || L.C == 2) && S >= 1 && S <= 4096) {
+        UpdFwdArgs a{};
+        a.L = L;
+        a.S = (int)S;
+        for (int g = 0; g < 2; ++g) {
+            QWork &w = *net[g].w;
+            const bool train = w.has_train != 0;
+            a.net[g] = UpdFwdNet{net[g].src, net[g].th, net[g].wtb, train ? w.a1 : nullptr, train ? w.a2 : nullptr,
+                                 w.a3, train ? w.x0 : nullptr};
+        }
+        if (upd_fwd_launch(a, s)) {
+            for (int g = 0; g < 2; ++g) {
+                net[g].w->x0_valid = net[g].w->has_train ? 1 : 0;
+                net[g].w->wmax_n = 0;   // no conv3 weight-max partials from this path
+            }
+            forward_layers(L, net, 2, S, s, 3, 3);   // Dense1 slabs
+            return;
+        }
+    }
     forward_layers(L, net, 2, S, s, 0, 3);
 }
 

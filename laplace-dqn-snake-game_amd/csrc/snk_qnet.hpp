@@ -41,24 +41,18 @@ struct BoardSrc {
     const int64_t *idx = nullptr;   // replay slot per sample
     const int64_t *tptr = nullptr;  // env frame-ring step counter
     int pitch = 0, C = 1, ncell = 0, chan0 = 0, replay_nf = 0;
+    int64_t slot_stride = 0;        // env frame ring: bytes between frame slots (n * pitch)
     __device__ __forceinline__ float load(int64_t s, int c, int cell) const {
         if (fbase) return fbase[(s * C + c) * ncell + cell];
-        const int8_t *p;
-        if (idx) {
-            p = base + idx[s] * (int64_t)replay_nf * pitch + (int64_t)(c + chan0) * pitch;
-        } else {
-            const int64_t t = *tptr;
-            const int slot = (int)((t + 3 - (C - 1 - c)) % 3);
-            p = base + (s * 3 + slot) * (int64_t)pitch;
-        }
-        return (float)p[cell];
+        return (float)plane(s, c)[cell];
     }
-    // int8 plane of (sample, channel); nullptr in float mode
+    // int8 plane of (sample, channel); nullptr in float mode. The env frame ring is
+    // slot-major ([3][n][pitch], slot_stride = n * pitch): slot = (t + 3 - (C - 1 - c)) % 3
     __device__ __forceinline__ const int8_t *plane(int64_t s, int c) const {
         if (fbase) return nullptr;
         if (idx) return base + idx[s] * (int64_t)replay_nf * pitch + (int64_t)(c + chan0) * pitch;
         const int slot = (int)((*tptr + 3 - (C - 1 - c)) % 3);
-        return base + (s * 3 + slot) * (int64_t)pitch;
+        return base + slot * slot_stride + s * (int64_t)pitch;
     }
 };
 
@@ -119,6 +113,10 @@ struct FwdNet {
 };
 // conv1 .. Dense1 of two independent nets over S samples each, both in every launch (grid z/y = net)
 void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s);
+// the update's two forwards (net[0] = t_net on s', net[1] = q_net on s, which keeps the
+// training activations) up to the Dense1 slabs: conv1-conv3 in one launch
+// (snk_upd_fwd.hpp) when the geometry allows, else the layer-by-layer path
+void qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s);
 // TD-target head of t_net and loss head of q_net (HeadArgs as for HEAD_LOSS) in one launch
 void qnet_head_pair(const QLayout &L, const float *theta_t, QWork &wt, const float *theta_q, QWork &wq, int64_t S,
                     const HeadArgs &ha, hipStream_t s);
