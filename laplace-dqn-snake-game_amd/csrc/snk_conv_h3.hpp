@@ -34,6 +34,7 @@
 #pragma once
 
 #include "snk_conv_x6.hpp"
+#include "snk_internal.hpp"
 
 namespace snk {
 
@@ -69,22 +70,28 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // partial max |w| of w[0, n): block b (256 threads) covers a grid-stride share; part[b]
-// block blockIdx.x of nblk scanning blocks (a launch may hold other workgroups too)
+// scanning block bid of nblk (a launch may hold other workgroups too)
 __device__ __forceinline__ void wmax_block(const float *__restrict__ w, int64_t n, float *__restrict__ part,
-                                           float *red4, int nblk) {
+                                           float *red4, int nblk, int bid) {
     float m = 0.0f;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)nblk * 256)
+    for (int64_t i = (int64_t)bid * 256 + threadIdx.x; i < n; i += (int64_t)nblk * 256)
         m = fmaxf(m, fabsf(w[i]));
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
+    if (threadIdx.x == 0) part[bid] = fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
 }
 
+// rd.out: workgroup 0 runs the replay sample instead (the trainer's rider, see SampleRider)
 static __global__ __launch_bounds__(256) void wmax_scan_kernel(const float *__restrict__ w, int64_t n,
-                                                        float *__restrict__ part) {
+                                                        float *__restrict__ part, SampleRider rd) {
+    const int rb = rd.out ? 1 : 0;
+    if (rb && blockIdx.x == 0) {
+        if (threadIdx.x < 64) sample_wave(rd);
+        return;
+    }
     __shared__ float red4[4];
-    wmax_block(w, n, part, red4, (int)gridDim.x);
+    wmax_block(w, n, part, red4, (int)gridDim.x - rb, (int)blockIdx.x - rb);
 }
 
 // conv3 (CK = 32 -> CN = 64, pad 0, EPI_BIAS_RELU) on the h3 split; ConvArgs:

@@ -1,5 +1,10 @@
-// snk_conv_h3f.hpp — conv2 + conv3 of the large-batch act forward in ONE kernel
-// on the h3 split (snk_conv_h3.hpp).
+// snk_conv_h3f.hpp — conv1 + conv2 + conv3 of the large-batch act forward in ONE
+// kernel on the h3 split (snk_conv_h3.hpp).
+//
+// conv1 (3x3, C -> 16, fp32 VALU in conv1_fwd_kernel's order, bit-identical) runs
+// first, from the workgroup's four boards staged as floats in LDS (in the conv3 B
+// buffers, idle until conv2 is done): a1 never goes to memory either, which saves
+// the conv1 launch and a1's write + re-read (9.2 KB per sample at 12x12).
 //
 // conv_h3s_kernel stages four samples' fp32 conv2 outputs (a2, 18 KB each at
 // 12x12) from HBM, takes a per-sample max and splits them into its LDS A image.
@@ -17,11 +22,14 @@
 #pragma once
 
 #include "snk_conv_h3.hpp"
+#include "snk_qnet.hpp"
 
 namespace snk {
 
 struct H3FArgs {
-    const float *a1;     // conv1 output [S][HIN^2][16] (fp32, relu'd)
+    BoardSrc src;        // the input planes (env frame ring, replay slots or floats)
+    const float *w1;     // conv1 weights W[(kk * C + ci) * 16 + co] (packed theta; C = the CF template)
+    const float *b1;     // conv1 bias [16]
     const float *w2;     // conv2 forward image [9 kk][32 co][16 ci]
     const float *b2;     // conv2 bias [32]
     const float *w3;     // conv3 forward image [36 kk][64 co][32 ci]
@@ -44,7 +52,7 @@ constexpr int h3f_lds_bytes() {
 
 // NBUF conv3 B buffers: 2 = one barrier per kernel offset (B(kk+2) staged while kk
 // runs); 4 = one barrier per offset PAIR (B(kk+3) staged, read two offsets later)
-template <int HIN, int NBUF = 4>
+template <int HIN, int NBUF = 4, int CF = 2>
 __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     static_assert(NBUF == 2 || NBUF == 4, "B buffers");
     constexpr int KS = 6, CN = 64, CK = 32, NSG = 4, NB = 2 * CN * CK / 8;
@@ -109,12 +117,57 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     }
     f32x4 wv[LW], av[LA];
     const f32x4 *w4 = reinterpret_cast<const f32x4 *>(a.w2);
-    const f32x4 *x4 = reinterpret_cast<const f32x4 *>(a.a1) + (int64_t)s0 * hin2 * 4;
     const int na4 = ns * hin2 * 4;
 #pragma unroll
     for (int u = 0; u < LW; ++u) wv[u] = w4[min(u * 512 + tid, NW4 - 1)];
+    {
+        // ---- conv1: boards -> bordered float planes in the B buffers; each thread always
+        // computes the same four output channels (4 (tid & 3) .. +3), so its 9 CF weight
+        // quads live in registers and a tap costs one LDS float
+        constexpr int C = CF;
+        float *xin = reinterpret_cast<float *>(Bs);    // [NSG][C][NPB]
+        static_assert(NSG * C * NPB <= NBUF * NB * 4, "conv1 staging fits the B buffers");
+        __shared__ const int8_t *pbase[NSG * C];
+        if (tid < NSG * C) pbase[tid] = tid / C < ns ? a.src.plane(s0 + tid / C, tid % C) : nullptr;
+        const int cq = tid & 3;
+        f32x4 w1r[9 * C], b1r;
 #pragma unroll
-    for (int u = 0; u < LA; ++u) av[u] = x4[min(u * 512 + tid, na4 - 1)];
+        for (int q = 0; q < 9 * C; ++q) w1r[q] = reinterpret_cast<const f32x4 *>(a.w1)[q * 4 + cq];
+        b1r = reinterpret_cast<const f32x4 *>(a.b1)[cq];
+        __syncthreads();
+        for (int q = tid; q < NSG * C * NPB; q += 512) {
+            const int sc = q / NPB, b = q - sc * NPB;
+            const int bj = b / BP, bi = b - bj * BP;
+            float v = 0.0f;
+            if (sc / C < ns && bi >= 1 && bi <= hin && bj >= 1 && bj <= hin) {
+                const int cell = (bi - 1) + (bj - 1) * hin;
+                const int8_t *pl = pbase[sc];
+                v = pl ? (float)pl[cell] : a.src.fbase[((int64_t)(s0 + sc / C) * C + sc % C) * hin2 + cell];
+            }
+            xin[q] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < LA; ++u) {   // output (sample, position, channels 4 cq..): a1's layout
+            const int e = min(u * 512 + tid, na4 - 1);
+            const int sr = e / (hin2 * 4), pos = (e - sr * hin2 * 4) >> 2;
+            const int j = pos / hin, i = pos - j * hin;
+            f32x4 acc = b1r;
+#pragma unroll
+            for (int kk = 0; kk < 9; ++kk) {
+                const int du = kk % 3, dv = kk / 3;
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const float x = xin[(sr * C + c) * NPB + (i + du) + (j + dv) * BP];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] = __builtin_fmaf(x, w1r[kk * C + c][q], acc[q]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = fmaxf(acc[q], 0.f);
+            av[u] = acc;
+        }
+    }
     float wm3 = 0.0f;
     for (int i = tid; i < a.nwmax; i += 512) wm3 = fmaxf(wm3, a.wmax[i]);
     float mw2 = 0.0f, ms[NSG] = {0.0f, 0.0f, 0.0f, 0.0f};

@@ -131,8 +131,9 @@ __device__ inline void sample_wave(const SampleRider &r) {
     const int64_t t = lane < B ? (int64_t)__umul64hi(rng_hash(r.seed, draw, (uint64_t)lane), (uint64_t)(len - B + lane + 1))
                                : -1;
     int64_t v = -2;
-    for (int n = 0; n < B; ++n) {
-        const int64_t tn = __shfl(t, n, 64);
+    for (int n = 0; n < B; ++n) {   // n is wave-uniform: v_readlane, not an LDS permute
+        const int64_t tn = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)t >> 32), n) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)t, n));
         const bool hit = __ballot(lane < n && v == tn) != 0;
         if (lane == n) v = hit ? len - B + n : tn;
     }

@@ -399,10 +399,13 @@ struct Conv1Pair {
 };
 template <int C>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S, int bs, int NS) {
-    if (cp.rider.out && blockIdx.x == gridDim.x - 1) {   // the rider workgroup: independent of conv1
+    // the rider is workgroup 0 (dispatched first, so its serial loop overlaps conv1)
+    const int rb = cp.rider.out ? 1 : 0;
+    if (rb && blockIdx.x == 0) {
         if (blockIdx.y == 0 && threadIdx.x < 64) sample_wave(cp.rider);
         return;
     }
+    const int bx = (int)blockIdx.x - rb;
     const Conv1Args &ca = cp.g[blockIdx.y];
     const BoardSrc &src = ca.src;
     const float *__restrict__ w = ca.w;
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
     const int bp = bs + 2, plane = bp * bp, ncell = bs * bs;
     for (int i = threadIdx.x; i < 9 * C * 16; i += blockDim.x) sw[i] = w[i];
     if (threadIdx.x < 16) sw[9 * C * 16 + threadIdx.x] = b[threadIdx.x];
-    const int64_t s0 = (int64_t)blockIdx.x * NS;
+    const int64_t s0 = (int64_t)bx * NS;
     const int ns = (int)min((int64_t)NS, S - s0);
     // plane base pointers once per (sample, channel): the element loads below
     // are then independent (no per-element ring-counter / slot-index load)
@@ -424,7 +427,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
     for (int i = threadIdx.x; i < NS * C * plane; i += blockDim.x) sx[i] = 0.0f;
     if (ca.wscan) {   // block-uniform
         __shared__ float red4[4];
-        wmax_block(ca.wscan, ca.wscan_n, ca.wpart, red4, (int)gridDim.x - (cp.rider.out ? 1 : 0));
+        wmax_block(ca.wscan, ca.wscan_n, ca.wpart, red4, (int)gridDim.x - rb, bx);
     }
     __syncthreads();
     const int nel = ns * C * ncell;
@@ -808,24 +811,31 @@ static void h3c2_launch_bs(const float *a1, const float *wimg, const float *b2, 
 }
 
 // conv3 B staging: 4 LDS buffers, one barrier per offset pair
-template <int HIN>
-static void h3f_launch_bs(const H3FArgs &fa, int64_t S, hipStream_t s) {
+template <int HIN, int CF>
+static void h3f_launch_t(const H3FArgs &fa, int64_t S, hipStream_t s) {
     constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, 4>();
     static_assert(lds <= 160 * 1024, "conv_h3f LDS");
-    set_lds_limit((const void *)conv_h3f_kernel<HIN, 4>, lds);
-    conv_h3f_kernel<HIN, 4><<<(unsigned)ceil_div(S, 4), 512, lds, s>>>(fa, (int)S);
+    set_lds_limit((const void *)conv_h3f_kernel<HIN, 4, CF>, lds);
+    conv_h3f_kernel<HIN, 4, CF><<<(unsigned)ceil_div(S, 4), 512, lds, s>>>(fa, (int)S);
     launch_check("conv_h3f_kernel");
 }
+template <int HIN>
+static void h3f_launch_bs(const H3FArgs &fa, int C, int64_t S, hipStream_t s) {
+    if (C == 1)
+        h3f_launch_t<HIN, 1>(fa, S, s);
+    else
+        h3f_launch_t<HIN, 2>(fa, S, s);
+}
 
-static void conv_h3f_launch(int bs, const H3FArgs &fa, int64_t S, hipStream_t s) {
+static void conv_h3f_launch(int bs, int C, const H3FArgs &fa, int64_t S, hipStream_t s) {
     SNK_CHECK(S <= INT32_MAX, SNK_ERR_INTERNAL, "h3f batch");
     switch (bs) {
-        case 8: h3f_launch_bs<8>(fa, S, s); return;
-        case 9: h3f_launch_bs<9>(fa, S, s); return;
-        case 10: h3f_launch_bs<10>(fa, S, s); return;
-        case 11: h3f_launch_bs<11>(fa, S, s); return;
-        case 12: h3f_launch_bs<12>(fa, S, s); return;
-        case 13: h3f_launch_bs<13>(fa, S, s); return;
+        case 8: h3f_launch_bs<8>(fa, C, S, s); return;
+        case 9: h3f_launch_bs<9>(fa, C, S, s); return;
+        case 10: h3f_launch_bs<10>(fa, C, S, s); return;
+        case 11: h3f_launch_bs<11>(fa, C, S, s); return;
+        case 12: h3f_launch_bs<12>(fa, C, S, s); return;
+        case 13: h3f_launch_bs<13>(fa, C, S, s); return;
         default: SNK_CHECK(false, SNK_ERR_INTERNAL, "h3f: board side outside 8..13");
     }
 }
@@ -863,6 +873,33 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
     // h3 also for conv2 (conv_h3c2_kernel): conv1 then writes fp32 a1 only. SNK_H3C2=0: x6 conv2.
     const bool h3c2 = h3 && h3c2_on();
     const int64_t n3 = 36LL * 32 * 64;   // conv3 weight image floats
+    // act forward (no backward needs a1/a2): conv1 + conv2 + conv3 in conv_h3f_kernel. Its
+    // "conv1" slot is the conv3 weight-max scan (the h3 weight scale), which also carries
+    // the sample rider.
+    bool f123 = h3c2;
+    for (int g = 0; g < ng; ++g) f123 = f123 && !net[g].w->has_train;
+    if (f123 && hi >= 0 && lo <= 2) {
+        for (int g = 0; g < ng; ++g) {
+            const FwdNet &n = net[g];
+            QWork &w = *n.w;
+            const float *img = n.wt + L.off_t3;
+            if ((lo <= 0 && hi >= 0) || !w.wmax_n || w.wmax_img != img) {
+                const SampleRider rd = (rider && g == 0) ? *rider : SampleRider{};
+                wmax_scan_kernel<<<256 + (rd.out ? 1 : 0), 256, 0, s>>>(img, n3, w.wmax_part, rd);
+                launch_check("wmax_scan_kernel");
+                w.wmax_n = 256;
+                w.wmax_img = img;
+            }
+            if (lo <= 2 && hi >= 1) {
+                H3FArgs fa{};
+                fa.src = n.src; fa.w1 = n.th + L.off_w1; fa.b1 = n.th + L.off_b1;
+                fa.w2 = n.wt + L.off_t2; fa.b2 = n.th + L.off_b2; fa.w3 = img; fa.wmax = w.wmax_part;
+                fa.nwmax = w.wmax_n; fa.b3 = n.th + L.off_b3; fa.out = w.a3;
+                conv_h3f_launch(L.bs, L.C, fa, S, s);
+            }
+        }
+        lo = std::max(lo, 3);
+    }
     if (lo <= 0 && hi >= 0) {
         // samples per workgroup: S*ng/1024 capped at 8 (4 at the 4096-env act forward: measured
         // 20 us against 25 at 8; 1 sample per workgroup costs the per-workgroup weight/board latency)
@@ -892,25 +929,6 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         }
     }
     FwdIO io[2];
-    // conv2 + conv3 fused (conv_h3f_kernel) when this call runs both
-    bool h3f = h3c2 && lo <= 1 && hi >= 2;
-    for (int g = 0; g < ng; ++g) h3f = h3f && !net[g].w->has_train;   // a backward needs a2 in memory
-    if (h3f) {
-        for (int g = 0; g < ng; ++g) {
-            const FwdNet &n = net[g];
-            QWork &w = *n.w;
-            if (!w.wmax_n || w.wmax_img != n.wt + L.off_t3) {   // conv1 did not scan this image
-                wmax_scan_kernel<<<256, 256, 0, s>>>(n.wt + L.off_t3, n3, w.wmax_part);
-                launch_check("wmax_scan_kernel");
-                w.wmax_n = 256;
-                w.wmax_img = n.wt + L.off_t3;
-            }
-            const H3FArgs fa{w.a1, n.wt + L.off_t2, n.th + L.off_b2, n.wt + L.off_t3, w.wmax_part, w.wmax_n,
-                             n.th + L.off_b3, w.a3};
-            conv_h3f_launch(L.bs, fa, S, s);
-        }
-        lo = std::max(lo, 3);
-    }
     if (lo <= 1 && hi >= 1 && h3c2) {   // conv2 on the h3 kernel: fp32 a1 -> fp32 a2
         for (int g = 0; g < ng; ++g) conv_h3c2_launch(L, net[g], S, s);
     } else if (lo <= 1 && hi >= 1) {   // conv2: M = S*bs^2, K = 9 offsets x 16, N = 32
@@ -933,7 +951,7 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             if (h3) {
                 QWork &w = *n.w;
                 if (!w.wmax_n || w.wmax_img != n.wt + L.off_t3) {   // conv1 did not scan this image
-                    wmax_scan_kernel<<<256, 256, 0, s>>>(n.wt + L.off_t3, n3, w.wmax_part);
+                    wmax_scan_kernel<<<256, 256, 0, s>>>(n.wt + L.off_t3, n3, w.wmax_part, SampleRider{});
                     launch_check("wmax_scan_kernel");
                     w.wmax_n = 256;
                     w.wmax_img = n.wt + L.off_t3;
@@ -985,7 +1003,7 @@ static void upd_fwd_launch_t(const UpdFwdArgs &a, hipStream_t s) {
     constexpr size_t lds = (size_t)updf_lds_bytes(HIN, C);
     static_assert(lds <= 160 * 1024, "upd_fwd LDS");
     set_lds_limit((const void *)upd_fwd_kernel<HIN, C>, lds);
-    upd_fwd_kernel<HIN, C><<<dim3((unsigned)(2 * a.S), 2), 256, lds, s>>>(a);
+    upd_fwd_kernel<HIN, C><<<dim3((unsigned)(2 * a.S), 2), UPDF_NT, lds, s>>>(a);
     launch_check("upd_fwd_kernel");
 }
 
@@ -1391,17 +1409,27 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
     }
     // every block read *counter (nb) above; the last to arrive advances it. The bookkeeping
     // reads nothing another block of this launch wrote, so the ticket needs no fence.
+    // Arrivals are counted in 8 shards (blockIdx % 8); the last of a shard adds to the top
+    // counter (one word would serialise every block's atomic).
     if (!a.has_post) return;
     __shared__ int s_last;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(a.post.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == gridDim.x - 1;
+        const int nwg = (int)gridDim.x, k = (int)(blockIdx.x & 7);
+        uint32_t *tk = a.post.ticket;
+        int last = 0;
+        if (__hip_atomic_fetch_add(tk + k * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (uint32_t)(((nwg - k + 7) >> 3) - 1)) {
+            __hip_atomic_store(tk + k * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = __hip_atomic_fetch_add(tk + 8 * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   (uint32_t)(min(nwg, 8) - 1);
+        }
+        s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
     post_update_block(a.post);
-    if (threadIdx.x == 0) __hip_atomic_store(a.post.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(a.post.ticket + 8 * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
@@ -1419,7 +1447,7 @@ void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad,
     a.apply = apply != nullptr;
     if (!a.finish && !a.apply) return;
     if (a.apply && !a.u.counter) a.u.rate = 1;
-    grad_update_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.off_d2w, 256), 2048) + 1, 256, 0, s>>>(a);
+    grad_update_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.off_d2w, 256), 1024) + 1, 256, 0, s>>>(a);
     launch_check("grad_update_kernel");
 }
 
@@ -1526,3 +1554,26 @@ void loss_mean_launch(const double *loss, int64_t B, double *out, hipStream_t s)
 }
 
 }  // namespace snk
+
+#ifdef SNK_ENV_CLOCKS
+using namespace snk;
+// profiling builds: out[wg][8] = upd_fwd_kernel phase stamps of the LAST launch (call after it)
+extern "C" int snk_upd_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t arm) {
+    return guard([&] {
+        static uint64_t *buf = nullptr;
+        static int64_t cap = 0;
+        if (arm) {
+            if (n_wg > cap) {
+                dfree(buf);
+                buf = dalloc<uint64_t>(n_wg * 8);
+                cap = n_wg;
+            }
+            SNK_HIP(hipMemset(buf, 0, n_wg * 8 * sizeof(uint64_t)));
+            SNK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_upd_clk), &buf, sizeof(buf)));
+            return;
+        }
+        SNK_HIP(hipDeviceSynchronize());
+        SNK_HIP(hipMemcpy(out_host, buf, n_wg * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    });
+}
+#endif

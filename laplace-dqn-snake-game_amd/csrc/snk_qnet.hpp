@@ -169,7 +169,7 @@ struct PostUpdate {
     int64_t *updates, *nb;
     float *epsilon;
     float decay, eps_end;
-    uint32_t *ticket;      // 0 between launches
+    uint32_t *ticket;      // [9 * 32] arrival counters (8 shards + top), 0 between launches
 };
 // tr.losses / epsilon decay / nb += 1 after an update (utils.jl:456-481), the Huber
 // mean over the batch in a fixed order (256-thread strided sums, then a tree)

@@ -165,8 +165,8 @@ extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, sn
         h->act = dalloc<uint8_t>(E.n);
         h->idx = dalloc<int64_t>(h->B);
         h->loss_log = dalloc<double>(h->log_cap);
-        h->ticket = dalloc<uint32_t>(1);
-        SNK_HIP(hipMemsetAsync(h->ticket, 0, sizeof(uint32_t), s));
+        h->ticket = dalloc<uint32_t>(9 * 32);
+        SNK_HIP(hipMemsetAsync(h->ticket, 0, 9 * 32 * sizeof(uint32_t), s));
         // iterations per captured graph: they only communicate through device
         // counters, so a longer graph is the same launch sequence with the
         // graph launch gap paid once per `unroll` (measured 12.34 M env-steps/s

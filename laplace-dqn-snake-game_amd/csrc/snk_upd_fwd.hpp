@@ -18,7 +18,8 @@
 //            -> a2 (global, training net) and its split into LDS;
 //   phase 3  conv3 (6x6, 32 -> 64, this workgroup's 32 channels): A from the
 //            LDS image, B (the weight planes the update keeps current) streamed
-//            from L2 into registers one offset ahead; bias + relu -> a3.
+//            from L2 into registers eight offsets ahead, each wave only its own 16
+//            columns; bias + relu -> a3.
 // conv1 and conv2 run in both halves of a sample (they are ~20 % of the work);
 // only half 0 writes a1, a2 and x0. Dense1 and the heads follow as before.
 #pragma once
@@ -27,6 +28,19 @@
 #include "snk_qnet.hpp"
 
 namespace snk {
+
+// Profiling builds only (make clocks): per-workgroup phase timestamps, read back by
+// snk_upd_debug_clocks (slots: start, phase 0, 1, 2 done, phase 3 done)
+#ifdef SNK_ENV_CLOCKS
+__device__ uint64_t *g_upd_clk;
+#define UPD_CLK(slot)                                                                                  \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && g_upd_clk)                                                             \
+            g_upd_clk[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define UPD_CLK(slot) do { } while (0)
+#endif
 
 struct UpdFwdNet {
     BoardSrc src;
@@ -43,6 +57,7 @@ struct UpdFwdArgs {
 
 // LDS strides (halves): A1 position record 3 planes x 16 ch + 8 pad, A2 3 x 32 + 8
 constexpr int UPDF_A1S = 56, UPDF_A2S = 104;
+constexpr int UPDF_NT = 512;   // 8 waves: two per SIMD, so one wave's LDS / MFMA latency hides under the other's
 
 // floats of the input planes + conv1 weights, rounded up to a 16-byte boundary
 __host__ __device__ constexpr int updf_f32_words(int hin, int C) {
@@ -78,7 +93,7 @@ __device__ __forceinline__ f32x4v mfma_x6(const u32x4 *a, const u32x4 *b, f32x4v
 }
 
 template <int HIN, int C>
-__global__ __launch_bounds__(256) void upd_fwd_kernel(UpdFwdArgs args) {
+__global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     constexpr int BP = HIN + 2, NB = BP * BP, NC = HIN * HIN;
     constexpr int WO = HIN - 5, NO = WO * WO;
     constexpr int T2 = (NC + 15) / 16, T3 = (NO + 15) / 16;
@@ -90,6 +105,7 @@ __global__ __launch_bounds__(256) void upd_fwd_kernel(UpdFwdArgs args) {
     uint16_t *A2 = B2 + 9 * 3 * 32 * 16;                             // [NC][UPDF_A2S]
     static_assert((NB * UPDF_A1S * 2) % 16 == 0, "16-B regions");
 
+    UPD_CLK(0);
     const UpdFwdNet &n = args.net[blockIdx.y];
     const QLayout &L = args.L;
     const int s = blockIdx.x >> 1, half = blockIdx.x & 1;
@@ -98,31 +114,62 @@ __global__ __launch_bounds__(256) void upd_fwd_kernel(UpdFwdArgs args) {
     const int r = lane & 15, g = lane >> 4;
 
     // ---- phase 0: input planes, conv1 weights, conv2 weight planes, A1 border --------
-    for (int e = tid; e < C * NB; e += 256) {
-        const int c = e / NB, b = e - c * NB;
-        const int bj = b / BP, bi = b - bj * BP;
-        float v = 0.0f;
-        if (bi >= 1 && bi <= HIN && bj >= 1 && bj <= HIN) {
-            const int cell = (bi - 1) + (bj - 1) * HIN;
-            v = n.src.load(s, c, cell);
-            if (wr && n.x0) n.x0[((int64_t)s * C + c) * NC + cell] = v;
-        }
-        xin[e] = v;
-    }
-    for (int e = tid; e < 9 * C * 16; e += 256) w1[e] = n.th[L.off_w1 + e];
-    if (tid < 16) w1[9 * C * 16 + tid] = n.th[L.off_b1 + tid];
+    // (every load of a thread is issued before its first LDS store)
     {
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(n.wtb + 3 * L.off_t2);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(B2);
-        for (int e = tid; e < 9 * 3 * 32 * 16 / 8; e += 256) dst[e] = src[e];
-    }
-    for (int e = tid; e < NB * (UPDF_A1S / 8); e += 256) {   // zero the whole A1 image (border stays 0)
-        reinterpret_cast<u32x4 *>(A1)[e] = u32x4{0u, 0u, 0u, 0u};
+        constexpr int NB2 = 9 * 3 * 32 * 16 / 8, KB2 = (NB2 + UPDF_NT - 1) / UPDF_NT;   // conv2 planes, 16-B pieces
+        constexpr int KX = (C * NB + UPDF_NT - 1) / UPDF_NT;
+        const u32x4 *src2 = reinterpret_cast<const u32x4 *>(n.wtb + 3 * L.off_t2);
+        u32x4 bv[KB2];
+#pragma unroll
+        for (int k = 0; k < KB2; ++k) bv[k] = src2[min(tid + k * UPDF_NT, NB2 - 1)];
+        const int8_t *pl[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) pl[c] = n.src.plane(s, c);
+        float xv[KX];
+#pragma unroll
+        for (int k = 0; k < KX; ++k) {
+            const int e = tid + k * UPDF_NT;
+            const int c = e / NB, b = e - c * NB;
+            const int bj = b / BP, bi = b - bj * BP;
+            xv[k] = 0.0f;
+            if (e < C * NB && bi >= 1 && bi <= HIN && bj >= 1 && bj <= HIN) {
+                const int cell = (bi - 1) + (bj - 1) * HIN;
+                xv[k] = pl[c] ? (float)pl[c][cell] : n.src.fbase[((int64_t)s * C + c) * NC + cell];
+            }
+        }
+        constexpr int NW1 = 9 * C * 16 + 16;   // conv1 weights + bias: at most two per thread
+        static_assert(NW1 <= 2 * UPDF_NT, "conv1 weights");
+        float w1v[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int e = tid + k * UPDF_NT;
+            w1v[k] = e < 9 * C * 16 ? n.th[L.off_w1 + e] : e < NW1 ? n.th[L.off_b1 + e - 9 * C * 16] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < KX; ++k) {
+            const int e = tid + k * UPDF_NT;
+            if (e < C * NB) {
+                xin[e] = xv[k];
+                const int c = e / NB, b = e - c * NB;
+                const int bj = b / BP, bi = b - bj * BP;
+                if (wr && n.x0 && bi >= 1 && bi <= HIN && bj >= 1 && bj <= HIN)
+                    n.x0[((int64_t)s * C + c) * NC + (bi - 1) + (bj - 1) * HIN] = xv[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (tid + k * UPDF_NT < NW1) w1[tid + k * UPDF_NT] = w1v[k];
+#pragma unroll
+        for (int k = 0; k < KB2; ++k)
+            if (tid + k * UPDF_NT < NB2) reinterpret_cast<u32x4 *>(B2)[tid + k * UPDF_NT] = bv[k];
+        for (int e = tid; e < NB * (UPDF_A1S / 8); e += UPDF_NT)   // zero the whole A1 image (border stays 0)
+            reinterpret_cast<u32x4 *>(A1)[e] = u32x4{0u, 0u, 0u, 0u};
     }
     __syncthreads();
+    UPD_CLK(1);
 
     // ---- phase 1: conv1 (VALU), a1 and its split ---------------------------------------
-    for (int o = tid; o < NC * 16; o += 256) {
+    for (int o = tid; o < NC * 16; o += UPDF_NT) {
         const int p = o >> 4, co = o & 15;
         const int j = p / HIN, i = p - j * HIN;
         float acc = w1[9 * C * 16 + co];
@@ -143,99 +190,125 @@ __global__ __launch_bounds__(256) void upd_fwd_kernel(UpdFwdArgs args) {
         d[32] = l;
     }
     __syncthreads();
+    UPD_CLK(2);
 
     // ---- phase 2: conv2 on x6 MFMA: rows = the HIN^2 positions, 32 columns -------------
+    // wave w owns column tile w & 1 and row tiles (w >> 1) + 4u; offset pair p outermost so
+    // each B fragment is read from LDS once
     {
-        const float *b2 = n.th + L.off_b2;
-        for (int t = wave; t < T2; t += 4) {
-            const int q = min(t * 16 + r, NC - 1);
+        constexpr int NT2 = (T2 + 3) / 4;
+        const int ct = wave & 1, rt0 = wave >> 1;
+        const int col = ct * 16 + r;
+        const float bv = n.th[L.off_b2 + col];
+        int qb[NT2];
+        f32x4v acc[NT2];
+#pragma unroll
+        for (int u = 0; u < NT2; ++u) {
+            const int q = min((rt0 + 4 * u) * 16 + r, NC - 1);
             const int qj = q / HIN, qi = q - qj * HIN;
-            f32x4v acc[2] = {f32x4v{0.f, 0.f, 0.f, 0.f}, f32x4v{0.f, 0.f, 0.f, 0.f}};
+            qb[u] = qi + qj * BP;
+            acc[u] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
-            for (int p = 0; p < 5; ++p) {
-                const int kk = 2 * p + (g >> 1);   // k 0..15: offset 2p, k 16..31: offset 2p + 1
-                const bool live = kk < 9;
-                const int kc = live ? kk : 8, du = kc % 3, dv = kc / 3;
-                u32x4 a[3], b[2][3];
-                const uint16_t *pa = A1 + ((qi + du) + (qj + dv) * BP) * UPDF_A1S + 8 * (g & 1);
+        for (int p = 0; p < 5; ++p) {
+            const int kk = 2 * p + (g >> 1);   // k 0..15: offset 2p, k 16..31: offset 2p + 1
+            const bool live = kk < 9;
+            const int kc = live ? kk : 8, du = kc % 3, dv = kc / 3;
+            u32x4 b[3];
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) {
-                    a[pl] = live ? *reinterpret_cast<const u32x4 *>(pa + pl * 16) : u32x4{0u, 0u, 0u, 0u};
+            for (int pl = 0; pl < 3; ++pl)
+                b[pl] = live ? *reinterpret_cast<const u32x4 *>(B2 + ((kc * 3 + pl) * 32 + col) * 16 + 8 * (g & 1))
+                             : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-                    for (int ct = 0; ct < 2; ++ct)
-                        b[ct][pl] = live ? *reinterpret_cast<const u32x4 *>(
-                                               B2 + ((kc * 3 + pl) * 32 + ct * 16 + r) * 16 + 8 * (g & 1))
-                                         : u32x4{0u, 0u, 0u, 0u};
+            for (int u = 0; u < NT2; ++u) {
+                if (rt0 + 4 * u < T2) {   // wave-uniform
+                    const uint16_t *pa = A1 + (qb[u] + du + dv * BP) * UPDF_A1S + 8 * (g & 1);
+                    u32x4 a[3];
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl)
+                        a[pl] = live ? *reinterpret_cast<const u32x4 *>(pa + pl * 16) : u32x4{0u, 0u, 0u, 0u};
+                    acc[u] = mfma_x6(a, b, acc[u]);
                 }
-#pragma unroll
-                for (int ct = 0; ct < 2; ++ct) acc[ct] = mfma_x6(a, b[ct], acc[ct]);
             }
-            // C[row 4g + e][col r]: bias + relu -> a2 and its split
+        }
+        // C[row 4g + e][col r]: bias + relu -> a2 and its split
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-                const int col = ct * 16 + r;
-                const float bv = b2[col];
+        for (int u = 0; u < NT2; ++u) {
+            const int t = rt0 + 4 * u;
+            if (t >= T2) continue;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int row = t * 16 + 4 * g + e;
-                    if (row >= NC) continue;
-                    const float v = fmaxf(acc[ct][e] + bv, 0.f);
-                    if (wr && n.a2) n.a2[((int64_t)s * NC + row) * 32 + col] = v;
-                    uint16_t h, m, l;
-                    split3_scalar(v, h, m, l);
-                    uint16_t *d = A2 + row * UPDF_A2S + col;
-                    d[0] = h;
-                    d[32] = m;
-                    d[64] = l;
-                }
+            for (int e = 0; e < 4; ++e) {
+                const int row = t * 16 + 4 * g + e;
+                if (row >= NC) continue;
+                const float v = fmaxf(acc[u][e] + bv, 0.f);
+                if (wr && n.a2) n.a2[((int64_t)s * NC + row) * 32 + col] = v;
+                uint16_t h, m, l;
+                split3_scalar(v, h, m, l);
+                uint16_t *d = A2 + row * UPDF_A2S + col;
+                d[0] = h;
+                d[32] = m;
+                d[64] = l;
             }
         }
     }
     __syncthreads();
-
+    UPD_CLK(3);
     // ---- phase 3: conv3 on x6 MFMA: rows = the WO^2 output positions, 32 columns -------
+    // wave w owns column tile w & 1 (16 of the workgroup's 32 columns) and row tiles
+    // (w >> 1) + 4u: each wave streams only its own 16 columns of B (3 KB per offset) from
+    // L2 straight into registers, D offsets in flight; even and odd offsets accumulate
+    // separately (two independent MFMA chains), summed at the end
     {
-        const int n0 = half * 32;
+        constexpr int NTW = (T3 + 3) / 4;   // row tiles per wave
+        constexpr int D = 8;
+        const int ct = wave & 1, rt0 = wave >> 1;
+        const int col = half * 32 + ct * 16 + r;
         const float *b3 = n.th + L.off_b3;
-        // B fragment of column n0 + 16 ct + r, k = 8g..8g+7 of offset kk, plane pl:
+        // B fragment of column col, k = 8g..8g+7 of offset kk, plane pl:
         // planes [kk][3][64 co][32 ci] -> 16 contiguous bytes
-        const uint16_t *wb3 = n.wtb + 3 * L.off_t3 + (n0 + r) * 32 + 8 * g;
-        auto bload = [&](int kk, u32x4 (&b)[2][3]) {
+        const uint16_t *wb3 = n.wtb + 3 * L.off_t3 + col * 32 + 8 * g;
+        auto bload = [&](int kk, u32x4 (&b)[3]) {
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-                    b[ct][pl] = *reinterpret_cast<const u32x4 *>(wb3 + ((int64_t)(kk * 3 + pl) * 64 + ct * 16) * 32);
+            for (int pl = 0; pl < 3; ++pl)
+                b[pl] = *reinterpret_cast<const u32x4 *>(wb3 + (int64_t)(kk * 3 + pl) * 64 * 32);
         };
-        for (int t = wave; t < T3; t += 4) {
-            const int q = min(t * 16 + r, NO - 1);
+        int qb[NTW];
+        f32x4v acc[NTW][2];
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) {
+            const int q = min((rt0 + 4 * u) * 16 + r, NO - 1);
             const int qj = q / WO, qi = q - qj * WO;
-            f32x4v acc[2] = {f32x4v{0.f, 0.f, 0.f, 0.f}, f32x4v{0.f, 0.f, 0.f, 0.f}};
-            u32x4 bc[2][3], bn[2][3];
-            bload(0, bc);
-            for (int kk = 0; kk < 36; ++kk) {
-                if (kk + 1 < 36) bload(kk + 1, bn);
-                const int du = kk % 6, dv = kk / 6;
-                const uint16_t *pa = A2 + ((qi + du) + (qj + dv) * HIN) * UPDF_A2S + 8 * g;
-                u32x4 a[3];
+            qb[u] = qi + qj * HIN;
+            acc[u][0] = acc[u][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        }
+        u32x4 bq[D][3];
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const u32x4 *>(pa + pl * 32);
+        for (int d = 0; d < D; ++d) bload(d, bq[d]);
+#pragma clang loop unroll(full)
+        for (int kk = 0; kk < 36; ++kk) {
+            const int du = kk % 6, dv = kk / 6;
 #pragma unroll
-                for (int ct = 0; ct < 2; ++ct) acc[ct] = mfma_x6(a, bc[ct], acc[ct]);
+            for (int u = 0; u < NTW; ++u) {
+                if (rt0 + 4 * u < T3) {   // wave-uniform
+                    const uint16_t *pa = A2 + (qb[u] + du + dv * HIN) * UPDF_A2S + 8 * g;
+                    u32x4 a[3];
 #pragma unroll
-                for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                    for (int pl = 0; pl < 3; ++pl) bc[ct][pl] = bn[ct][pl];
-            }
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-                const int col = n0 + ct * 16 + r;
-                const float bv = b3[col];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int row = t * 16 + 4 * g + e;
-                    if (row < NO) n.a3[((int64_t)s * NO + row) * 64 + col] = fmaxf(acc[ct][e] + bv, 0.f);
+                    for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const u32x4 *>(pa + pl * 32);
+                    acc[u][kk & 1] = mfma_x6(a, bq[kk % D], acc[u][kk & 1]);
                 }
+            }
+            if (kk + D < 36) bload(kk + D, bq[kk % D]);
+        }
+        UPD_CLK(4);
+        const float bv = b3[col];
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) {
+            const int t = rt0 + 4 * u;
+            if (t >= T3) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = t * 16 + 4 * g + e;
+                if (row < NO) n.a3[((int64_t)s * NO + row) * 64 + col] = fmaxf((acc[u][0][e] + acc[u][1][e]) + bv, 0.f);
             }
         }
     }
