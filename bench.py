@@ -19,6 +19,7 @@ For N > 1 launch one process per GPU with torch.distributed.run.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -34,13 +35,14 @@ H3_PRODUCTS = 3            # fp16 MFMA products per fp32 product in the h3 conv3
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
 
 
-def _latest_traffic(kern: str):
-    """HBM bytes per conv3 act-forward launch from the newest committed PMC pass
-    (profiles/*_conv3_traffic.json, written by tools/traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 --pmc runs; FETCH_SIZE doubled per
+def _latest_traffic(kern: str, pattern: str = "*_conv3_traffic.json"):
+    """HBM bytes per launch of a dominant kernel from the newest committed PMC pass
+    (profiles/*_conv3_traffic.json for the act forward, *_syrk_traffic.json for the
+    D build; written by tools/traffic.py from separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 --pmc runs of tools/pmc_traffic.sh, FETCH_SIZE doubled per
     MI355X_MICROARCH.md's gfx950 note), for the kernel this run uses."""
     import glob
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_conv3_traffic.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", pattern)), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -312,6 +314,13 @@ def d_build_gram(args, snk, model, dist, rank, world) -> dict:
                                     "traffic": None, "half_mfma_tflops_executed": tf * H3_PRODUCTS,
                                     "mfma_utilization": tf * H3_PRODUCTS / PEAK_BF16_TFLOPS,
                                     "fp32_mfma_peak": PEAK_FP32_TFLOPS}}}
+    tr_file = _latest_traffic("syrk_h3_kernel", "*_syrk_traffic.json") if n == 50000 and world == 1 else None
+    if tr_file:
+        rf = res["d_build"]["roofline"]
+        rf["traffic"] = tr_file["bytes_per_launch"]
+        rf["traffic_source"] = tr_file["source"]
+        rf["traffic_note"] = ("L2-miss bytes (HBM + Infinity Cache) of the Gram launch; its unique operand bytes "
+                              "are the n x Kc fp16 h/l row planes (4 B per entry) + the lower-triangle fp32 G")
     del G, rb
     return res
 
@@ -466,13 +475,21 @@ def main():
         ms = np.zeros(5, np.float64)
         _lib.call("snk_dqn_time_act_layers", tr.model.handle, tr.game.handle, 20, _lib.ptr(ms))
         wo = bs - 5
+        flop_conv1 = 2.0 * n * bs * bs * 16 * 9 * C
         flop_conv3 = 2.0 * n * wo * wo * (36 * 32) * 64
         flop_conv2 = 2.0 * n * bs * bs * 144 * 32
         flop_total = 2.0 * n * (bs * bs * 16 * 9 * C + bs * bs * 32 * 144 + wo * wo * 64 * 1152 + wo * wo * 64 * 64 + 64 * 3)
-        # ms[1] == 0: conv2 runs inside conv3's kernel (conv_h3f_kernel), ms[2] times both
+        # ms[1] == 0: conv1 + conv2 run inside conv3's kernel (conv_h3f_kernel), ms[2] times all
+        # three; ms[0] is then the conv3 weight-max scan (the h3 weight scale)
         fused = ms[1] == 0.0
-        flop_dom = flop_conv3 + (flop_conv2 if fused else 0.0)
-        tf = flop_dom / (ms[2] * 1e-3) / 1e12
+        flop_dom = flop_conv3 + (flop_conv2 + flop_conv1 if fused else 0.0)
+        # the dominant kernel's duration INSIDE the training loop (eager iterations after the
+        # timed region, HIP events around that launch on the library stream); back to back in
+        # isolation (ms[2]) it runs hotter and slower
+        loop_ms = _lib.f64(0)
+        _lib.call("snk_trainer_time_act_kernel", tr.handle, 50, ctypes.byref(loop_ms))
+        dom_ms = loop_ms.value if loop_ms.value > 0 else ms[2]
+        tf = flop_dom / (dom_ms * 1e-3) / 1e12
         # the forward GEMMs run fp32 products as 6 exact bf16 split products on the
         # bf16 MFMA (SNK_CONV=fp32: native f32 MFMA): the fp32-equivalent peak is
         # the bf16 dense peak / 6
@@ -481,22 +498,28 @@ def main():
         h3 = x6 and os.environ.get("SNK_H3S", "1") != "0" and n >= 1024 and 8 <= bs <= 13
         nprod = H3_PRODUCTS if h3 else X6_PRODUCTS
         peak = PEAK_BF16_TFLOPS / nprod if x6 else PEAK_FP32_TFLOPS
-        kname = ("conv_h3f_kernel: conv2 + conv3 in one kernel, fp16 h3 split on v_mfma_f32_16x16x32_f16"
-                 if h3 and fused else
+        kname = ("conv_h3f_kernel: conv1 (fp32 VALU) + conv2 + conv3 (fp16 h3 split on v_mfma_f32_16x16x32_f16) "
+                 "in one kernel" if h3 and fused else
                  "conv_h3s_kernel: fp16 h3 split on v_mfma_f32_16x16x32_f16" if h3 else
                  "bf16x6 split on v_mfma_f32_16x16x32_bf16" if x6 else "v_mfma_f32_32x32x2_f32")
         out["roofline"] = {"bound": "mfma",
-                           "kernel": ("conv2 + conv3 implicit GEMMs" if fused else "conv3 implicit GEMM") +
+                           "kernel": ("conv1 + conv2 + conv3" if fused else "conv3 implicit GEMM") +
                                      ", act forward (" + kname + ")",
                            "achieved": tf, "peak": peak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / peak,
-                           "traffic": None, "avg_launch_ms": ms[2], "flop_per_launch": flop_dom,
+                           "traffic": None, "avg_launch_ms": dom_ms,
+                           "avg_launch_ms_how": "HIP events around the launch in 50 eager training iterations"
+                                                if loop_ms.value > 0 else "HIP events, back-to-back launches",
+                           "isolated_back_to_back_ms": ms[2], "flop_per_launch": flop_dom,
+                           "flop_note": "conv1's 2*n*bs^2*16*9C FLOP (1 % of the launch) run on the VALU and are "
+                                        "counted against the MFMA peak" if fused else None,
                            "half_mfma_tflops_executed": tf * nprod if x6 else None,
                            "fp32_mfma_peak": PEAK_FP32_TFLOPS}
         tr_file = _latest_traffic("conv_h3f_kernel" if fused else "conv_h3s_kernel" if h3 else "conv_x6")
         if tr_file:
             out["roofline"]["traffic"] = tr_file["bytes_per_launch"]
             out["roofline"]["traffic_source"] = tr_file["source"]
-        out["act_forward_ms"] = {"conv1": ms[0], "conv2": ms[1], ("conv2+conv3" if fused else "conv3"): ms[2],
+        out["act_forward_ms"] = {("wmax_scan" if fused else "conv1"): ms[0], "conv2": ms[1],
+                                 ("conv1+conv2+conv3" if fused else "conv3"): ms[2],
                                  "dense1": ms[3], "head": ms[4],
                                  "total": float(ms.sum()),
                                  "tflops_total": flop_total / (ms.sum() * 1e-3) / 1e12}

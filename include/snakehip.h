@@ -170,8 +170,9 @@ int snk_dqn_forward_env(snk_dqn m, int32_t which, snk_env env, float *q_dev);
 int snk_dqn_act(snk_dqn m, snk_env env, float epsilon, uint64_t seed, uint8_t *act_dev);
 /* measurement: average ms per launch of each stage of the epsilon_greedy
  * forward over env's batch, ms_out[5] = conv1, conv2, conv3, dense1, head
- * (HIP events on the library stream); when the forward fuses conv2 into
- * conv3 (conv_h3f_kernel) ms_out[1] = 0 and ms_out[2] is the fused kernel */
+ * (HIP events on the library stream); when the forward fuses conv1 and conv2
+ * into conv3 (conv_h3f_kernel) ms_out[0] is the conv3 weight-max scan,
+ * ms_out[1] = 0 and ms_out[2] is the fused kernel */
 int snk_dqn_time_act_layers(snk_dqn m, snk_env env, int32_t reps, double *ms_out);
 /* measurement: average ms of the fused step(+store) kernel over reps real steps */
 int snk_env_time_step(snk_env env, snk_replay rb_or_null, const uint8_t *act_dev, int32_t reps, double *ms_out);
@@ -230,6 +231,11 @@ int snk_trainer_stats(snk_trainer t, snk_trainer_stats_t *out);
 /* tr.losses: loss of update u at host[u % loss_log_capacity] */
 int snk_trainer_losses(snk_trainer t, double *host, int64_t n);
 int snk_trainer_act_ptr(snk_trainer t, uint8_t **act_dev);
+/* measurement: `iters` real (learning) trainer iterations, eager, with HIP events
+ * around the act forward's fused conv kernel (conv_h3f_kernel) on the library
+ * stream: *ms_out = its mean duration inside the training loop (0 when this
+ * trainer's act forward does not run it) */
+int snk_trainer_time_act_kernel(snk_trainer t, int32_t iters, double *ms_out);
 
 /* ---------------------------------------------------------------- multi-GPU
  * Data-parallel replicas (new: the reference is single-process). One process

@@ -113,6 +113,9 @@ struct FwdNet {
 };
 // conv1 .. Dense1 of two independent nets over S samples each, both in every launch (grid z/y = net)
 void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s);
+// measurement hook: when armed (a, b non-null), the act forward's conv_h3f_kernel launch is
+// bracketed by hipEventRecord(a) / hipEventRecord(b) on its stream (eager launches only)
+void h3f_timing_hook(hipEvent_t a, hipEvent_t b);
 // the update's two forwards (net[0] = t_net on s', net[1] = q_net on s, which keeps the
 // training activations) up to the Dense1 slabs: conv1-conv3 in one launch
 // (snk_upd_fwd.hpp) when the geometry allows, else the layer-by-layer path

@@ -338,6 +338,45 @@ extern "C" int snk_trainer_losses(snk_trainer h, double *host, int64_t n) {
     });
 }
 
+extern "C" int snk_trainer_time_act_kernel(snk_trainer h, int32_t iters, double *ms_out) {
+    return guard([&] {
+        SNK_CHECK(h && iters > 0 && ms_out, SNK_ERR_INVALID, "bad time_act_kernel arguments");
+        const int upi = h->cfg.updates_per_iter;
+        if (upi > 0) trainer_check_replay(h);
+        trainer_refresh(h);
+        hipStream_t s = stream();
+        hipEvent_t a, b;
+        SNK_HIP(hipEventCreate(&a));
+        SNK_HIP(hipEventCreate(&b));
+        double total = 0.0;
+        int timed = 0;
+        try {
+            for (int i = 0; i < iters; ++i) {
+                SNK_HIP(hipEventRecord(a, s));   // completes at once if the kernel is absent
+                SNK_HIP(hipEventRecord(b, s));
+                h3f_timing_hook(a, b);
+                trainer_iteration(h, true, upi, s);
+                h3f_timing_hook(nullptr, nullptr);
+                SNK_HIP(hipEventSynchronize(b));
+                float ms = 0.0f;
+                SNK_HIP(hipEventElapsedTime(&ms, a, b));
+                if (ms > 0.0f) {
+                    total += ms;
+                    ++timed;
+                }
+            }
+        } catch (...) {
+            h3f_timing_hook(nullptr, nullptr);
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+            throw;
+        }
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        *ms_out = timed ? total / timed : 0.0;
+    });
+}
+
 extern "C" int snk_trainer_act_ptr(snk_trainer h, uint8_t **act_dev) {
     return guard([&] {
         SNK_CHECK(h && act_dev, SNK_ERR_INVALID, "NULL argument");
