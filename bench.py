@@ -527,7 +527,6 @@ def main():
         act = snk.DeviceArray(n, np.uint8)
         snk.synth_actions_dev(tr.game, 99, act)
         sms = _lib.f64(0)
-        import ctypes
         _lib.call("snk_env_time_step", tr.game.handle, tr.buffer.handle, act.ptr, 50, ctypes.byref(sms))
         step_bytes = (C + 4) * bs * bs + 57
         gbs = n * step_bytes / (sms.value * 1e-3) / 1e9
