@@ -60,7 +60,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     constexpr int hin = HIN, ho = HIN - KS + 1, ho2 = ho * ho, hin2 = hin * hin;
     constexpr int XW = ho + 8, PL = (hin * XW + 3) & ~3, GG = 2 * PL, XS = 4 * GG + 4;
     constexpr int BP = HIN + 2, NPB = BP * BP, XR = 24, BR = 40;
-    constexpr int A1_H = NSG * 2 * NPB * XR, B2_H = 5 * 2 * 32 * BR;
+    constexpr int A1_H = NSG * 2 * NPB * XR;   // the B2 image (5 x 2 x 32 x BR halves) follows
     constexpr int R2 = NSG * hin2, T2 = (R2 + 15) / 16, U2 = (T2 + 7) / 8;
     constexpr int NW4 = 9 * 32 * 16 / 4, LW = (NW4 + 511) / 512, LA = (NSG * hin2 * 4 + 511) / 512;
     static_assert(XR % 8 == 0 && BR % 8 == 0, "16-byte pieces");

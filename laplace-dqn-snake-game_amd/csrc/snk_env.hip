@@ -180,10 +180,7 @@ __global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_
 #pragma clang loop unroll(full)
     for (int k = 0; k < NPT; ++k) {
         const int idx = tid + k * ENV_NT;
-        if (idx < ne * NCH) {
-            const int el = idx / NCH, c = idx - el * NCH;
-            vcur[k] = *reinterpret_cast<const i32x4 *>(fcur + idx * 16);
-        }
+        if (idx < ne * NCH) vcur[k] = *reinterpret_cast<const i32x4 *>(fcur + idx * 16);
     }
 #pragma clang loop unroll(full)
     for (int k = 0; k < NPT; ++k) {
