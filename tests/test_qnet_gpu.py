@@ -82,8 +82,12 @@ def _random_replay(snk, bs, C, n=96, T=30, seed=3):
     return g, rb
 
 
-@pytest.mark.parametrize("bs,C", [(12, 2), (10, 1)])
+@pytest.mark.parametrize("bs,C", [(12, 2), (10, 1), (16, 2), (13, 1)])
 def test_loss_and_grad_vs_oracle(snk, bs, C):
+    """One DQN loss + gradient (utils.jl:442-466) on a replay batch: the fused update
+    forward (upd_fwd_kernel, instantiated for board sides 8/10/12/13/16) and the
+    backward. Loss within 1e-5 relative, gradient normwise 1e-5 plus an elementwise
+    bound; the stack_exp float-tensor path is bit-identical to the slot path."""
     g, rb = _random_replay(snk, bs, C)
     m = snk.DQNModel(bs, 3, n_frames=C, seed=21)
     rng = np.random.default_rng(0)
