@@ -17,9 +17,9 @@
 //            accumulation), offsets paired into 5 k-steps of 32; bias + relu
 //            -> a2 (global, training net) and its split into LDS;
 //   phase 3  conv3 (6x6, 32 -> 64, this workgroup's 32 channels): A from the
-//            LDS image, B (the weight planes the update keeps current) streamed
-//            from L2 into registers eight offsets ahead, each wave only its own 16
-//            columns; bias + relu -> a3.
+//            LDS image, B (the weight planes the update keeps current) staged
+//            through LDS three offsets at a time (double-buffered, loaded two stages
+//            ahead); bias + relu -> a3.
 // conv1 and conv2 run in both halves of a sample (they are ~20 % of the work);
 // only half 0 writes a1, a2 and x0. Dense1 and the heads follow as before.
 #pragma once
@@ -255,22 +255,44 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     UPD_CLK(3);
     // ---- phase 3: conv3 on x6 MFMA: rows = the WO^2 output positions, 32 columns -------
     // wave w owns column tile w & 1 (16 of the workgroup's 32 columns) and row tiles
-    // (w >> 1) + 4u: each wave streams only its own 16 columns of B (3 KB per offset) from
-    // L2 straight into registers, D offsets in flight; even and odd offsets accumulate
-    // separately (two independent MFMA chains), summed at the end
+    // (w >> 1) + 4u. The workgroup's B (its 32 columns, 6 KB per offset) is staged once
+    // per 3-offset stage into the LDS the conv1/conv2 images no longer need (double-buffered,
+    // one barrier per stage): read straight from L2 by every wave it cost four times the L1
+    // traffic. Even and odd offsets accumulate separately (two MFMA chains).
     {
         constexpr int NTW = (T3 + 3) / 4;   // row tiles per wave
-        constexpr int D = 8;
+        // offsets per stage; halves per LDS B row (16-byte piece p of row c stored at p ^ ((c >> 2) & 3):
+        // the fragment reads of 16 rows hit distinct bank quads)
+        constexpr int KB = 3, NSTG = 36 / KB, LDB = 32;
+        constexpr int SPL = KB * 3 * 32 * LDB;            // halves per stage buffer
+        static_assert(2 * SPL * 2 <= NB * UPDF_A1S * 2 + 9 * 3 * 32 * 16 * 2, "B stages fit the dead A1 + B2 images");
+        constexpr int NQ = KB * 3 * 32 * 4;               // 16-byte pieces per stage (4 per 32-ci row)
+        constexpr int QPT = (NQ + UPDF_NT - 1) / UPDF_NT;
+        uint16_t *B3 = A1;   // [2][KB kk][3 pl][32 cols][LDB]
         const int ct = wave & 1, rt0 = wave >> 1;
         const int col = half * 32 + ct * 16 + r;
         const float *b3 = n.th + L.off_b3;
-        // B fragment of column col, k = 8g..8g+7 of offset kk, plane pl:
-        // planes [kk][3][64 co][32 ci] -> 16 contiguous bytes
-        const uint16_t *wb3 = n.wtb + 3 * L.off_t3 + col * 32 + 8 * g;
-        auto bload = [&](int kk, u32x4 (&b)[3]) {
+        const uint16_t *wsrc = n.wtb + 3 * L.off_t3 + (int64_t)half * 32 * 32;   // planes [kk][3][64 co][32 ci]
+        // stage s is loaded into registers two stages ahead (sa / sb alternate), stored into
+        // LDS buffer s & 1 one stage ahead
+        u32x4 sa[QPT], sb[QPT];
+        auto sload = [&](int stg, u32x4 (&st)[QPT]) {
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-                b[pl] = *reinterpret_cast<const u32x4 *>(wb3 + (int64_t)(kk * 3 + pl) * 64 * 32);
+            for (int u = 0; u < QPT; ++u) {
+                const int q = min(tid + u * UPDF_NT, NQ - 1);
+                const int row = q >> 2, piece = q & 3;   // row = (kl * 3 + pl) * 32 + c
+                const int kl = row / 96, pl = (row / 32) % 3, c = row & 31;
+                st[u] = *reinterpret_cast<const u32x4 *>(wsrc + ((int64_t)((stg * KB + kl) * 3 + pl) * 64 + c) * 32 +
+                                                         piece * 8);
+            }
+        };
+        auto sstore = [&](int buf, const u32x4 (&st)[QPT]) {
+#pragma unroll
+            for (int u = 0; u < QPT; ++u) {
+                const int q = tid + u * UPDF_NT;
+                if (q < NQ)
+                    *reinterpret_cast<u32x4 *>(B3 + buf * SPL + (q >> 2) * LDB + ((q & 3) ^ ((q >> 4) & 3)) * 8) = st[u];
+            }
         };
         int qb[NTW];
         f32x4v acc[NTW][2];
@@ -281,23 +303,41 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
             qb[u] = qi + qj * HIN;
             acc[u][0] = acc[u][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
         }
-        u32x4 bq[D][3];
+        auto compute = [&](int stg) {
+            const uint16_t *bb = B3 + (stg & 1) * SPL + (ct * 16 + r) * LDB + 8 * (g ^ ((r >> 2) & 3));
 #pragma unroll
-        for (int d = 0; d < D; ++d) bload(d, bq[d]);
-#pragma clang loop unroll(full)
-        for (int kk = 0; kk < 36; ++kk) {
-            const int du = kk % 6, dv = kk / 6;
+            for (int kl = 0; kl < KB; ++kl) {
+                const int kk = stg * KB + kl, du = kk % 6, dv = kk / 6;
+                u32x4 b[3];
 #pragma unroll
-            for (int u = 0; u < NTW; ++u) {
-                if (rt0 + 4 * u < T3) {   // wave-uniform
-                    const uint16_t *pa = A2 + (qb[u] + du + dv * HIN) * UPDF_A2S + 8 * g;
-                    u32x4 a[3];
+                for (int pl = 0; pl < 3; ++pl) b[pl] = *reinterpret_cast<const u32x4 *>(bb + (kl * 3 + pl) * 32 * LDB);
 #pragma unroll
-                    for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const u32x4 *>(pa + pl * 32);
-                    acc[u][kk & 1] = mfma_x6(a, bq[kk % D], acc[u][kk & 1]);
+                for (int u = 0; u < NTW; ++u) {
+                    if (rt0 + 4 * u < T3) {   // wave-uniform
+                        const uint16_t *pa = A2 + (qb[u] + du + dv * HIN) * UPDF_A2S + 8 * g;
+                        u32x4 a[3];
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const u32x4 *>(pa + pl * 32);
+                        acc[u][kl & 1] = mfma_x6(a, b, acc[u][kl & 1]);
+                    }
                 }
             }
-            if (kk + D < 36) bload(kk + D, bq[kk % D]);
+        };
+        static_assert(NSTG % 2 == 0, "stages come in pairs");
+        sload(0, sa);
+        sload(1, sb);
+        sstore(0, sa);
+        sload(2, sa);
+        __syncthreads();
+        for (int stg = 0; stg < NSTG; stg += 2) {
+            compute(stg);                          // buffer 0
+            sstore(1, sb);                         // stage stg + 1 (buffer 1 last read at stg - 1)
+            __syncthreads();
+            if (stg + 3 < NSTG) sload(stg + 3, sb);
+            compute(stg + 1);                      // buffer 1
+            if (stg + 2 < NSTG) sstore(0, sa);     // stage stg + 2 (buffer 0 last read at stg)
+            __syncthreads();
+            if (stg + 4 < NSTG) sload(stg + 4, sa);
         }
         UPD_CLK(4);
         const float bv = b3[col];
