@@ -125,6 +125,16 @@ def cpu_baseline(args) -> dict:
                                    f"work) not included"}
 
 
+def _deep_traffic(d: int, n: int, bs: int) -> dict:
+    """PMC bytes per launch of the configs[2] dominant layer (the 6x6 64->64 conv,
+    deep_conv_kernel<64, 64, 6, ...>) from profiles/*_deep_traffic.json (tools/pmc_traffic.sh
+    <tag> deep + tools/traffic.py), when this run's dominant layer is that one at 65,536 x 20x20."""
+    if d != 3 or n != 65536 or bs != 20:
+        return {}
+    t = _latest_traffic("deep_conv_kernel<64, 64, 6", "*_deep_traffic.json")
+    return {"traffic": t["bytes_per_launch"], "traffic_source": t["source"]} if t else {}
+
+
 def configs2(args, snk, graph) -> dict:
     """BASELINE.json configs[2]: 65,536 lockstep 20x20 envs with the deeper
     bf16 conv Q-net (snk_dqn_create_deep), one trainer
@@ -167,9 +177,10 @@ def configs2(args, snk, graph) -> dict:
             "act_forward_ms": {nm: float(t) for nm, t in zip(names, ms)},
             "act_forward_total_ms": float(ms.sum()),
             "act_forward_tflops": fwd_flop / (ms.sum() * 1e-3) / 1e12,
-            "roofline": {"bound": "mfma", "kernel": names[d], "achieved": tf, "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s (bf16)", "frac": tf / PEAK_BF16_TFLOPS, "avg_launch_ms": float(ms[d]),
-                         "flop_per_launch": flop[d], "traffic": None},
+            "roofline": dict({"bound": "mfma", "kernel": names[d], "achieved": tf, "peak": PEAK_BF16_TFLOPS,
+                              "unit": "TFLOP/s (bf16)", "frac": tf / PEAK_BF16_TFLOPS, "avg_launch_ms": float(ms[d]),
+                              "flop_per_launch": flop[d], "traffic": None},
+                             **_deep_traffic(d, n, bs)),
             "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"]}}
 
 

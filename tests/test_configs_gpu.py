@@ -63,8 +63,8 @@ def test_configs1_env_4096_store_bitexact(snk):
 
 
 def test_configs1_act_forward_4096_vs_oracle(snk):
-    """configs[1]: Q of all 4096 env states in one act forward (conv1, fused
-    conv2+conv3 conv_h3f_kernel, Dense1, head); every 4th state (1024, every
+    """configs[1]: Q of all 4096 env states in one act forward (conv1 + conv2 +
+    conv3 fused in conv_h3f_kernel, Dense1, head); every 4th state (1024, every
     workgroup slot position) within |q - q_ref| <= 1e-5 max(1, |q_ref|) of
     the fp64 oracle, and epsilon_greedy at epsilon 0 picks the oracle's first
     argmax wherever the top-2 margin exceeds 1e-4."""
