@@ -39,6 +39,19 @@ struct H3FArgs {
     float *out;          // a3 [S][ho^2][64]
 };
 
+// Profiling builds only (make clocks): per-workgroup phase timestamps, read back by
+// snk_h3f_debug_clocks (slots: start, conv1, scales + splits, conv2, conv3 image + B
+// stages, conv3 offsets, end)
+#ifdef SNK_ENV_CLOCKS
+__device__ uint64_t *g_h3f_clk;
+#define H3F_CLK(slot)                                                                                 \
+    do {                                                                                              \
+        if (threadIdx.x == 0 && g_h3f_clk) g_h3f_clk[(int64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define H3F_CLK(slot) do { } while (0)
+#endif
+
 template <int HIN, int NBUF = 4>
 constexpr int h3f_lds_bytes() {
     constexpr int ho = HIN - 5, XW = ho + 8, PL = (HIN * XW + 3) & ~3, XS = 4 * 2 * PL + 4;
@@ -75,6 +88,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     const int r = lane & 15, g = lane >> 4;
     const int s0 = blockIdx.x * NSG;
     const int ns = min(NSG, S - s0);
+    H3F_CLK(0);
 
     // conv3 B register sets (as conv_h3s_kernel)
     const f32x4 *__restrict__ wsrc = reinterpret_cast<const f32x4 *>(a.w3);
@@ -168,6 +182,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             av[u] = acc;
         }
     }
+    H3F_CLK(1);
     float wm3 = 0.0f;
     for (int i = tid; i < a.nwmax; i += 512) wm3 = fmaxf(wm3, a.wmax[i]);
     float mw2 = 0.0f, ms[NSG] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -239,6 +254,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         }
     }
     __syncthreads();
+    H3F_CLK(2);
 
     // ---- conv2, transposed: C^T[co][row] = sum_k W[co][k] * A[row][k] with the weight
     // fragments as the MFMA's A operand and the activation fragments as its B (the
@@ -309,6 +325,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         for (int q = 0; q < NSG; ++q) red[wave][q] = m2[q];
     }
     __syncthreads();   // also: every conv2 fragment read is done (the A image overlays them)
+    H3F_CLK(3);
     int ea[NSG];
 #pragma unroll
     for (int q = 0; q < NSG; ++q) {
@@ -423,11 +440,13 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             b_store(2, 0);
         }
         __syncthreads();
+        H3F_CLK(4);
         static_assert(NKK % 2 == 0, "offsets come in pairs");
         for (int kk = 0; kk < NKK; kk += 2) {
             step(kk, f0, f1, 0);
             step(kk + 1, f1, f0, 1);
         }
+        H3F_CLK(5);
         // output through LDS as conv_h3s_kernel
         constexpr int CS = 80;
         static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN, NBUF>() - NBUF * NB * 16, "output staging fits");
@@ -452,6 +471,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         f32x4 *o4 = reinterpret_cast<f32x4 *>(a.out + (int64_t)s0 * ho2 * CN);
         const f32x4 *c4 = reinterpret_cast<const f32x4 *>(Cs);
         for (int q = tid; q < n4o; q += 512) o4[q] = c4[(q >> 4) * (CS / 4) + (q & 15)];
+        H3F_CLK(6);
     };
     if (nt == 4) run(std::integral_constant<int, 4>{});
     else if (nt == 3) run(std::integral_constant<int, 3>{});
