@@ -105,6 +105,9 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     };
     b_load(0, 0);
     b_load(1, 1);
+    // conv3 weight-max partials: loaded here, reduced after conv1 (their latency hides
+    // behind the board loads instead of following conv1)
+    const float wmx = tid < a.nwmax ? a.wmax[tid] : 0.0f;
 
     // conv2 bias of this lane's output channels (16 ct + 4 g + e), early
     float b2v[2][4];
@@ -183,8 +186,8 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         }
     }
     H3F_CLK(1);
-    float wm3 = 0.0f;
-    for (int i = tid; i < a.nwmax; i += 512) wm3 = fmaxf(wm3, a.wmax[i]);
+    float wm3 = wmx;
+    for (int i = tid + 512; i < a.nwmax; i += 512) wm3 = fmaxf(wm3, a.wmax[i]);
     float mw2 = 0.0f, ms[NSG] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int u = 0; u < LW; ++u) {
@@ -281,22 +284,35 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             wl[ct] = as_h(*reinterpret_cast<const u32x4 *>(pb + 32 * BR));
         }
         const int kk = min(2 * p + (g >> 1), 8), du = kk % 3, dv = kk / 3;
+        // every wave has tiles u < UF: their fragments are all read before any MFMA of
+        // the pair (no wave-uniform branch between a read and its use, so the reads go
+        // out together and overlap the previous pair's MFMAs); tile UF, which only
+        // waves < T2 - 8 UF have, runs under its branch
+        constexpr int UF = T2 / 8;
+        f16x8 fah[U2], fal[U2];
+        auto frag = [&](int u) {
+            const uint16_t *pa = A1 + ((rsl[u] * 2) * NPB + rpos[u] + du + dv * BP) * XR + 8 * (g & 1);
+            fah[u] = as_h(*reinterpret_cast<const u32x4 *>(pa));
+            fal[u] = as_h(*reinterpret_cast<const u32x4 *>(pa + NPB * XR));
+        };
+        auto tile = [&](int u) {
 #pragma unroll
-        for (int u = 0; u < U2; ++u) {
-            if (wave + 8 * u < T2) {
-                const uint16_t *pa = A1 + ((rsl[u] * 2) * NPB + rpos[u] + du + dv * BP) * XR + 8 * (g & 1);
-                const f16x8 ah = as_h(*reinterpret_cast<const u32x4 *>(pa));
-                const f16x8 al = as_h(*reinterpret_cast<const u32x4 *>(pa + NPB * XR));
-#pragma unroll
-                for (int ct = 0; ct < 2; ++ct) {
-                    f32x4v c = acc2[u][ct];
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ct], al, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[ct], ah, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ct], ah, c, 0, 0, 0);
-                    acc2[u][ct] = c;
-                }
+            for (int ct = 0; ct < 2; ++ct) {
+                f32x4v c = acc2[u][ct];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ct], fal[u], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[ct], fah[u], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[ct], fah[u], c, 0, 0, 0);
+                acc2[u][ct] = c;
             }
+        };
+#pragma unroll
+        for (int u = 0; u < UF; ++u) frag(u);
+        if (U2 > UF && wave + 8 * UF < T2) {
+            frag(U2 - 1);
+            tile(U2 - 1);
         }
+#pragma unroll
+        for (int u = 0; u < UF; ++u) tile(u);
     }
     // acc2[u][ct][e]: channel co = 16 ct + 4 g + e of row (wave + 8u) * 16 + r.
     // bias + relu in place; per-sample max (rows of absent samples excluded)
