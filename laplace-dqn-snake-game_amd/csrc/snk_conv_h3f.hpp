@@ -56,7 +56,7 @@ template <int HIN, int NBUF = 4>
 constexpr int h3f_lds_bytes() {
     constexpr int ho = HIN - 5, XW = ho + 8, PL = (HIN * XW + 3) & ~3, XS = 4 * 2 * PL + 4;
     constexpr int BP = HIN + 2;
-    constexpr int c2 = (4 * 2 * BP * BP * 24 + 5 * 2 * 32 * 40) * 2;   // conv2 staging (halves)
+    constexpr int c2 = (4 * 2 * BP * BP * 16 + 5 * 2 * 32 * 48) * 2;   // conv2 staging (halves)
     constexpr int c3 = 4 * XS * 16;                                     // conv3 A image
     constexpr int cs = 4 * ho * ho * 80 * 4;                            // output staging
     constexpr int m = c2 > c3 ? (c2 > cs ? c2 : cs) : (c3 > cs ? c3 : cs);
@@ -72,7 +72,9 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     constexpr int NKK = KS * KS;
     constexpr int hin = HIN, ho = HIN - KS + 1, ho2 = ho * ho, hin2 = hin * hin;
     constexpr int XW = ho + 8, PL = (hin * XW + 3) & ~3, GG = 2 * PL, XS = 4 * GG + 4;
-    constexpr int BP = HIN + 2, NPB = BP * BP, XR = 24, BR = 40;
+    // A1 rows of 16 halves and B2 rows of 48: 2 and 6 16-byte units per row, for which
+    // the ds_read_b128 lane groups of the conv2 fragment reads hit 16 distinct bank quads
+    constexpr int BP = HIN + 2, NPB = BP * BP, XR = 16, BR = 48, XP = XR / 8;
     constexpr int A1_H = NSG * 2 * NPB * XR;   // the B2 image (5 x 2 x 32 x BR halves) follows
     constexpr int R2 = NSG * hin2, T2 = (R2 + 15) / 16, U2 = (T2 + 7) / 8;
     constexpr int NW4 = 9 * 32 * 16 / 4, LW = (NW4 + 511) / 512, LA = (NSG * hin2 * 4 + 511) / 512;
@@ -120,8 +122,8 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     // (kk = 9: k 16..31 of pair 4); the rest is overwritten below
     {
         constexpr int NBD = 4 * (BP - 1);   // border positions per plane
-        for (int q = tid; q < NSG * 2 * NBD * 3; q += 512) {
-            const int pc = q / (NBD * 3), rem = q - pc * NBD * 3, bpos = rem / 3, piece = rem - bpos * 3;
+        for (int q = tid; q < NSG * 2 * NBD * XP; q += 512) {
+            const int pc = q / (NBD * XP), rem = q - pc * NBD * XP, bpos = rem / XP, piece = rem - bpos * XP;
             const int side = bpos / (BP - 1), t = bpos - side * (BP - 1);
             const int pb = side == 0 ? t : side == 1 ? (BP - 1) + t * BP : side == 2 ? (BP * BP - 1) - t
                                                                                      : (BP - 1 - t) * BP;
