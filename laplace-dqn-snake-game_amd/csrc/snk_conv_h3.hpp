@@ -63,10 +63,25 @@ __device__ __forceinline__ void h3_split4(const f32x4 &x, int e, u32x2 &h, u32x2
     }
 }
 
+// max over the wave, returned to every lane: DPP within each row of 16 lanes (xor 1,
+// xor 2, half mirror, mirror), then the four row maxima by v_readlane. max is exact and
+// order-free, so the result equals any other reduction order's (no LDS round trips,
+// which the ds_bpermute form of __shfl_xor costs six of, each dependent on the last)
+template <int CTRL>
+__device__ __forceinline__ float dpp_max(float v) {
+    const int o = __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false);
+    return fmaxf(v, __builtin_bit_cast(float, o));
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
+    v = dpp_max<0xB1>(v);    // quad_perm [1,0,3,2]
+    v = dpp_max<0x4E>(v);    // quad_perm [2,3,0,1]
+    v = dpp_max<0x141>(v);   // row_half_mirror
+    v = dpp_max<0x140>(v);   // row_mirror: every lane holds its row's max
+    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+    const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+    const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+    return fmaxf(fmaxf(a, b), fmaxf(c, d));
 }
 
 // partial max |w| of w[0, n): block b (256 threads) covers a grid-stride share; part[b]
