@@ -154,16 +154,38 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         for (int q = 0; q < 9 * C; ++q) w1r[q] = reinterpret_cast<const f32x4 *>(a.w1)[q * 4 + cq];
         b1r = reinterpret_cast<const f32x4 *>(a.b1)[cq];
         __syncthreads();
-        for (int q = tid; q < NSG * C * NPB; q += 512) {
-            const int sc = q / NPB, b = q - sc * NPB;
+        // every cell load of the thread goes out before the first is used (a loop of
+        // load-then-store waited out one round trip per cell), through global (not flat)
+        // pointers: the plane pointers come from LDS as generic ones
+        typedef const __attribute__((address_space(1))) int8_t gi8;
+        constexpr int NX = NSG * C * NPB, LB = (NX + 511) / 512;
+        const bool fl = a.src.fbase != nullptr;
+        int bv[LB], bsc[LB], bcell[LB];
+        bool bin[LB];
+#pragma unroll
+        for (int u = 0; u < LB; ++u) {
+            const int q = u * 512 + tid;
+            const int sc = min(q / NPB, NSG * C - 1), b = q - sc * NPB;
             const int bj = b / BP, bi = b - bj * BP;
-            float v = 0.0f;
-            if (sc / C < ns && bi >= 1 && bi <= hin && bj >= 1 && bj <= hin) {
-                const int cell = (bi - 1) + (bj - 1) * hin;
-                const int8_t *pl = pbase[sc];
-                v = pl ? (float)pl[cell] : a.src.fbase[((int64_t)(s0 + sc / C) * C + sc % C) * hin2 + cell];
-            }
-            xin[q] = v;
+            bsc[u] = sc;
+            bcell[u] = (bi - 1) + (bj - 1) * hin;
+            bin[u] = q < NX && sc / C < ns && bi >= 1 && bi <= hin && bj >= 1 && bj <= hin;
+        }
+        if (fl) {
+#pragma unroll
+            for (int u = 0; u < LB; ++u)
+                bv[u] = bin[u] ? __float_as_int(a.src.fbase[((int64_t)(s0 + bsc[u] / C) * C + bsc[u] % C) * hin2 + bcell[u]]) : 0;
+        } else {
+            gi8 *pl[LB];
+#pragma unroll
+            for (int u = 0; u < LB; ++u) pl[u] = (gi8 *)pbase[bsc[u]];
+#pragma unroll
+            for (int u = 0; u < LB; ++u) bv[u] = bin[u] ? (int)pl[u][bcell[u]] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < LB; ++u) {
+            const int q = u * 512 + tid;
+            if (q < NX) xin[q] = fl ? __int_as_float(bv[u]) : (float)bv[u];
         }
         __syncthreads();
 #pragma unroll
