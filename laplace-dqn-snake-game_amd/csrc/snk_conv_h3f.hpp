@@ -193,20 +193,22 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             const int e = min(u * 512 + tid, na4 - 1);
             const int sr = e / (hin2 * 4), pos = (e - sr * hin2 * 4) >> 2;
             const int j = pos / hin, i = pos - j * hin;
-            f32x4 acc = b1r;
+            // channel pairs on v_pk_fma_f32 (two fp32 FMAs per lane and instruction; each
+            // channel's FMA chain and rounding are the scalar form's)
+            f32x2 acc01{b1r[0], b1r[1]}, acc23{b1r[2], b1r[3]};
 #pragma unroll
             for (int kk = 0; kk < 9; ++kk) {
                 const int du = kk % 3, dv = kk / 3;
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
                     const float x = xin[(sr * C + c) * NPB + (i + du) + (j + dv) * BP];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[q] = __builtin_fmaf(x, w1r[kk * C + c][q], acc[q]);
+                    const f32x2 xx{x, x};
+                    const f32x4 w = w1r[kk * C + c];
+                    acc01 = __builtin_elementwise_fma(xx, f32x2{w[0], w[1]}, acc01);
+                    acc23 = __builtin_elementwise_fma(xx, f32x2{w[2], w[3]}, acc23);
                 }
             }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[q] = fmaxf(acc[q], 0.f);
-            av[u] = acc;
+            av[u] = f32x4{fmaxf(acc01[0], 0.f), fmaxf(acc01[1], 0.f), fmaxf(acc23[0], 0.f), fmaxf(acc23[1], 0.f)};
         }
     }
     H3F_CLK(1);
