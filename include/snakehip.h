@@ -144,8 +144,10 @@ int snk_dqn_create(snk_dqn *out, int32_t board_size, int32_t n_frames, float lr,
  *   Conv(6,6,64=>64,relu) flatten Dense((bs-5)^2*64=>64,relu) Dense(64=>3)
  * with conv / Dense1 weights and every conv activation in bf16, fp32 sums,
  * fp32 master weights, RMSProp and head. board_size 10, 12 or 20.
- * The handle answers every DQNModel and trainer entry point below except the
- * Jacobian / Laplace ones and snk_dqn_time_act_layers / snk_dqn_last_q. */
+ * The handle answers every DQNModel and trainer entry point below, and
+ * snk_laplace_snapshot / snk_laplace_sample_params; snk_jacobian,
+ * snk_jacobian_gram(_shard), snk_laplace_sampling, snk_dqn_time_act_layers and
+ * snk_dqn_last_q refuse it (SNK_ERR_INVALID). */
 int snk_dqn_create_deep(snk_dqn *out, int32_t board_size, int32_t n_frames, float lr, float rho, float eps,
                         uint64_t init_seed);
 /* measurement: average ms per launch of each layer of the deep net's
@@ -178,6 +180,11 @@ int snk_dqn_time_act_layers(snk_dqn m, snk_env env, int32_t reps, double *ms_out
 int snk_env_time_step(snk_env env, snk_replay rb_or_null, const uint8_t *act_dev, int32_t reps, double *ms_out);
 /* Q of the last forward_env/act call, host [n][3] */
 int snk_dqn_last_q(snk_dqn m, float *q_host, int64_t n);
+/* test hook: the relu outputs of q_net in the last training forward (loss_grad,
+ * update, or the trainer's last update): layer 0 a1 [B][bs*bs][16], 1 a2
+ * [B][bs*bs][32], 2 a3 [B][(bs-5)^2][64], 3 h1 [B][64]; position = i + j*side
+ * for board[i, j]. n floats from the start. */
+int snk_dqn_train_activations(snk_dqn m, int32_t layer, float *host, int64_t n);
 /* utils.jl:448-464: TD target on t_net (Float64, suicidal mask -> -100),
  * Huber loss (delta 1, mean) and its gradient into SNK_NET_GRAD, for the
  * replay slots idx_dev[B]. loss_host may be NULL (no synchronisation). */
@@ -196,7 +203,12 @@ int snk_dqn_update(snk_dqn m, snk_replay rb, const int64_t *idx_dev, int64_t B, 
 /* ---------------------------------------------------------------- trainer
  * The batched train! loop (utils.jl:420-494) over a batch of envs. */
 typedef struct snk_trainer_s *snk_trainer;
+/* ABI guard: the caller sets struct_size = sizeof(the struct) as its first
+ * field; the library refuses (SNK_ERR_INVALID) any other size, so a host
+ * binding whose struct layout drifts from this header fails loudly instead of
+ * being read past its end. snk_abi_sizes reports the sizes it expects. */
 typedef struct {
+    int32_t struct_size;        /* = sizeof(snk_trainer_cfg_t) = 64 */
     float epsilon;              /* structs.jl:165 epsilon = 1.0 */
     float epsilon_end;          /* 0.05 */
     float decay;                /* 1e-6, subtracted per update (utils.jl:480) */
@@ -208,6 +220,7 @@ typedef struct {
     int32_t graph_unroll;       /* lockstep iterations per captured hipGraph (0 = 8) */
 } snk_trainer_cfg_t;
 typedef struct {
+    int32_t struct_size;        /* = sizeof(snk_trainer_stats_t) = 80, set by the caller */
     int64_t episodes, score_sum, updates, nb, env_steps;
     double reward_sum, last_loss;
     float reward_max;
@@ -215,6 +228,9 @@ typedef struct {
     float epsilon;
 } snk_trainer_stats_t;
 
+/* sizeof(snk_trainer_cfg_t), sizeof(snk_trainer_stats_t) as compiled into the library */
+int snk_abi_sizes(int64_t *trainer_cfg_size, int64_t *trainer_stats_size);
+/* Trainer(; ...) (structs.jl:164-174) over a batch of games, a model and a replay buffer */
 int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn m, snk_replay rb, const snk_trainer_cfg_t *cfg);
 int snk_trainer_destroy(snk_trainer t);
 /* iters lockstep iterations; learn = 0 is fill_buffer! (utils.jl:389-402);
@@ -227,6 +243,12 @@ int snk_trainer_run_partial(snk_trainer t, int32_t n_updates);
  * when nb % target_update_rate == 0, then nb += 1. train! starts at 0
  * (utils.jl:431,469), compute_D at 1 (compute_D.jl:56,134). Default 0. */
 int snk_trainer_set_nb(snk_trainer t, int64_t nb);
+/* test/trace hook: after every update the finished gradient (P floats, packed layout
+ * of snk_dqn_buffer_ptr) is also copied to grad_ring_dev + slot * P, where slot =
+ * (index of the update within the call's launch sequence: iteration in the captured
+ * graph x updates_per_iter + update) % slots. One device-to-device copy per update,
+ * appended to the same graphs (which are re-captured). NULL turns it off. */
+int snk_trainer_set_trace(snk_trainer t, float *grad_ring_dev, int64_t slots);
 int snk_trainer_stats(snk_trainer t, snk_trainer_stats_t *out);
 /* tr.losses: loss of update u at host[u % loss_log_capacity] */
 int snk_trainer_losses(snk_trainer t, double *host, int64_t n);

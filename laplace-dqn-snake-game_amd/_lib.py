@@ -100,15 +100,18 @@ _PROTOS = {
     "snk_dqn_last_q": [vp, vp, i64],
     "snk_dqn_time_act_layers": [vp, vp, i32, vp],
     "snk_env_time_step": [vp, vp, vp, i32, P(f64)],
+    "snk_dqn_train_activations": [vp, i32, vp, i64],
     "snk_dqn_loss_grad": [vp, vp, vp, i64, f64, P(f64)],
     "snk_dqn_loss_grad_batch": [vp, vp, vp, vp, vp, vp, vp, i64, f64, P(f64)],
     "snk_dqn_apply_grad": [vp],
     "snk_dqn_update": [vp, vp, vp, i64, f64, P(f64)],
+    "snk_abi_sizes": [P(i64), P(i64)],
     "snk_trainer_create": [P(vp), vp, vp, vp, vp],
     "snk_trainer_destroy": [vp],
     "snk_trainer_run": [vp, i64, i32, i32],
     "snk_trainer_run_partial": [vp, i32],
     "snk_trainer_set_nb": [vp, i64],
+    "snk_trainer_set_trace": [vp, vp, i64],
     "snk_trainer_stats": [vp, vp],
     "snk_trainer_time_act_kernel": [vp, i32, vp],
     "snk_trainer_losses": [vp, vp, i64],
@@ -149,17 +152,25 @@ SNK_LAP_D32 = 4
 
 
 class TrainerCfg(C.Structure):
-    """snk_trainer_cfg_t"""
-    _fields_ = [("epsilon", f32), ("epsilon_end", f32), ("decay", f32), ("updates_per_iter", i32),
+    """snk_trainer_cfg_t (struct_size set by the constructor: the library's ABI guard)"""
+    _fields_ = [("struct_size", i32), ("epsilon", f32), ("epsilon_end", f32), ("decay", f32), ("updates_per_iter", i32),
                 ("target_update_rate", i64), ("gamma", f64), ("seed", u64), ("loss_log_capacity", i64),
                 ("graph_unroll", i32)]
 
+    def __init__(self, *args, **kw):
+        super().__init__(C.sizeof(self), *args, **kw)
+
 
 class TrainerStats(C.Structure):
-    """snk_trainer_stats_t"""
-    _fields_ = [("episodes", i64), ("score_sum", i64), ("updates", i64), ("nb", i64), ("env_steps", i64),
+    """snk_trainer_stats_t (struct_size set by the constructor: the library's ABI guard)"""
+    _fields_ = [("struct_size", i32), ("episodes", i64), ("score_sum", i64), ("updates", i64), ("nb", i64), ("env_steps", i64),
                 ("reward_sum", f64), ("last_loss", f64), ("reward_max", f32), ("score_max", i32),
                 ("epsilon", f32)]
+
+    def __init__(self, *args, **kw):
+        super().__init__(C.sizeof(self), *args, **kw)
+
+
 _RESTYPE = {"snk_last_error": C.c_char_p}
 
 

@@ -412,6 +412,20 @@ extern "C" int snk_dqn_last_q(snk_dqn h, float *q_host, int64_t n) {
     });
 }
 
+extern "C" int snk_dqn_train_activations(snk_dqn h, int32_t layer, float *host, int64_t n) {
+    return guard([&] {
+        SNK_CHECK(h && host && n >= 0 && layer >= 0 && layer <= 3, SNK_ERR_INVALID, "bad train_activations arguments");
+        SNK_CHECK(!h->deep, SNK_ERR_INVALID, "deep net: train_activations is not supported");
+        const QWork &w = h->trn;
+        SNK_CHECK(w.cap > 0, SNK_ERR_STATE, "no training forward has run");
+        const float *src[4] = {w.a1, w.a2, w.a3, w.h1};
+        const int64_t per[4] = {(int64_t)h->L.ncell * 16, (int64_t)h->L.ncell * 32, h->L.K1, 64};
+        SNK_CHECK(n <= w.cap * per[layer], SNK_ERR_INVALID, "n exceeds the training workspace");
+        SNK_HIP(hipMemcpyAsync(host, src[layer], n * sizeof(float), hipMemcpyDeviceToHost, stream()));
+        SNK_HIP(hipStreamSynchronize(stream()));
+    });
+}
+
 static void finish_loss(snk_dqn h, double *loss_host) {
     if (!loss_host) return;
     SNK_HIP(hipMemcpyAsync(loss_host, h->loss_dev, sizeof(double), hipMemcpyDeviceToHost, stream()));

@@ -405,6 +405,7 @@ extern "C" int snk_laplace_gram(snk_laplace h, float *ms_out) {
 extern "C" int snk_jacobian(snk_dqn m, snk_replay rb, const int64_t *slots_dev, int64_t n, float *J_dev) {
     return guard([&] {
         SNK_CHECK(m && rb && J_dev && n > 0, SNK_ERR_INVALID, "bad argument");
+        SNK_CHECK(!m->deep, SNK_ERR_INVALID, "deep net: per-sample Jacobians are not supported");
         const ReplayDev &R = replay_dev(rb);
         SNK_CHECK(R.bs == m->L.bs && R.C == m->L.C, SNK_ERR_INVALID, "replay geometry differs from the model");
         int64_t len = 0;
@@ -431,6 +432,7 @@ static void jacobian_gram_tiles(snk_dqn m, snk_replay rb, int64_t n, float *G_de
     {
         SNK_CHECK(m && rb && G_dev && n > 0 && nranks >= 1 && rank >= 0 && rank < nranks, SNK_ERR_INVALID,
                   "bad argument");
+        SNK_CHECK(!m->deep, SNK_ERR_INVALID, "deep net: the Jacobian Gram is not supported");
         const ReplayDev &R = replay_dev(rb);
         SNK_CHECK(R.bs == m->L.bs && R.C == m->L.C, SNK_ERR_INVALID, "replay geometry differs from the model");
         int64_t len = 0;
@@ -954,6 +956,8 @@ extern "C" int snk_laplace_sampling(snk_laplace h, snk_dqn m, snk_replay rb, int
                                     int32_t *lengths_host) {
     return guard([&] {
         SNK_CHECK(h && m && rb && n_models >= 0 && tr_reward_out && n_better_out, SNK_ERR_INVALID, "NULL argument");
+        SNK_CHECK(!m->deep, SNK_ERR_INVALID, "deep net: laplace_sampling! is not supported (its rollout kernel is the "
+                  "reference architecture's)");
         const QLayout &L = m->L;
         const ReplayDev &D = replay_dev(rb);
         SNK_CHECK(D.bs == L.bs && D.C == L.C, SNK_ERR_INVALID, "replay geometry differs from the model");

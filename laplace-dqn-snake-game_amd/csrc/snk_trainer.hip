@@ -63,6 +63,10 @@ struct snk_trainer_s {
     hipGraphExec_t exec[4] = {nullptr, nullptr, nullptr, nullptr};
     int unroll = 8;
     int64_t ws_gen = 0;   // dqn workspace generation the graphs were captured against
+    // snk_trainer_set_trace: every update's finished gradient is also copied to
+    // trace + slot * P, slot = (position of the update in the launch sequence) % trace_slots
+    float *trace = nullptr;
+    int64_t trace_slots = 0;
     void drop_graphs() {
         for (int i = 0; i < 4; ++i) {
             if (exec[i]) (void)hipGraphExecDestroy(exec[i]);
@@ -76,7 +80,7 @@ struct snk_trainer_s {
 // One iteration's launch sequence (capturable: no host sync, no allocation),
 // with n_upd DQN updates after the env step. The first update's replay draw
 // counts the n transitions this step stores.
-static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream_t s) {
+static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream_t s, int it = 0) {
     const EnvDev &E = env_dev(h->env);
     const ReplayDev &R = replay_dev(h->rb);
     snk_dqn_s *q = h->dqn;
@@ -140,13 +144,31 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
                 grad_update_launch(q->L, &pend, q->grad, &ut, s, &post);
             }
         }
+        if (h->trace) {
+            const int64_t slot = ((int64_t)it * n_upd + u) % h->trace_slots;
+            SNK_HIP(hipMemcpyAsync(h->trace + slot * q->L.P, q->grad, q->L.P * sizeof(float),
+                                   hipMemcpyDeviceToDevice, s));
+        }
     }
+}
+
+static_assert(sizeof(snk_trainer_cfg_t) == 64 && sizeof(snk_trainer_stats_t) == 80, "ABI sizes in snakehip.h");
+
+extern "C" int snk_abi_sizes(int64_t *cfg_size, int64_t *stats_size) {
+    return guard([&] {
+        SNK_CHECK(cfg_size && stats_size, SNK_ERR_INVALID, "NULL argument");
+        *cfg_size = (int64_t)sizeof(snk_trainer_cfg_t);
+        *stats_size = (int64_t)sizeof(snk_trainer_stats_t);
+    });
 }
 
 extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, snk_replay rb,
                                   const snk_trainer_cfg_t *cfg) {
     return guard([&] {
         SNK_CHECK(out && env && dqn && rb && cfg, SNK_ERR_INVALID, "NULL argument");
+        SNK_CHECK(cfg->struct_size == (int32_t)sizeof(snk_trainer_cfg_t), SNK_ERR_INVALID,
+                  "snk_trainer_cfg_t.struct_size = %d, the library's struct has %d bytes (binding out of date)",
+                  cfg->struct_size, (int)sizeof(snk_trainer_cfg_t));
         const EnvDev &E = env_dev(env);
         const ReplayDev &R = replay_dev(rb);
         SNK_CHECK(E.autoreset, SNK_ERR_STATE, "the batched trainer needs auto-reset envs");
@@ -250,7 +272,7 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
             if (h->exec[slot]) return;
             SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             try {
-                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s);
+                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s, i);
             } catch (...) {
                 hipGraph_t dummy;
                 (void)hipStreamEndCapture(s, &dummy);
@@ -260,7 +282,7 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
             SNK_HIP(hipGraphInstantiate(&h->exec[slot], h->graph[slot], nullptr, nullptr, 0));
         };
         if (!use_graph) {
-            for (int64_t i = 0; i < iters; ++i) trainer_iteration(h, learn != 0, upi, s);
+            for (int64_t i = 0; i < iters; ++i) trainer_iteration(h, learn != 0, upi, s, (int)(i % (1 << 20)));
             return;
         }
         const int U = h->unroll;
@@ -281,6 +303,16 @@ extern "C" int snk_trainer_run_partial(snk_trainer h, int32_t n_updates) {
         if (n_updates > 0) trainer_check_replay(h);
         trainer_refresh(h);
         trainer_iteration(h, true, n_updates, stream());
+    });
+}
+
+extern "C" int snk_trainer_set_trace(snk_trainer h, float *grad_ring_dev, int64_t slots) {
+    return guard([&] {
+        SNK_CHECK(h && (grad_ring_dev == nullptr || slots > 0), SNK_ERR_INVALID, "bad set_trace arguments");
+        SNK_HIP(hipStreamSynchronize(stream()));
+        h->trace = grad_ring_dev;
+        h->trace_slots = grad_ring_dev ? slots : 0;
+        h->drop_graphs();   // re-captured with (or without) the copies
     });
 }
 
@@ -313,6 +345,9 @@ extern "C" int snk_trainer_set_comm(snk_trainer h, snk_comm comm) {
 extern "C" int snk_trainer_stats(snk_trainer h, snk_trainer_stats_t *out) {
     return guard([&] {
         SNK_CHECK(h && out, SNK_ERR_INVALID, "NULL argument");
+        SNK_CHECK(out->struct_size == (int32_t)sizeof(snk_trainer_stats_t), SNK_ERR_INVALID,
+                  "snk_trainer_stats_t.struct_size = %d, the library's struct has %d bytes (binding out of date)",
+                  out->struct_size, (int)sizeof(snk_trainer_stats_t));
         TrainStats st;
         hipStream_t s = stream();
         SNK_HIP(hipMemcpyAsync(&st, h->stats, sizeof st, hipMemcpyDeviceToHost, s));

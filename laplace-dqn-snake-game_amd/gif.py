@@ -129,7 +129,7 @@ def play_best_game(tr_or_model, name: str | None = None, path: str = "./trainer_
     model = getattr(tr_or_model, "model", tr_or_model)
     exp, ep_reward, boards = play_episode(model, 0.0)
     hist = board_history(boards, model.n_frames)
-    score = int(np.sum(np.asarray(exp["rewards"]) == np.float32(1.0)))
+    score = exp["score"]   # the device's game.score: an eat on a losing step still counts (utils.jl:72, :90)
     if name is not None:
         save_gif(hist, model.board_size, os.path.join(path, name + ".gif"), fps=fps)
     return score, ep_reward, hist

@@ -124,48 +124,71 @@ class LaplaceD:
 
 
 def compute_D(tr, K: int = 1000, thin: int = 10, burn_in: int = 50_000, graph: bool = True,
-              reset_optimizer: bool = True, schedule: str = "episode") -> LaplaceD:
+              reset_optimizer: bool = True, schedule: str = "episode", n_batches: int | None = None,
+              on_update=None) -> LaplaceD | None:
     """compute_D.jl:33-86 on a Trainer: fill_buffer!, a fresh RMSProp state
-    (`Flux.setup`, :47), then the training loop over nb = 1, 2, ...: from
-    nb == burn_in on, at nb % thin == 0 the current q_net goes into the next
-    column *before* that update runs; after the K-th column: Welford +
-    centring, return (the BSON save of :84 is the caller's business).
-    update_target_net! runs after update nb when nb % rate == 0 (:129-132).
+    (`Flux.setup`, :47), then the training loop `while nb <= n_batches`
+    (:56-58, nb from 1, n_batches = tr.n_batches unless given): from
+    nb == burn_in on (:61), at nb % thin == 0 the current q_net goes into the
+    next column *before* that nb's update runs (:67-71); right after the K-th
+    column (no update at that nb): Welford + centring (:74-81) and return (the
+    BSON save of :84 is the caller's business). update_target_net! runs after
+    update nb when nb % rate == 0 (:129-132).
+
+    If the loop ends (nb > n_batches) before the K-th column, the reference
+    returns `nothing` without building D; so does this: the updates still run,
+    and None is returned.
 
     schedule="episode": the reference's loop body, one full epsilon-greedy
     episode stored and one B-sample update per nb (:89-138, EpisodeLoop).
     schedule="batched": one lockstep step of tr's n_envs games per update
-    (the device trainer, graph-replayed), with the same nb bookkeeping."""
+    (the device trainer, graph-replayed), with the same nb bookkeeping.
+
+    on_update(nb, loss): observer called after every update (episode schedule;
+    loss = that update's Huber loss) or after every run of updates ending at nb
+    (batched schedule; loss = None). Test infrastructure uses it to check each
+    update against the oracle."""
     from .trainer import EpisodeLoop, fill_buffer_
 
     model = tr.model
+    n_batches = int(tr.n_batches if n_batches is None else n_batches)
     lap = LaplaceD(model.P, K)
     first = burn_in if burn_in % thin == 0 else burn_in + (thin - burn_in % thin)   # first nb snapshotted
+    snaps = [first + pos * thin for pos in range(K)]        # nb at which column pos is taken
     if schedule == "episode":
         loop = EpisodeLoop(tr)
         loop.fill()
-        if reset_optimizer:
-            model.set_params(np.zeros(model.P, np.float32), _lib.SNK_NET_OPT_STATE)
-        nb = 1
-        for pos in range(K):
-            while nb < first + pos * thin:
-                loop.step(nb)
-                nb += 1
-            lap.snapshot(model, pos)
     elif schedule == "batched":
         if tr.updates_per_iter != 1:
             raise ValueError("compute_D snapshots between single updates: use updates_per_iter = 1")
         fill_buffer_(tr, graph=graph)
-        if reset_optimizer:
-            model.set_params(np.zeros(model.P, np.float32), _lib.SNK_NET_OPT_STATE)
         tr.set_nb(1)
-        tr.run(first - 1, learn=True, graph=graph)          # updates nb = 1 .. first-1
-        for pos in range(K):
-            lap.snapshot(model, pos)                          # before update nb = first + pos*thin
-            if pos + 1 < K:
-                tr.run(thin, learn=True, graph=graph)
     else:
         raise ValueError(f"unknown schedule {schedule!r}")
+    if reset_optimizer:
+        model.set_params(np.zeros(model.P, np.float32), _lib.SNK_NET_OPT_STATE)
+
+    def updates(nb_from: int, nb_to: int) -> None:          # updates nb_from .. nb_to (inclusive)
+        if nb_to < nb_from:
+            return
+        if schedule == "episode":
+            for nb in range(nb_from, nb_to + 1):
+                _, loss = loop.step(nb)
+                if on_update is not None:
+                    on_update(nb, loss)
+        else:
+            tr.run(nb_to - nb_from + 1, learn=True, graph=graph)
+            if on_update is not None:
+                on_update(nb_to, None)
+
+    nb = 1
+    for pos, at in enumerate(snaps):
+        if at > n_batches:                                  # `while nb <= n_batches` ends first
+            updates(nb, n_batches)
+            return None
+        updates(nb, at - 1)
+        nb = at
+        lap.snapshot(model, pos)
     lap.fit_center()
     return lap
 

@@ -77,6 +77,17 @@ class DQNModel:
         call("snk_dqn_buffer_ptr", self._h, which, C.byref(p))
         return p.value
 
+    def flux_index(self) -> np.ndarray:
+        """perm[j] = the Flux.destructure index of packed position j (the
+        device layout behind buffer_ptr and the trainer's gradient trace):
+        flux[perm] = packed. Found by round-tripping 0..P-1 through the
+        gradient slot, which is restored afterwards."""
+        keep = self.grad
+        self.set_params(np.arange(self.P, dtype=np.float32), _lib.SNK_NET_GRAD)   # exact below 2^24
+        perm = _lib.view_numpy(self.buffer_ptr(_lib.SNK_NET_GRAD), self.P, np.float32).astype(np.int64)
+        self.set_params(keep, _lib.SNK_NET_GRAD)
+        return perm
+
     def forward(self, x, which: int = _lib.SNK_NET_Q) -> np.ndarray:
         """Chain forward on Float32 states [B, C, bs*bs] (Julia (bs,bs,C,B)
         memory) -> Q [B, 3]."""
@@ -116,6 +127,19 @@ class DQNModel:
         loss = C.c_double(0)
         call("snk_dqn_update", self._h, rpb.handle, idx.ptr, B, gamma, C.byref(loss))
         return loss.value
+
+    def train_relu_decisions(self, B: int) -> np.ndarray:
+        """The relu decisions (output > 0) of q_net in the last training forward
+        over B samples, [B, n] uint8 in the oracle's order: a1 | a2 | a3
+        channel-major (position = i + j*side) | h1. Test infrastructure (kink-aware
+        gradient parity, oracle.dqn_loss_grad_kinks)."""
+        bs, wo = self.board_size, self.board_size - 5
+        parts = []
+        for layer, (npos, ch) in enumerate(((bs * bs, 16), (bs * bs, 32), (wo * wo, 64), (1, 64))):
+            a = np.empty((B, npos, ch), np.float32)
+            call("snk_dqn_train_activations", self._h, layer, ptr(a), a.size)
+            parts.append((a > 0).transpose(0, 2, 1).reshape(B, -1))
+        return np.ascontiguousarray(np.concatenate(parts, axis=1), np.uint8)
 
     @property
     def grad(self) -> np.ndarray:

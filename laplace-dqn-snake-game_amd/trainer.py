@@ -85,10 +85,21 @@ class Trainer:
         (compute_D.jl:56)."""
         call("snk_trainer_set_nb", self._h, int(nb))
 
+    def set_trace(self, ring: DeviceArray | None) -> None:
+        """Copy every update's finished gradient into ring[slot] (a device
+        [slots, P] float32 array; slot = position of the update in the run's
+        launch sequence % slots); None turns it off. Test infrastructure: it
+        makes each update of a captured multi-iteration graph observable."""
+        if ring is None:
+            call("snk_trainer_set_trace", self._h, None, 0)
+        else:
+            call("snk_trainer_set_trace", self._h, ring.ptr, int(ring.shape[0]))
+        self._trace = ring
+
     def stats(self) -> dict:
         st = _lib.TrainerStats()
         call("snk_trainer_stats", self._h, C.byref(st))
-        return {k: getattr(st, k) for k, _ in st._fields_}
+        return {k: getattr(st, k) for k, _ in st._fields_ if k != "struct_size"}
 
     @property
     def losses(self) -> np.ndarray:
@@ -205,13 +216,14 @@ def play_episode(model: DQNModel, epsilon: float, *, actions_list=None, board_si
                  n_frames: int | None = None, seed: int = 0, max_steps: int = 100000):
     """utils.jl:198-259: one SnakeGame() played to the end (epsilon-greedy, or
     the fixed `actions_list` of action indices). Returns (experiences,
-    episode_reward, boards) where boards is the board history b_0..b_L."""
+    episode_reward, boards) where boards is the board history b_0..b_L;
+    experiences["score"] is the game's score at the end (game.score)."""
     bs = board_size or model.board_size
     nf = n_frames or model.n_frames
     game = SnakeGame(bs, nf, n_envs=1, autoreset=True)
     rb = ReplayBuffer(max_steps + 1, board_size=bs, n_frames=nf, batch_size=1)
     act = DeviceArray(1, np.uint8)
-    L = 0
+    L, score = 0, 0
     while L < max_steps:
         if actions_list is not None:
             if L >= len(actions_list):
@@ -221,9 +233,12 @@ def play_episode(model: DQNModel, epsilon: float, *, actions_list=None, board_si
             call("snk_dqn_act", model.handle, game.handle, float(epsilon), int(seed), act.ptr)
         step_indices_dev(game, act.ptr, replay=rb)
         L += 1
-        if game.last("done")["done"][0]:
+        o = game.last("done", "score")
+        score = int(o["score"][0])                           # game.score after this step (utils.jl:72)
+        if o["done"][0]:
             break
     exp = stack_exp(rb, np.arange(L, dtype=np.int64))
+    exp["score"] = score
     ep_reward = np.float32(0)
     for r in exp["rewards"]:
         ep_reward = np.float32(ep_reward + r)

@@ -61,6 +61,11 @@ def lib():
     L.orc_dqn_loss_grad.restype = C.c_double
     L.orc_dqn_loss_grad.argtypes = [C.c_int, C.c_int, F32P, F32P, C.c_int, F64P, I32P, F32P, F64P,
                                     U8P, U8P, C.c_double, F64P, F64P]
+    L.orc_qnet_relu_count.restype = C.c_int64
+    L.orc_qnet_relu_count.argtypes = [C.c_int, C.c_int]
+    L.orc_dqn_loss_grad_ex.restype = C.c_double
+    L.orc_dqn_loss_grad_ex.argtypes = [C.c_int, C.c_int, F32P, F32P, C.c_int, F64P, I32P, F32P, F64P,
+                                       U8P, U8P, C.c_double, F64P, F64P, C.c_void_p, C.c_void_p, C.c_void_p]
     L.orc_deep_nparams.restype = C.c_int64
     L.orc_deep_nparams.argtypes = [C.c_int, C.c_int]
     L.orc_deep_forward.argtypes = [C.c_int, C.c_int, F32P, C.c_int, F64P, F64P]
@@ -215,6 +220,30 @@ def dqn_loss_grad(bs, C, q_params, t_params, s, a_idx, r, s_next, done, mask3, g
                                    np.ascontiguousarray(done, np.uint8),
                                    np.ascontiguousarray(mask3, np.uint8).reshape(B, 3), gamma, g, tgt)
     return loss, g, tgt
+
+
+def dqn_loss_grad_kinks(bs, C, q_params, t_params, s, a_idx, r, s_next, done, mask3, gamma=0.97, relu_in=None):
+    """dqn_loss_grad with the q_net's relu decisions exposed: returns (loss,
+    grad, relu decisions [B, n], margins [B, n]) where n = a1 | a2 | a3 | h1
+    (channel-major per layer, orc_qnet_relu_count) and margin = z / sum|terms|.
+    relu_in ([B, n] uint8) replaces the z > 0 decisions (the device's own, to
+    check that a gradient difference is a kink decision and nothing else)."""
+    s = np.ascontiguousarray(s, np.float64).reshape(-1, C * bs * bs)
+    B = s.shape[0]
+    n = int(lib().orc_qnet_relu_count(bs, C))
+    g = np.zeros(len(q_params), np.float64)
+    tgt = np.zeros(B, np.float64)
+    dec = np.zeros((B, n), np.uint8)
+    mg = np.zeros((B, n), np.float64)
+    rin = None if relu_in is None else np.ascontiguousarray(relu_in, np.uint8).reshape(B, n)
+    loss = lib().orc_dqn_loss_grad_ex(bs, C, np.ascontiguousarray(q_params, np.float32),
+                                      np.ascontiguousarray(t_params, np.float32), B, s,
+                                      np.ascontiguousarray(a_idx, np.int32), np.ascontiguousarray(r, np.float32),
+                                      np.ascontiguousarray(s_next, np.float64).reshape(B, -1),
+                                      np.ascontiguousarray(done, np.uint8),
+                                      np.ascontiguousarray(mask3, np.uint8).reshape(B, 3), gamma, g, tgt,
+                                      None if rin is None else rin.ctypes.data, dec.ctypes.data, mg.ctypes.data)
+    return loss, g, dec, mg
 
 
 # ---------------------------------------------------------------- deeper bf16 Q-net (configs[2])

@@ -136,17 +136,17 @@ void orc_game_init(orc_game *g, int bs, int n_frames, int max_hist, const int32_
     int8_t *b = g->hist[0];
     for (int j = 0; j < bs; j++)
         for (int i = 0; i < bs; i++)
-            b[i + j * bs] = (i == 0 || i == bs - 1 || j == 0 || j == bs - 1) ? -1 : 0;  /* :78-81 */
-    b[3 + 4 * bs] = 2;                                   /* :84 board[4,5] = 2 */
-    g->snake[0] = (int16_t)((bs - 3) + 1 * bs);          /* :88 (bs-2, 2) head */
+            b[i + j * bs] = (i == 0 || i == bs - 1 || j == 0 || j == bs - 1) ? -1 : 0;  /* :37-40 walls */
+    b[3 + 4 * bs] = 2;                                   /* :43 board[4,5] = 2 */
+    g->snake[0] = (int16_t)((bs - 3) + 1 * bs);          /* :47 (bs-2, 2) head */
     g->snake[1] = (int16_t)((bs - 2) + 1 * bs);          /*      (bs-1, 2) tail */
     g->len = 2;
-    b[g->snake[0]] = 1; b[g->snake[1]] = 1;              /* :90-92 */
+    b[g->snake[0]] = 1; b[g->snake[1]] = 1;              /* :49-51 */
     memcpy(g->hist[1], b, (size_t)bs * bs);
     memcpy(g->hist[2], b, (size_t)bs * bs);
-    g->hist_len = n_frames;                              /* :94 n_frames copies */
-    g->dir = -1;                                         /* :106 (0,0) */
-    g->prev_dir = 0;                                     /* :107 (-1,0) = U */
+    g->hist_len = n_frames;                              /* :53 n_frames copies */
+    g->dir = -1;                                         /* :65 (0,0) */
+    g->prev_dir = 0;                                     /* :66 (-1,0) = U */
     g->n_food = n_food;
     memcpy(g->food, food, (size_t)n_food * sizeof(int32_t));
 }
@@ -354,13 +354,18 @@ static qlayout qnet_layout(int bs, int C) {
 }
 int64_t orc_qnet_nparams(int bs, int C) { return qnet_layout(bs, C).P; }
 
-static void conv_fwd(int H, int Cin, int Cout, int K, int pad, const float *w, const float *b,
-                     const double *x, double *y) {
+/* One relu layer's decision per element: active = s > 0 (the reference's
+ * relu), or the decision given in mk (kink-aware parity tests: the device's own
+ * decisions, see orc_qnet_backward_ex). mo (if set) receives the decisions, mg
+ * the margin s / (|b| + sum |w x|): how close the pre-activation is to the kink
+ * relative to the dot product's own scale. */
+static void conv_fwd_k(int H, int Cin, int Cout, int K, int pad, const float *w, const float *b,
+                       const double *x, double *y, const uint8_t *mk, uint8_t *mo, double *mg) {
     int Ho = H + 2 * pad - K + 1;
     for (int co = 0; co < Cout; co++)
         for (int j = 0; j < Ho; j++)
             for (int i = 0; i < Ho; i++) {
-                double s = b[co];
+                double s = b[co], sa = fabs((double)b[co]);
                 for (int ci = 0; ci < Cin; ci++)
                     for (int v = 0; v < K; v++) {
                         int xj = j + (K - 1 - v) - pad;
@@ -368,22 +373,33 @@ static void conv_fwd(int H, int Cin, int Cout, int K, int pad, const float *w, c
                         for (int u = 0; u < K; u++) {
                             int xi = i + (K - 1 - u) - pad;
                             if (xi < 0 || xi >= H) continue;
-                            s += (double)w[u + v * K + ci * K * K + co * K * K * Cin] * x[xi + xj * H + ci * H * H];
+                            double t = (double)w[u + v * K + ci * K * K + co * K * K * Cin] * x[xi + xj * H + ci * H * H];
+                            s += t;
+                            sa += fabs(t);
                         }
                     }
-                y[i + j * Ho + co * Ho * Ho] = s > 0 ? s : 0;     /* relu */
+                int oi = i + j * Ho + co * Ho * Ho;
+                int act = mk ? mk[oi] != 0 : s > 0;
+                y[oi] = act ? s : 0;                             /* relu */
+                if (mo) mo[oi] = (uint8_t)act;
+                if (mg) mg[oi] = sa > 0 ? s / sa : 0.0;
             }
 }
-/* dz = dy .* (y > 0); accumulates dw, db; dx (if non-NULL) overwritten */
-static void conv_bwd(int H, int Cin, int Cout, int K, int pad, const float *w, const double *x,
-                     const double *y, const double *dy, double *dw, double *db, double *dx) {
+static void conv_fwd(int H, int Cin, int Cout, int K, int pad, const float *w, const float *b,
+                     const double *x, double *y) {
+    conv_fwd_k(H, Cin, Cout, K, pad, w, b, x, y, NULL, NULL, NULL);
+}
+/* dz = dy .* relu'(z) with relu' = the layer's decisions (act) or y > 0;
+ * accumulates dw, db; dx (if non-NULL) overwritten */
+static void conv_bwd_k(int H, int Cin, int Cout, int K, int pad, const float *w, const double *x,
+                       const uint8_t *act, const double *y, const double *dy, double *dw, double *db, double *dx) {
     int Ho = H + 2 * pad - K + 1;
     if (dx) memset(dx, 0, sizeof(double) * (size_t)H * H * Cin);
     for (int co = 0; co < Cout; co++)
         for (int j = 0; j < Ho; j++)
             for (int i = 0; i < Ho; i++) {
                 int oi = i + j * Ho + co * Ho * Ho;
-                if (!(y[oi] > 0)) continue;
+                if (act ? !act[oi] : !(y[oi] > 0)) continue;
                 double dz = dy[oi];
                 db[co] += dz;
                 for (int ci = 0; ci < Cin; ci++)
@@ -401,16 +417,33 @@ static void conv_bwd(int H, int Cin, int Cout, int K, int pad, const float *w, c
                     }
             }
 }
+static void conv_bwd(int H, int Cin, int Cout, int K, int pad, const float *w, const double *x,
+                     const double *y, const double *dy, double *dw, double *db, double *dx) {
+    conv_bwd_k(H, Cin, Cout, K, pad, w, x, NULL, y, dy, dw, db, dx);
+}
 
-typedef struct { double *a1, *a2, *a3, *h1; } acts;
-static void fwd_one(const qlayout *L, int bs, int C, const float *p, const double *x, acts *A, double *q) {
-    conv_fwd(bs, C, 16, 3, 1, p + L->off_w1, p + L->off_b1, x, A->a1);
-    conv_fwd(bs, 16, 32, 3, 1, p + L->off_w2, p + L->off_b2, A->a1, A->a2);
-    conv_fwd(bs, 32, 64, 6, 0, p + L->off_w3, p + L->off_b3, A->a2, A->a3);
+typedef struct { double *a1, *a2, *a3, *h1; uint8_t *m; } acts;   /* m: decisions [a1 | a2 | a3 | h1] */
+static int64_t relu_count(const qlayout *L, int bs) { return (int64_t)bs * bs * 48 + (int64_t)L->Wo * L->Wo * 64 + 64; }
+/* mk / mg: this sample's [a1 | a2 | a3 | h1] slices (or NULL) */
+static void fwd_one_k(const qlayout *L, int bs, int C, const float *p, const double *x, acts *A, double *q,
+                      const uint8_t *mk, double *mg) {
+    const int64_t o2 = (int64_t)bs * bs * 16, o3 = o2 + (int64_t)bs * bs * 32, oh = o3 + (int64_t)L->Wo * L->Wo * 64;
+    conv_fwd_k(bs, C, 16, 3, 1, p + L->off_w1, p + L->off_b1, x, A->a1, mk, A->m, mg);
+    conv_fwd_k(bs, 16, 32, 3, 1, p + L->off_w2, p + L->off_b2, A->a1, A->a2, mk ? mk + o2 : NULL, A->m + o2,
+               mg ? mg + o2 : NULL);
+    conv_fwd_k(bs, 32, 64, 6, 0, p + L->off_w3, p + L->off_b3, A->a2, A->a3, mk ? mk + o3 : NULL, A->m + o3,
+               mg ? mg + o3 : NULL);
     for (int o = 0; o < 64; o++) {                               /* Dense(F1 -> 64, relu) */
-        double s = p[L->off_d1b + o];
-        for (int f = 0; f < L->F1; f++) s += (double)p[L->off_d1w + o + f * 64] * A->a3[f];
-        A->h1[o] = s > 0 ? s : 0;
+        double s = p[L->off_d1b + o], sa = fabs((double)p[L->off_d1b + o]);
+        for (int f = 0; f < L->F1; f++) {
+            double t = (double)p[L->off_d1w + o + f * 64] * A->a3[f];
+            s += t;
+            sa += fabs(t);
+        }
+        int act = mk ? mk[oh + o] != 0 : s > 0;
+        A->h1[o] = act ? s : 0;
+        A->m[oh + o] = (uint8_t)act;
+        if (mg) mg[oh + o] = sa > 0 ? s / sa : 0.0;
     }
     for (int a = 0; a < 3; a++) {                                /* Dense(64 -> 3) */
         double s = p[L->off_d2b + a];
@@ -418,15 +451,19 @@ static void fwd_one(const qlayout *L, int bs, int C, const float *p, const doubl
         q[a] = s;
     }
 }
+static void fwd_one(const qlayout *L, int bs, int C, const float *p, const double *x, acts *A, double *q) {
+    fwd_one_k(L, bs, C, p, x, A, q, NULL, NULL);
+}
 static acts acts_alloc(int bs) {
     acts A; int Wo = bs - 5;
     A.a1 = (double *)malloc(sizeof(double) * bs * bs * 16);
     A.a2 = (double *)malloc(sizeof(double) * bs * bs * 32);
     A.a3 = (double *)malloc(sizeof(double) * Wo * Wo * 64);
     A.h1 = (double *)malloc(sizeof(double) * 64);
+    A.m = (uint8_t *)malloc((size_t)bs * bs * 48 + (size_t)Wo * Wo * 64 + 64);
     return A;
 }
-static void acts_free(acts *A) { free(A->a1); free(A->a2); free(A->a3); free(A->h1); }
+static void acts_free(acts *A) { free(A->a1); free(A->a2); free(A->a3); free(A->h1); free(A->m); }
 
 void orc_qnet_forward(int bs, int C, const float *params, int B, const double *x, double *q) {
     qlayout L = qnet_layout(bs, C);
@@ -435,19 +472,31 @@ void orc_qnet_forward(int bs, int C, const float *params, int B, const double *x
     acts_free(&A);
 }
 
-void orc_qnet_backward(int bs, int C, const float *p, int B, const double *x, const double *dq, double *g) {
+int64_t orc_qnet_relu_count(int bs, int C) { qlayout L = qnet_layout(bs, C); return relu_count(&L, bs); }
+
+/* orc_qnet_backward with the relu decisions of every sample given (mask_in,
+ * [B][relu_count]: a1 (bs*bs*16), a2 (bs*bs*32), a3 (Wo*Wo*64) channel-major
+ * like the activations, then h1 (64); NULL = the reference's z > 0), and the
+ * decisions taken / margins returned (mask_out, margin_out, same layout, may be
+ * NULL). A kink (z within rounding of 0) makes the gradient discontinuous: an
+ * fp32 device may decide it the other way than fp64; the parity tests use this
+ * to check such differences are kink decisions and nothing else. */
+void orc_qnet_backward_ex(int bs, int C, const float *p, int B, const double *x, const double *dq, double *g,
+                          const uint8_t *mask_in, uint8_t *mask_out, double *margin_out) {
     qlayout L = qnet_layout(bs, C);
     acts A = acts_alloc(bs);
-    int Wo = L.Wo;
+    const int64_t NR = relu_count(&L, bs);
+    const int64_t o2 = (int64_t)bs * bs * 16, o3 = o2 + (int64_t)bs * bs * 32, oh = o3 + (int64_t)L.Wo * L.Wo * 64;
     double *dh1 = (double *)malloc(sizeof(double) * 64);
-    double *da3 = (double *)malloc(sizeof(double) * Wo * Wo * 64);
+    double *da3 = (double *)malloc(sizeof(double) * L.F1);
     double *da2 = (double *)malloc(sizeof(double) * bs * bs * 32);
     double *da1 = (double *)malloc(sizeof(double) * bs * bs * 16);
     double q[3];
     for (int b = 0; b < B; b++) {
         const double *xb = x + (size_t)b * C * bs * bs;
         const double *d = dq + 3 * b;
-        fwd_one(&L, bs, C, p, xb, &A, q);
+        fwd_one_k(&L, bs, C, p, xb, &A, q, mask_in ? mask_in + b * NR : NULL, margin_out ? margin_out + b * NR : NULL);
+        if (mask_out) memcpy(mask_out + b * NR, A.m, (size_t)NR);
         for (int a = 0; a < 3; a++) {
             g[L.off_d2b + a] += d[a];
             for (int o = 0; o < 64; o++) g[L.off_d2w + a + o * 3] += d[a] * A.h1[o];
@@ -455,7 +504,7 @@ void orc_qnet_backward(int bs, int C, const float *p, int B, const double *x, co
         for (int o = 0; o < 64; o++) {
             double s = 0;
             for (int a = 0; a < 3; a++) s += d[a] * (double)p[L.off_d2w + a + o * 3];
-            dh1[o] = A.h1[o] > 0 ? s : 0;
+            dh1[o] = A.m[oh + o] ? s : 0;
         }
         memset(da3, 0, sizeof(double) * L.F1);
         for (int o = 0; o < 64; o++) {
@@ -466,19 +515,24 @@ void orc_qnet_backward(int bs, int C, const float *p, int B, const double *x, co
                 da3[f] += dh1[o] * (double)p[L.off_d1w + o + f * 64];
             }
         }
-        conv_bwd(bs, 32, 64, 6, 0, p + L.off_w3, A.a2, A.a3, da3, g + L.off_w3, g + L.off_b3, da2);
-        conv_bwd(bs, 16, 32, 3, 1, p + L.off_w2, A.a1, A.a2, da2, g + L.off_w2, g + L.off_b2, da1);
-        conv_bwd(bs, C, 16, 3, 1, p + L.off_w1, xb, A.a1, da1, g + L.off_w1, g + L.off_b1, NULL);
+        conv_bwd_k(bs, 32, 64, 6, 0, p + L.off_w3, A.a2, A.m + o3, A.a3, da3, g + L.off_w3, g + L.off_b3, da2);
+        conv_bwd_k(bs, 16, 32, 3, 1, p + L.off_w2, A.a1, A.m + o2, A.a2, da2, g + L.off_w2, g + L.off_b2, da1);
+        conv_bwd_k(bs, C, 16, 3, 1, p + L.off_w1, xb, A.m, A.a1, da1, g + L.off_w1, g + L.off_b1, NULL);
     }
     free(dh1); free(da3); free(da2); free(da1);
     acts_free(&A);
 }
 
+void orc_qnet_backward(int bs, int C, const float *p, int B, const double *x, const double *dq, double *g) {
+    orc_qnet_backward_ex(bs, C, p, B, x, dq, g, NULL, NULL, NULL);
+}
+
 /* utils.jl:448-464: q_next = t_net(s'); q_next[mask] = -100; max; target =
  * r + 0.97*max*(1-done) (Float64); loss = huber(Q(s)[a], target; delta=1, mean). */
-double orc_dqn_loss_grad(int bs, int C, const float *qp, const float *tp, int B, const double *s,
-                         const int32_t *a_idx, const float *r, const double *s_next, const uint8_t *done,
-                         const uint8_t *mask3, double gamma, double *grad, double *target_out) {
+double orc_dqn_loss_grad_ex(int bs, int C, const float *qp, const float *tp, int B, const double *s,
+                            const int32_t *a_idx, const float *r, const double *s_next, const uint8_t *done,
+                            const uint8_t *mask3, double gamma, double *grad, double *target_out,
+                            const uint8_t *relu_in, uint8_t *relu_out, double *margin_out) {
     double *qn = (double *)malloc(sizeof(double) * 3 * B);
     double *qs = (double *)malloc(sizeof(double) * 3 * B);
     double *dq = (double *)calloc((size_t)3 * B, sizeof(double));
@@ -499,9 +553,15 @@ double orc_dqn_loss_grad(int bs, int C, const float *qp, const float *tp, int B,
         dq[3 * b + a_idx[b]] = (ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / B;
     }
     loss /= B;
-    if (grad) orc_qnet_backward(bs, C, qp, B, s, dq, grad);
+    if (grad) orc_qnet_backward_ex(bs, C, qp, B, s, dq, grad, relu_in, relu_out, margin_out);
     free(qn); free(qs); free(dq);
     return loss;
+}
+double orc_dqn_loss_grad(int bs, int C, const float *qp, const float *tp, int B, const double *s,
+                         const int32_t *a_idx, const float *r, const double *s_next, const uint8_t *done,
+                         const uint8_t *mask3, double gamma, double *grad, double *target_out) {
+    return orc_dqn_loss_grad_ex(bs, C, qp, tp, B, s, a_idx, r, s_next, done, mask3, gamma, grad, target_out,
+                                NULL, NULL, NULL);
 }
 
 /* ======================= deeper bf16 Q-net (configs[2]) =====================

@@ -99,6 +99,17 @@ double orc_dqn_loss_grad(int bs, int C, const float *q_params, const float *t_pa
                          const double *s, const int32_t *a_idx, const float *r,
                          const double *s_next, const uint8_t *done, const uint8_t *mask3,
                          double gamma, double *grad, double *target_out);
+/* kink-aware variants (test infrastructure): relu decisions per sample
+ * [B][orc_qnet_relu_count] = a1 | a2 | a3 (channel-major) | h1; relu_in NULL =
+ * the reference's z > 0; relu_out / margin_out (z / sum|terms|) may be NULL */
+int64_t orc_qnet_relu_count(int bs, int C);
+void orc_qnet_backward_ex(int bs, int C, const float *params, int B, const double *x, const double *dq,
+                          double *grad, const uint8_t *relu_in, uint8_t *relu_out, double *margin_out);
+double orc_dqn_loss_grad_ex(int bs, int C, const float *q_params, const float *t_params, int B,
+                            const double *s, const int32_t *a_idx, const float *r,
+                            const double *s_next, const uint8_t *done, const uint8_t *mask3,
+                            double gamma, double *grad, double *target_out,
+                            const uint8_t *relu_in, uint8_t *relu_out, double *margin_out);
 /* ---- deeper bf16 Q-net (BASELINE configs[2], builder-defined; see the .c) -- */
 int64_t orc_deep_nparams(int bs, int C);
 void orc_deep_forward(int bs, int C, const float *params, int B, const double *x, double *q);

@@ -69,6 +69,7 @@ class OracleEpisodeLoop:
         C = self.C
         loss, g, _ = oracle.dqn_loss_grad(self.bs, C, self.th, self.tt, f[:, :C], self.act[ids], self.rew[ids],
                                           f[:, 1:], self.done[ids], self.mask[ids], self.gamma)
+        self.last_grad, self.last_ids = g, ids
         self.th, self.acc = oracle.rmsprop(self.th, self.acc, g.astype(np.float32))
         if nb % self.rate == 0:
             self.tt = self.th.copy()

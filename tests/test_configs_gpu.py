@@ -233,3 +233,63 @@ def test_compute_D_episode_schedule_vs_oracle(snk):
     print(f"compute_D: rel err {err:.2e} (train! phase: {err_wrong:.2e})")
     assert err <= 5e-3 and err_wrong > 10 * err
     assert np.linalg.norm(lap.mean() - mref) <= 5e-5 * np.linalg.norm(mref)
+
+
+def test_compute_D_teacher_forced_vs_oracle(snk):
+    """compute_D.jl:33-142 (episode schedule, nb from 1) teacher-forced, update
+    by update: before every update nb the oracle replica takes the device's
+    q_net, t_net and RMSProp state, plays the same episode (counter-RNG
+    decisions; greedy ones from its own fp64 forward of the device q_net),
+    draws the same batch and computes the loss and gradient. Per update:
+    episode reward bit-exact, loss within rel 1e-5, gradient normwise 1e-5,
+    (q_net, accumulator) after the update bit-exact with Float32 RMSProp of
+    the device gradient, t_net == q_net exactly when nb % rate == 0 (else
+    unchanged). The K = 6 snapshot columns are the device q_net before updates
+    nb = 8, 12, ..., 28 bit for bit: the Welford mean/var and centred D equal
+    the oracle's over those columns bit for bit. 10x10, 2 frames, capacity
+    300, rate 3, epsilon 1 -> 0.4 (decay 0.025) so greedy decisions appear."""
+    from oracle_loops import OracleEpisodeLoop
+    bs, C, cap, seed, rate = 10, 2, 300, 0xD00D, 3
+    K, thin, burn_in = 6, 4, 8
+    tr = snk.Trainer(n_envs=1, board_size=bs, n_frames=C, capacity=cap, target_update_rate=rate, seed=seed,
+                     epsilon=1.0, epsilon_end=0.4, decay=0.025, n_batches=1000)
+    m = tr.model
+    th0 = m.get_params()
+    ol = OracleEpisodeLoop(bs, C, cap, seed, th0, rate=rate, epsilon=1.0, epsilon_end=0.4, decay=0.025)
+    state = {"th": th0, "acc": np.zeros_like(th0), "tt": th0.copy(), "filled": False}
+    after = {}                                   # nb -> device q_net after update nb
+
+    def on_update(nb, loss):
+        if not state["filled"]:                  # the device filled before update 1: follow it
+            ol.fill()
+            state["filled"] = True
+        ol.th, ol.acc, ol.tt = state["th"].copy(), state["acc"].copy(), state["tt"].copy()
+        ep_o, l_o = ol.step(nb)
+        g = m.grad
+        th, acc, tt = m.get_params(), m.get_params(snk.SNK_NET_OPT_STATE), m.get_params(snk.SNK_NET_TARGET)
+        assert abs(loss - l_o) <= 1e-5 * abs(l_o), (nb, loss, l_o)
+        assert np.linalg.norm(g - ol.last_grad) <= 1e-5 * np.linalg.norm(ol.last_grad), nb
+        th_ref, acc_ref = oracle.rmsprop(state["th"], state["acc"], g)
+        assert np.array_equal(th, th_ref) and np.array_equal(acc, acc_ref), nb
+        assert np.array_equal(tt, th if nb % rate == 0 else state["tt"]), nb
+        assert np.float32(tr.epsilon) == ol.eps, nb
+        state.update(th=th, acc=acc, tt=tt)
+        after[nb] = th
+
+    lap = snk.compute_D(tr, K=K, thin=thin, burn_in=burn_in, on_update=on_update)
+    snaps = [burn_in + thin * p for p in range(K)]
+    assert sorted(after) == list(range(1, snaps[-1])), "updates nb = 1 .. 27 (none at the K-th snapshot)"
+    cols = np.stack([after[nb - 1].astype(np.float64) for nb in snaps])
+    Dref, mref, vref = oracle.welford_center(cols)
+    assert np.array_equal(lap.D(), Dref) and np.array_equal(lap.mean(), mref) and np.array_equal(lap.var(), vref)
+    assert ol.n_greedy > 0
+    print(f"compute_D teacher-forced: {len(after)} updates, {ol.n_greedy} greedy oracle decisions")
+
+
+def test_compute_D_stops_at_n_batches(snk):
+    """compute_D.jl:58 `while nb <= n_batches`: when the K-th column would fall
+    after n_batches, the loop runs updates 1..n_batches and returns nothing."""
+    tr = snk.Trainer(n_envs=1, board_size=10, n_frames=2, capacity=200, seed=3, n_batches=9)
+    losses = []
+    out = snk.compute_D(tr, K=3, thin=2, burn_in=6, on_update=lambda nb, loss: losses.append(nb))
+    assert out is None and losses == list(range(1, 10))

@@ -158,3 +158,27 @@ def test_configs2_act_forward_65536_envs(snk):
     ok = top[:, 2] - top[:, 1] > 1e-3
     ref_a = np.argmax(qref, axis=1)
     assert ok.sum() > 40 and np.array_equal(a[sel][ok], ref_a[ok])
+
+
+def test_deep_net_refused_by_jacobian_and_laplace_sampling(snk):
+    """The per-sample Jacobian, the Jacobian Gram and laplace_sampling! run the
+    reference architecture's kernels: a deeper-net handle is refused with
+    SnakeHipError (no fault, no silent wrong answer)."""
+    m = snk.DQNModel(12, 3, n_frames=2, seed=3, deep=True)
+    rb = snk.ReplayBuffer(256, board_size=12, n_frames=2, batch_size=64)
+    g = snk.SnakeGame(12, 2, n_envs=64, autoreset=True)
+    act = snk.DeviceArray(64, np.uint8)
+    for _ in range(4):
+        snk.synth_actions_dev(g, 1, act)
+        snk.step_indices_dev(g, act.ptr, replay=rb)
+    with pytest.raises(snk.SnakeHipError, match="deep"):
+        snk.jacobian(m, rb, 8)
+    with pytest.raises(snk.SnakeHipError, match="deep"):
+        snk.jacobian_gram(m, rb, 128)
+    lap = snk.LaplaceD(m.P, 3)
+    for k in range(3):
+        lap.snapshot(m, k)
+    lap.fit_center()
+    tr = snk.Trainer(n_envs=64, board_size=12, n_frames=2, capacity=256, model=m, seed=3)
+    with pytest.raises(snk.SnakeHipError, match="deep"):
+        snk.laplace_sampling_(tr, lap, n_models=4)

@@ -49,6 +49,7 @@ def test_play_episode_with_animation_on_device(snk, golden, tmp_path):
     exp, ep, hist = gif.play_episode_with_animation(fx["act_idx"], model=m, gif_name="double3",
                                                     path=str(tmp_path))
     assert np.array_equal(hist, fx["boards_cells"]) and ep == np.float32(29.969957)
+    assert exp["score"] == 33                              # README.md:54-58, the device's game.score
     assert np.array_equal(to_cells(decode_gif(str(tmp_path / "double3.gif"))), fx["boards_cells"])
     score, _, h2 = gif.play_best_game(m, name="greedy", path=str(tmp_path))
     assert h2.shape[1] == 100 and os.path.exists(tmp_path / "greedy.gif") and score >= 0

@@ -80,6 +80,43 @@ def test_gram_vs_oracle(snk, K, P):
     assert lam.size > 0 and np.all(lam > 0)
 
 
+def test_gram_reference_scale_entrywise(snk):
+    """plot_traj.jl:10-16 at compute_D.jl's own size: K = 1000 snapshots of
+    the 12x12 net (P = 279,699). The snapshots are a training-like
+    trajectory (a random walk around theta_0 plus per-snapshot jitter), so the
+    centred Gram has large off-diagonal entries of both signs. Checked against
+    fp64 Dc Dc' of the oracle's centred D (itself bit-exact with the device's):
+    every entry |G - G_ref| <= 1e-5 sqrt(G_ii G_jj), and every entry with
+    |G_ref| >= 0.01 sqrt(G_ii G_jj) also relative <= 1e-5."""
+    K, P = 1000, 279_699
+    rng = np.random.default_rng(1000)
+    D0 = rng.standard_normal((K, P), dtype=np.float32).astype(np.float64)
+    D0 *= 2e-4
+    np.cumsum(D0, axis=0, out=D0)                                  # the walk
+    D0 += rng.standard_normal((K, P), dtype=np.float32) * 1e-4     # jitter
+    D0 += rng.standard_normal(P, dtype=np.float32)[None, :] * 0.05  # theta_0
+    lap = snk.LaplaceD(P, K)
+    for k in range(K):
+        lap.set_column(k, D0[k])
+    lap.fit_center()
+    G, ms = lap.gram()
+    Dc, _, _ = oracle.welford_center(D0)
+    del D0
+    assert np.array_equal(lap.D(), Dc)
+    Gref = Dc @ Dc.T
+    d = np.sqrt(np.diag(Gref))
+    scale = np.outer(d, d)
+    err = np.abs(G - Gref)
+    big = np.abs(Gref) >= 0.01 * scale
+    rel = err[big] / np.abs(Gref[big])
+    print(f"D'D K={K} P={P}: max normalised err {float((err / scale).max()):.2e}; {int(big.sum())} of {K * K} "
+          f"entries >= 0.01 sqrt(GiiGjj): max rel {rel.max():.2e}, median {np.median(rel):.2e}; "
+          f"{int((Gref < 0).sum())} negative; kernel {ms:.2f} ms")
+    assert np.array_equal(G, G.T)
+    assert float((err / scale).max()) <= 1e-5
+    assert big.sum() > K * K // 2 and (Gref[big] < 0).sum() > 1000 and rel.max() <= 1e-5
+
+
 def test_gram_matches_restated_oracle_small(snk):
     rng = np.random.default_rng(1)
     D0 = rng.standard_normal((20, 333))

@@ -17,6 +17,7 @@ import pytest
 
 import oracle
 from devrng import TRAINER_SAMPLE_SALT, explore, first_argmax, floyd
+from kinks import grad_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -189,3 +190,139 @@ def test_trainer_graph_survives_workspace_growth(snk):
         tr.run(3)
         outs.append((tr.model.get_params(), tr.losses))
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_bench_graph_trajectory_vs_oracle(snk):
+    """The graph bench.py times, replayed on the oracle update by update
+    (utils.jl:434-482): 4096 lockstep 12x12 games, 2 frames, B = 64, capacity
+    50,000, graph_unroll 8, so each snk_trainer_run(8) is ONE captured graph of
+    8 iterations of conv_h3f_kernel act forward (>= 1024 states) + the
+    wmax_scan sample rider, env_step_kernel with store!, upd_fwd_kernel<12,2>
+    update forward, the backward kernels and grad_update_kernel. epsilon 1 (no
+    decay) in the checked window, so every action is the restated counter
+    stream (the 4096-state greedy forward is test_configs1_act_forward_4096_vs_oracle).
+    Target sync every 5 updates (nb = 0, 5, 10, 15) to put syncs inside graphs.
+    The trainer's gradient trace (snk_trainer_set_trace: one device copy of
+    each update's finished gradient, appended to the same graph) makes the
+    8 updates inside a graph observable.
+
+    After the fill (13 iterations) and after each of 2 graphs (16 updates,
+    the replay ring wrapping past 50,000):
+      boards, the last iteration's outputs and actions          bit-exact
+      replay ring (all 50,000 slots) at the end                 bit-exact
+      every update, teacher-forced: the oracle takes the device's q_net,
+        t_net and accumulator before the update (start of the graph,
+        then RMSProp of the traced device gradients) and the Floyd draw
+          loss (tr.losses)                                      relative 1e-5
+          gradient                                              normwise 1e-5, kink-aware
+            (tests/kinks.py: a relu decision at z within fp32 rounding of 0 may go
+            either way; such an update is re-run on the device, and the oracle under
+            the device's decisions must then agree, every differing decision at a kink)
+      q_net, accumulator, t_net after each graph == Float32 RMSProp of the
+        8 traced gradients from the graph-start state, t_net synced after
+        nb % 5 == 0                                             bit-exact
+    """
+    from devrng import rng_hash
+    bs, C, n, cap, B, rate, seed, U = 12, 2, 4096, 50_000, 64, 5, 0xBE4C, 8
+    tr = snk.Trainer(n_envs=n, board_size=bs, n_frames=C, capacity=cap, batch_size=B, n_batches=10_000,
+                     target_update_rate=rate, epsilon=1.0, epsilon_end=1.0, decay=0.0, seed=seed, graph_unroll=U)
+    m = tr.model
+    P = m.P
+    perm = m.flux_index()
+    ring = snk.DeviceArray((U, P), np.float32)
+    from snake_amd import _lib
+    act_ptr = _lib.vp()
+    _lib.call("snk_trainer_act_ptr", tr.handle, _lib.C.byref(act_ptr))
+    ob = oracle.OracleBatch(n, bs, C)
+    nc = bs * bs
+    frames = np.zeros((cap, C + 1, nc), np.int8)
+    o_act = np.zeros(cap, np.int32)
+    o_rew = np.zeros(cap, np.float32)
+    o_done = np.zeros(cap, np.uint8)
+    o_mask = np.zeros((cap, 3), np.uint8)
+    count, t = 0, 0
+    sseed = seed ^ TRAINER_SAMPLE_SALT
+    salt = seed ^ 0xA5A5A5A5A5A5A5A5
+
+    def oracle_iteration():
+        nonlocal count, t
+        a = np.array([(rng_hash(salt, e, t) >> 32) % 3 for e in range(n)], np.uint8)   # explore() at eps = 1
+        out = ob.step(a)
+        k = (count + np.arange(n)) % cap
+        frames[k], o_act[k], o_rew[k], o_done[k], o_mask[k] = out["frames"], a, out["reward"], out["done"], out["mask"]
+        count += n
+        t += 1
+        return a, out
+
+    def check_env(a, out):
+        got = np.zeros(n, np.uint8)
+        _lib.call("snk_memcpy_d2h", got.ctypes.data_as(_lib.vp), act_ptr, n)
+        assert np.array_equal(got, a), t
+        o = tr.game.last("reward", "done", "mask")
+        assert np.array_equal(o["reward"], out["reward"]) and np.array_equal(o["done"], out["done"]), t
+        assert np.array_equal(o["mask"], out["mask"] @ np.array([1, 2, 4], np.uint8)), t
+        assert np.array_equal(tr.game.board_cells(), ob.boards()), t
+
+    snk.fill_buffer_(tr)                                   # 13 iterations: one 8-graph + 5 single graphs
+    for _ in range(13):
+        a, out = oracle_iteration()
+    check_env(a, out)
+    assert len(tr.buffer) == cap and count == 13 * n
+
+    tr.set_trace(ring)
+    u = 0
+    worst_loss = worst_grad = 0.0
+    kinks = 0
+
+    def save_state():                                      # the graph-end state, restored after a kink replay
+        keep = [(w, m.get_params(w)) for w in (snk.SNK_NET_Q, snk.SNK_NET_TARGET, snk.SNK_NET_OPT_STATE)]
+
+        def put():
+            for w, v in keep:
+                m.set_params(v, w)
+        return put
+
+    for graph in range(2):
+        th = m.get_params()
+        acc = m.get_params(snk.SNK_NET_OPT_STATE)
+        tt = m.get_params(snk.SNK_NET_TARGET)
+        draws = []
+        for _ in range(U):
+            a, out = oracle_iteration()
+            f_ids = floyd(sseed, u + len(draws), min(count, cap), B)
+            draws.append((f_ids, frames[f_ids].copy(), o_act[f_ids].copy(), o_rew[f_ids].copy(),
+                          o_done[f_ids].copy(), o_mask[f_ids].copy()))
+        tr.run(U, learn=True, graph=True)                 # ONE replay of the captured 8-iteration graph
+        check_env(a, out)
+        losses = tr.losses[u:u + U]
+        gdev = np.empty((U, P), np.float32)
+        gdev[:, perm] = ring.numpy()
+        for k, (ids, f, ac, rw, dn, mk) in enumerate(draws):
+            ref = oracle.dqn_loss_grad_kinks(bs, C, th, tt, f[:, :C], ac, rw, f[:, 1:], dn, mk)
+            rl = abs(losses[k] - ref[0]) / abs(ref[0])
+            assert rl <= 1e-5, (u, losses[k], ref[0])
+            rg, rk, nk = grad_parity(snk, m, bs, C, th, tt, (f, ac, rw, dn, mk), gdev[k], restore=save_state,
+                                     ref=ref)
+            worst_loss, worst_grad = max(worst_loss, rl), max(worst_grad, rk)
+            kinks += nk
+            if nk:
+                print(f"update {u}: gradient {rg:.2e} vs the oracle's relu decisions, {rk:.2e} under the device's "
+                      f"({nk} kink decision(s))")
+            th, acc = oracle.rmsprop(th, acc, gdev[k])
+            if u % rate == 0:
+                tt = th.copy()
+            u += 1
+        assert np.array_equal(m.get_params(), th), graph
+        assert np.array_equal(m.get_params(snk.SNK_NET_OPT_STATE), acc), graph
+        assert np.array_equal(m.get_params(snk.SNK_NET_TARGET), tt), graph
+    assert np.array_equal(m.get_params(snk.SNK_NET_TARGET), m.get_params())   # nb = 15 synced last
+    st = tr.stats()
+    assert st["updates"] == 16 and st["nb"] == 16 and st["env_steps"] == t * n
+    got = snk.stack_exp(tr.buffer, np.arange(cap))
+    assert np.array_equal(got["states"], frames[:, :C].astype(np.float32))
+    assert np.array_equal(got["next_states"], frames[:, 1:].astype(np.float32))
+    assert np.array_equal(got["actions"], o_act + 1) and np.array_equal(got["rewards"], o_rew)
+    assert np.array_equal(got["dones"], o_done.astype(bool))
+    assert np.array_equal(got["suicidal_mask"], o_mask.astype(bool))
+    print(f"bench graph, 16 teacher-forced updates: loss rel max {worst_loss:.2e}, gradient max {worst_grad:.2e} "
+          f"({kinks} relu kink decision(s) accounted)")
