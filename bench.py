@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--updates-per-iter", type=int, default=1)
     p.add_argument("--epsilon", type=float, default=0.05)
     p.add_argument("--capacity", type=int, default=50000)
+    p.add_argument("--settle-ms", type=float, default=300.0,
+                   help="untimed iterations after the warm-up, for this long, before the timed windows")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip per-kernel timing")
@@ -105,7 +107,7 @@ def cpu_baseline(args) -> dict:
     t1, tn = np.zeros(4), np.zeros(4)
     v1 = L.cpuf_bench(n, bs, C, 1, 0, 1, args.updates_per_iter, args.capacity, food, len(food), t1)
     vn = L.cpuf_bench(n, bs, C, threads, 1, 3, args.updates_per_iter, args.capacity, food, len(food), tn)
-    ns, Kc = 2000, 9 * C * 16 + 16 + 4640 + 73792
+    ns, Kc = 6000, 9 * C * 16 + 16 + 4640 + 73792
     X = np.random.default_rng(0).standard_normal((ns, Kc)).astype(np.float32)
     G = np.zeros((ns, ns), np.float32)
     tg = L.cpuf_gram(ns, Kc, X, G, threads)
@@ -117,7 +119,13 @@ def cpu_baseline(args) -> dict:
                        f"update(s); {threads} threads: 3 iterations (fwd {tn[0]:.2f}s, step {tn[1]:.3f}s, "
                        f"update {tn[2]:.2f}s); 1 thread: 1 iteration (fwd {t1[0]:.2f}s, step {t1[1]:.3f}s, "
                        f"update {t1[2]:.2f}s)"),
-            "single_thread": {"value": v1, "cores": 1},
+            "cores_note": (f"the job's CPU share on the GPU box (OMP_NUM_THREADS = {threads}) of {os.cpu_count()} "
+                           f"host CPUs shared with other jobs"),
+            "env_steps_per_s_step_only": n * 3 / max(tn[1], 1e-12),
+            "updates_per_s": 3 * args.updates_per_iter / max(tn[2], 1e-12),
+            "act_forward_states_per_s": n * 3 / max(tn[0], 1e-12),
+            "single_thread": {"value": v1, "cores": 1, "env_steps_per_s_step_only": n / max(t1[1], 1e-12),
+                              "updates_per_s": args.updates_per_iter / max(t1[2], 1e-12)},
             "d_build_gram_sec_extrapolated": tg * (N * (N + 1.0)) / (ns * (ns + 1.0)),
             "d_build_gram_sample": f"G = X X' of {ns} rows x {Kc} conv columns in {tg:.2f}s on {threads} threads "
                                    f"({2.0 * ns * (ns + 1) / 2 * Kc / tg / 1e9:.0f} GFLOP/s), scaled by the "
@@ -422,6 +430,14 @@ def main():
     graph = not args.no_graph
     snk.fill_buffer_(tr, graph=graph)                    # fill_buffer!: untimed
     tr.run(args.warmup, learn=True, graph=graph)
+    # untimed settle: the driver's windows fell monotonically after 5 warm-up steps (the
+    # device's clocks still ramping), so keep iterating for args.settle_ms before timing
+    _lib.call("snk_synchronize")
+    t_settle, settle_iters = time.perf_counter(), 0
+    while time.perf_counter() - t_settle < args.settle_ms / 1e3:
+        tr.run(8, learn=True, graph=graph)
+        _lib.call("snk_synchronize")
+        settle_iters += 8
 
     def barrier():
         _lib.call("snk_synchronize")
@@ -460,6 +476,9 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "windows_ms": [1000.0 * w for w in windows],
+        "windows_spread": (max(windows) - min(windows)) / elapsed,
+        "settle": {"iterations": settle_iters, "ms": args.settle_ms,
+                   "note": "untimed trainer iterations after the warm-up, before the timed windows"},
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

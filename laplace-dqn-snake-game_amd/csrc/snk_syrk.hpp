@@ -337,6 +337,7 @@ struct SyrkArgs {
     const uint16_t *xh, *xl;
     const int32_t *xe;
     int64_t ldh;
+    int direct;              // tiles[] is indexed by blockIdx.x itself (a per-XCD table: syrk_xcd_table)
 };
 
 // h3 operands for the Gram (snk_conv_h3.hpp's split, one scale per ROW):
@@ -391,7 +392,10 @@ __device__ __forceinline__ constexpr int waitcnt_vm(int n) { return (n & 15) | (
 
 // NW waves: 8 (two per SIMD, 64 x 32 per wave) or 4 (one per SIMD, 64 x 64 per wave:
 // half the fragment reads per MFMA)
-template <int NW>
+// VAR (measurement builds selected by SNK_SYRK_VAR): 0 the kernel, 1 no MFMA (the
+// fragments feed one VALU op each: data movement + LDS reads + barriers alone),
+// 2 no stage DMA after the prologue (MFMAs + fragment reads + barriers alone)
+template <int NW, int VAR = 0>
 __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
     constexpr int NC = NW == 4 ? 2 : 1, NJ = 32 / NW;   // column tiles per wave, DMA jobs per wave and stage
     __shared__ __attribute__((aligned(16))) uint16_t lds[SH_BUF * 2 * 2 * SY_T * SH_ROW];   // 128 KB
@@ -425,6 +429,7 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
         ddst[q] = ((op * 2 + pl) * SY_T + rb * 16) * SH_ROW;
     }
     auto dma = [&](int st, int buf) {
+        if (VAR == 2 && st > 2) return;
         const int64_t k = (int64_t)min(st, nst - 1) * 2 * SY_KS;   // past the end: harmless reloads
 #pragma unroll
         for (int q = 0; q < NJ; ++q)
@@ -468,9 +473,18 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
     // the six MFMAs of one k-step, split after the first: the next fragments'
     // ds_reads go out between the two parts (see step)
     auto mfma_first = [&](const Frag &f) {
+        if (VAR == 1) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NC; ++j)
+                    acc[i][j][0] += (float)(f.a[i][0][0] * f.b[j][0][0]) + (float)(f.a[i][1][1] * f.b[j][1][1]);
+            return;
+        }
         acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[0][1], f.b[0][0], acc[0][0], 0, 0, 0);
     };
     auto mfma_rest = [&](const Frag &f) {
+        if (VAR == 1) return;
 #pragma unroll
         for (int j = 0; j < NC; ++j)
 #pragma unroll
@@ -555,6 +569,203 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
                 const int row = bi * SY_T + wr + mi * 32 + acc_row(g, lane);
                 if (row >= N) continue;
                 a.g32[(int64_t)row * a.ldg + col] = (float)__builtin_ldexp(accd[mi][j][g], -(a.xe[row] + a.xe[col]));
+            }
+        }
+}
+
+// syrk_h3q_kernel: syrk_h3_kernel's tile, waves, stages and LDS-DMA ring on
+// v_mfma_f32_16x16x32_f16 (one MFMA per 32-k stage and 16 x 16 tile; at equal
+// cycles per FLOP the 16 x 16 shape holds a higher clock under load,
+// MI355X_MICROARCH.md 'DVFS give-back' (7)). Wave w owns rows 64 (w / 4) ..
+// +63 and columns 32 (w % 4) .. +31: 4 x 2 tiles of 16 x 16, the same LDS bytes
+// per wave as the 32 x 32 form. A fragment is a 16-row x 32-k slice: lane l
+// reads row (l & 15), 16-byte chunk (l >> 4) of the stage. The chunk of row r is
+// stored at slot chunk ^ swz(r), swz(r) = (-(r >> 2)) & 3, which puts every
+// ds_read_b128 lane group of that pattern on 16 distinct bank quads.
+// Per step: see `step` below (row tiles 2-3 of a stage are read during the
+// MFMAs of tiles 0-1, the next stage's tiles 0-1 and B during those of 2-3).
+__device__ __forceinline__ int syrk_swz16(int row) { return (-(row >> 2)) & 3; }
+
+// NB stage buffers (32 KB each): NB - 1 stages in flight
+template <int VAR = 0, int NB = 4>
+__global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
+    constexpr int NJ = 4;   // DMA jobs per wave and stage (32 KB / 8 waves / 1 KB)
+    __shared__ __attribute__((aligned(16))) uint16_t lds[NB * 2 * 2 * SY_T * SH_ROW];
+    int bi, bj;
+    {
+        const int64_t t = a.direct ? (int64_t)blockIdx.x : a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
+        if (a.tiles) {
+            const int2 tb = a.tiles[t];
+            bi = tb.x;
+            bj = tb.y;
+        } else {
+            syrk_tile(t, bi, bj);
+        }
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int wr = (wave >> 2) * 64, wc = (wave & 3) * 32;
+    const int N = a.N;
+    const int nst = (int)(a.ldh / SY_KS);
+    // this wave's NJ DMA jobs per stage: j = NJ * wave + q -> operand j >> 4, plane
+    // (j >> 3) & 1, 16-row block j & 7; operand and plane are the wave's, the row
+    // blocks consecutive, and the swizzle of row 16 rb + (lane >> 2) does not depend
+    // on rb: one source pointer per lane. Rows past N exist (the planes are zero-padded
+    // to whole SW_ROWS_B blocks) and are never stored.
+    const uint16_t *dsrc;
+    int ddst;
+    {
+        const int j = NJ * wave, op = j >> 4, pl = (j >> 3) & 1, rb = j & 7;
+        const int row = rb * 16 + (lane >> 2);
+        const int chunk = (lane & 3) ^ syrk_swz16(row);
+        dsrc = a.xh + (int64_t)((op ? bj : bi) * SY_T + row) * 2 * a.ldh + pl * SY_KS + chunk * 8;
+        ddst = ((op * 2 + pl) * SY_T + rb * 16) * SH_ROW;
+    }
+    const int64_t qstride = 16 * 2 * a.ldh;
+    auto dma = [&](int st, int buf) {
+        if (VAR == 2 && st > NB - 2) return;
+        const int64_t k = (int64_t)min(st, nst - 1) * 2 * SY_KS;
+#pragma unroll
+        for (int q = 0; q < NJ; ++q)
+            __builtin_amdgcn_global_load_lds((const void *)(dsrc + k + q * qstride),
+                                             (__attribute__((address_space(3))) void *)(lds + buf * (4 * SY_T * SH_ROW) + ddst +
+                                                                                       q * 16 * SH_ROW),
+                                             16, 0, 0);
+    };
+    // fragments: A row tiles 0-1 (lo) and 2-3 (hi), B column tiles 0-1 twice (this
+    // stage's and the next's): [tile][plane]
+    typedef f16x8 FA[2][2];
+    typedef f16x8 FB[2][2];
+    auto frag_a = [&](int buf, int t0, FA &f) {
+        const uint16_t *base = lds + buf * (4 * SY_T * SH_ROW);
+#pragma unroll
+        for (int pn = 0; pn < 2; ++pn)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = wr + 16 * (t0 + i) + r;
+                f[i][pn] = as_h(*reinterpret_cast<const u32x4 *>(
+                    base + ((0 * 2 + pn) * SY_T + row) * SH_ROW + 8 * (g ^ syrk_swz16(row))));
+            }
+    };
+    auto frag_b = [&](int buf, FB &f) {
+        const uint16_t *base = lds + buf * (4 * SY_T * SH_ROW);
+#pragma unroll
+        for (int pn = 0; pn < 2; ++pn)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = wc + 16 * j + r;
+                f[j][pn] = as_h(*reinterpret_cast<const u32x4 *>(
+                    base + ((1 * 2 + pn) * SY_T + row) * SH_ROW + 8 * (g ^ syrk_swz16(row))));
+            }
+    };
+    f32x4 acc[4][2];
+    double accd[4][2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                acc[i][j][e] = 0.0f;
+                accd[i][j][e] = 0.0;
+            }
+    // half of a stage's 24 MFMAs: row tiles t0, t0+1 x both column tiles; per
+    // tile pair l*h, h*l, then h*h (small products first)
+    // part 0: only the first MFMA (tile t0 x column 0, l*h); part 1: the other 11;
+    // part 2: all 12
+    auto mfma_half = [&](const FA &fa, const FB &fb, int t0, int part) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int i = t0 + ii;
+                const bool first = ii == 0 && j == 0;
+                if (VAR == 1) {
+                    if (part != 0 && (part == 2 || !first))
+                        acc[i][j][0] += (float)(fa[ii][0][0] * fb[j][0][0]) + (float)(fa[ii][1][1] * fb[j][1][1]);
+                    continue;
+                }
+                if (part == 2 || (part == 0) == first)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][1], fb[j][0], acc[i][j], 0, 0, 0);
+                if (part != 0) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][0], fb[j][1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][0], fb[j][0], acc[i][j], 0, 0, 0);
+                }
+            }
+    };
+    auto flush = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    accd[i][j][e] += (double)acc[i][j][e];
+                    acc[i][j][e] = 0.0f;
+                }
+    };
+#pragma unroll
+    for (int q = 0; q < NB - 1; ++q) dma(q, q);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    FA lo, hi;
+    FB b0, b1;
+    frag_a(0, 0, lo);
+    frag_b(0, b0);
+    // step st (buffer B = st % NB; lo / bc hold stage st's row tiles 0-1 and B):
+    // read stage st's row tiles 2-3, MFMAs of tiles 0-1, DMA of stage st+NB-1 (into
+    // the buffer of stage st-1, whose last readers passed step st-1's barrier),
+    // wait for stage st+1 and the barrier, read stage st+1's tiles 0-1 and B
+    // (lo is free now), MFMAs of tiles 2-3
+    auto step = [&](int st, auto bc_, FB &bc, FB &bn) {
+        constexpr int B = decltype(bc_)::value;
+        // the compiler's waitcnt pass drains lgkmcnt to 0 before the first MFMA of
+        // the step: issue the row-tile 2-3 reads after it
+        mfma_half(lo, bc, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_a(B, 2, hi);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_half(lo, bc, 0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        dma(st + NB - 1, (B + NB - 1) % NB);
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));   // my part of stage st+1 landed
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        frag_a((B + 1) % NB, 0, lo);
+        frag_b((B + 1) % NB, bn);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_half(hi, bc, 2, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st % SY_FLUSH == SY_FLUSH - 1) flush();
+    };
+    // U = lcm(NB, 2) steps per loop trip: buffer and B-fragment roles are constants
+    constexpr int U = NB % 2 ? 2 * NB : NB;
+    auto trip = [&](int st0, bool tail) {
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+            ((!tail || st0 + I < nst
+                  ? step(st0 + I, std::integral_constant<int, I % NB>{}, I % 2 ? b1 : b0, I % 2 ? b0 : b1)
+                  : void()),
+             ...);
+        }(std::make_integer_sequence<int, U>{});
+    };
+    int st = 0;
+    for (; st + U <= nst; st += U) trip(st, false);
+    if (st < nst) trip(st, true);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    flush();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = bj * SY_T + wc + 16 * j + r;
+            if (col >= N) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = bi * SY_T + wr + 16 * i + 4 * g + e;
+                if (row >= N) continue;
+                a.g32[(int64_t)row * a.ldg + col] = (float)__builtin_ldexp(accd[i][j][e], -(a.xe[row] + a.xe[col]));
             }
         }
 }
