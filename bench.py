@@ -326,20 +326,23 @@ def d_build_gram(args, snk, model, dist, rank, world) -> dict:
                                     "conv_gram": ms[2], "dense_terms_and_mirror": ms[3]},
                        "naive_flop": 2.0 * n * n * model.P, "executed_gram_flop_this_rank": flop_gram,
                        "roofline": {"bound": "mfma",
-                                    "kernel": "h3_rows_kernel + syrk_h3_kernel (fp16 h3 split, LDS-DMA staged), "
-                                              "conv-column Gram",
+                                    "kernel": "h3_rows_kernel + syrk_h3q_kernel (fp16 h3 split on "
+                                              "v_mfma_f32_16x16x32_f16, LDS-DMA staged), conv-column Gram",
                                     "achieved": tf, "peak": speak, "unit": "TFLOP/s (fp32-equivalent)",
                                     "frac": tf / speak, "avg_launch_ms": ms[2], "flop_per_launch": flop_gram,
                                     "traffic": None, "half_mfma_tflops_executed": tf * H3_PRODUCTS,
                                     "mfma_utilization": tf * H3_PRODUCTS / PEAK_BF16_TFLOPS,
                                     "fp32_mfma_peak": PEAK_FP32_TFLOPS}}}
-    tr_file = _latest_traffic("syrk_h3_kernel", "*_syrk_traffic.json") if n == 50000 and world == 1 else None
+    tr_file = _latest_traffic("syrk_h3q_kernel", "*_syrk_traffic.json") if n == 50000 and world == 1 else None
     if tr_file:
         rf = res["d_build"]["roofline"]
         rf["traffic"] = tr_file["bytes_per_launch"]
         rf["traffic_source"] = tr_file["source"]
         rf["traffic_note"] = ("L2-miss bytes (HBM + Infinity Cache) of the Gram launch; its unique operand bytes "
                               "are the n x Kc fp16 h/l row planes (4 B per entry) + the lower-triangle fp32 G")
+        uniq = 4.0 * n * ((Kc + 31) // 32 * 32) + 4.0 * n * (n + 1) / 2
+        rf["unique_operand_bytes"] = uniq
+        rf["traffic_over_unique"] = rf["traffic"] / uniq
     del G, rb
     return res
 

@@ -195,74 +195,6 @@ static std::vector<int2> syrk_tile_order_host(int N) {
     SNK_CHECK((int64_t)t.size() == (int64_t)T * (T + 1) / 2, SNK_ERR_INTERNAL, "syrk tile order");
     return t;
 }
-// The Gram's tiles as a table indexed by blockIdx.x for a one-shard launch (workgroup w
-// runs on XCD w % 8): the lower triangle is cut into super-blocks of SB x SB tiles, each
-// dealt to the 8 XCDs as 8 x 4 sub-blocks (rows (x % 2) * 8, columns (x / 2) * 4), and the
-// XCDs walk the super-blocks in the same order. An XCD's 32 CUs then share 12 row blocks
-// in its L2 (the 8 x 4 supertile of syrk_tile_order), and the 8 XCDs of a super-block
-// share its 2 SB row blocks in the Infinity Cache instead of streaming 8 disjoint sets
-// from HBM. Super-blocks whose tiles do not divide into 8 equal sub-blocks (diagonal and
-// edge) are split into 8 consecutive runs of equal length (+-1); the lists are balanced
-// to ceil((total - x) / 8) tiles at the end.
-static std::vector<int2> syrk_xcd_table_host(int N) {
-    const int T = (int)ceil_div(N, SY_T);
-    constexpr int SB = 16;
-    std::vector<std::vector<int2>> L(8);
-    for (int I0 = 0; I0 < T; I0 += SB)
-        for (int J0 = 0; J0 <= I0; J0 += SB) {
-            std::vector<int2> all;
-            bool even = true;
-            std::vector<std::vector<int2>> sub(8);
-            for (int x = 0; x < 8; ++x) {
-                for (int i = I0 + (x % 2) * 8; i < std::min(T, I0 + (x % 2) * 8 + 8); ++i)
-                    for (int j = J0 + (x / 2) * 4; j < std::min(J0 + (x / 2) * 4 + 4, i + 1); ++j) sub[x].push_back(int2{i, j});
-                if (sub[x].size() != sub[0].size()) even = false;
-                all.insert(all.end(), sub[x].begin(), sub[x].end());
-            }
-            if (even) {
-                for (int x = 0; x < 8; ++x) L[x].insert(L[x].end(), sub[x].begin(), sub[x].end());
-            } else {
-                const size_t n = all.size();
-                for (int x = 0; x < 8; ++x)
-                    L[x].insert(L[x].end(), all.begin() + n * x / 8, all.begin() + n * (x + 1) / 8);
-            }
-        }
-    const int64_t tot = (int64_t)T * (T + 1) / 2;
-    std::vector<int2> spill;
-    for (int x = 0; x < 8; ++x) {
-        const size_t want = (size_t)((tot - x + 7) / 8);
-        while (L[x].size() > want) {
-            spill.push_back(L[x].back());
-            L[x].pop_back();
-        }
-    }
-    for (int x = 0; x < 8; ++x) {
-        const size_t want = (size_t)((tot - x + 7) / 8);
-        while (L[x].size() < want) {
-            SNK_CHECK(!spill.empty(), SNK_ERR_INTERNAL, "syrk xcd table");
-            L[x].push_back(spill.back());
-            spill.pop_back();
-        }
-    }
-    std::vector<int2> t((size_t)tot);
-    for (int64_t w = 0; w < tot; ++w) t[(size_t)w] = L[w % 8][(size_t)(w / 8)];
-    return t;
-}
-static const int2 *syrk_xcd_table(int N) {
-    static std::mutex mu;
-    static std::vector<std::pair<std::pair<int, int>, int2 *>> cache;
-    int dev = 0;
-    SNK_HIP(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(mu);
-    for (auto &c : cache)
-        if (c.first.first == N && c.first.second == dev) return c.second;
-    const std::vector<int2> t = syrk_xcd_table_host(N);
-    int2 *d = nullptr;
-    SNK_HIP(hipMalloc(&d, t.size() * sizeof(int2)));
-    SNK_HIP(hipMemcpy(d, t.data(), t.size() * sizeof(int2), hipMemcpyHostToDevice));
-    cache.emplace_back(std::make_pair(N, dev), d);
-    return d;
-}
 static const int2 *syrk_tile_order(int N) {
     static std::mutex mu;
     static std::vector<std::pair<std::pair<int, int>, int2 *>> cache;   // (N, device) -> table
@@ -299,22 +231,14 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s, int r
     dim3 grid((unsigned)a.ntiles, (unsigned)z);
     if (a.xh) {   // pre-split rows (h3): fp16 parts, 3 products per fp32 product
         SNK_CHECK(out == SYRK_F32 && z == 1 && a.ldh % SY_KS == 0 && a.xe, SNK_ERR_INTERNAL, "syrk h3 arguments");
-        // SNK_SYRK=h3 (32x32x16, the round-2 kernel) | h3q (16x16x32); SNK_SYRK_VAR = 1 / 2:
-        // measurement builds without MFMAs / without stage DMAs (snk_syrk.hpp)
+        // production: syrk_h3q_kernel (v_mfma_f32_16x16x32_f16). Measurement builds:
+        // SNK_SYRK=h3 the round-2 32x32x16 kernel; SNK_SYRK_VAR = 1 / 2 without MFMAs /
+        // without stage DMAs (snk_syrk.hpp)
         static const char *kind = getenv("SNK_SYRK");
         static const int var = getenv("SNK_SYRK_VAR") ? atoi(getenv("SNK_SYRK_VAR")) : 0;
-        const bool q16 = kind && !strcmp(kind, "h3q");
-        static const int nbuf = getenv("SNK_SYRK_NB") ? atoi(getenv("SNK_SYRK_NB")) : 4;
-        static const bool xtab = getenv("SNK_SYRK_ORDER") && atoi(getenv("SNK_SYRK_ORDER")) == 2;
-        if (q16 && xtab && nranks == 1) {
-            a.tiles = syrk_xcd_table(a.N);
-            a.direct = 1;
-        }
-        if (q16) {
+        if (!(kind && !strcmp(kind, "h3"))) {
             if (var == 1) syrk_h3q_kernel<1><<<grid, 512, 0, s>>>(a);
             else if (var == 2) syrk_h3q_kernel<2><<<grid, 512, 0, s>>>(a);
-            else if (nbuf == 5) syrk_h3q_kernel<0, 5><<<grid, 512, 0, s>>>(a);
-            else if (nbuf == 3) syrk_h3q_kernel<0, 3><<<grid, 512, 0, s>>>(a);
             else syrk_h3q_kernel<0><<<grid, 512, 0, s>>>(a);
         } else {
             if (var == 1) syrk_h3_kernel<8, 1><<<grid, 512, 0, s>>>(a);

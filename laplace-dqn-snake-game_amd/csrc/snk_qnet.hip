@@ -1321,56 +1321,162 @@ struct UpdArgs {
 };
 
 
-// index of packed parameter i in the forward weight image, or -1; x6 = its
-// plane-0 index in the bf16 split image (planes CK*CN apart)
-template <int CK, int CN>
-__device__ __forceinline__ int64_t image_index_of(int64_t u, int64_t base, int64_t &x6, int &pstride) {
-    const int64_t kk = u / (CK * CN);
-    const int r = (int)(u - kk * CK * CN);
-    const int c = r / CN, n = r - c * CN;
-    x6 = 3 * base + kk * 3 * CK * CN + (int64_t)n * CK + c;
-    pstride = CK * CN;
-    return base + kk * CK * CN + (int64_t)n * CK + c;
-}
-__device__ __forceinline__ int64_t image_index(const QLayout &L, int64_t i, int64_t &x6, int &pstride) {
-    if (i >= L.off_w2 && i < L.off_b2) return image_index_of<16, 32>(i - L.off_w2, L.off_t2, x6, pstride);
-    if (i >= L.off_w3 && i < L.off_b3) return image_index_of<32, 64>(i - L.off_w3, L.off_t3, x6, pstride);
-    if (i >= L.off_d1w && i < L.off_d1b) return image_index_of<64, 64>(i - L.off_d1w, L.off_td, x6, pstride);
-    return -1;
+// the finished gradient of packed parameter i: the sum of its K-split slabs
+// (slab_reduce order, z ascending; eight loads in flight) or the value already there
+__device__ __forceinline__ float finish_one(const UpdArgs &a, int64_t i) {
+    float g = a.grad[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t j = i - a.g.off[k];
+        if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
+            const float *sl = a.g.slab[k] + j;
+            const int64_t n = a.g.n[k];
+            const int zc = a.g.z[k];
+            float v = 0.0f;
+            int z = 0;
+            for (; z + 8 <= zc; z += 8) {
+                float x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = sl[(int64_t)(z + u) * n];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v += x[u];
+            }
+            for (; z < zc; ++z) v += sl[(int64_t)z * n];
+            g = v;
+        }
+    }
+    return g;
 }
 
-// one parameter: optional target copy, images, RMSProp (rmsprop_kernel order)
-__device__ __forceinline__ void apply_one(const UpdArgs &a, const QLayout &L, int64_t i, float g, bool due,
-                                          float omr) {
+// finish_one for the four parameters i0 .. i0+3 (i0 % 4 == 0, all in one section):
+// float4 slab loads, sixteen in flight per batch; per component the same z-ascending
+// sum as finish_one
+__device__ __forceinline__ f32x4 finish4(const UpdArgs &a, int64_t i0) {
+    f32x4 g = *reinterpret_cast<const f32x4 *>(a.grad + i0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t j = i0 - a.g.off[k];
+        if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
+            const float *sl = a.g.slab[k] + j;
+            const int64_t n = a.g.n[k];
+            const int zc = a.g.z[k];
+            f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+            int z = 0;
+            for (; z + 16 <= zc; z += 16) {
+                f32x4 x[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) x[u] = *reinterpret_cast<const f32x4 *>(sl + (int64_t)(z + u) * n);
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v += x[u];
+            }
+            if (z < zc) {
+                f32x4 x[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (z + u < zc) x[u] = *reinterpret_cast<const f32x4 *>(sl + (int64_t)(z + u) * n);
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (z + u < zc) v += x[u];
+            }
+            g = v;
+        }
+    }
+    return g;
+}
+
+// RMSProp of one parameter (rmsprop_kernel order); returns the new theta
+__device__ __forceinline__ float rms_one(const UpdArgs &a, int64_t i, float g, bool due, float omr) {
     const float qd = a.u.rho * a.u.acc[i] + omr * (g * g);
     a.u.acc[i] = qd;
     const float th = a.u.theta[i] - (g * a.u.lr) / (__builtin_sqrtf(qd) + a.u.eps);
     a.u.theta[i] = th;
-    int64_t x6 = 0;
-    int ps = 0;
-    const int64_t t = image_index(L, i, x6, ps);
-    if (t >= 0) {
-        a.u.wt[t] = th;
-        if (a.u.wtb)
-            for (int p = 0; p < 3; ++p) a.u.wtb[x6 + p * ps] = split_part(th, p);
+    if (due) a.u.theta_t[i] = th;
+    return th;
+}
+
+// The weight-image sections (conv2, conv3, Dense1) in blocks of GU_ROWS input
+// channels c of one kernel offset kk: the block's parameters (kk*CK + c)*CN + n are one
+// contiguous run (coalesced gradient / slab / theta / acc traffic); the new theta goes
+// through LDS and leaves in image order [kk][n][c] (float4 of four c, and the three bf16
+// planes as 8-byte pieces), so no image write is a stride-CK scatter.
+constexpr int GU_ROWS = 16;
+struct GuSec {
+    int64_t off, base;   // packed offset of the section's weights, image offset
+    int CK, CN, nkk;
+};
+__device__ __forceinline__ GuSec gu_sec(const QLayout &L, int s) {
+    if (s == 0) return GuSec{L.off_w2, L.off_t2, 16, 32, 9};
+    if (s == 1) return GuSec{L.off_w3, L.off_t3, 32, 64, 36};
+    return GuSec{L.off_d1w, L.off_td, 64, 64, L.Wo * L.Wo};
+}
+__host__ __device__ inline int gu_blocks(int CK, int nkk) { return nkk * (CK / GU_ROWS); }
+
+__device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb, bool due, float omr) {
+    __shared__ __attribute__((aligned(16))) float th_s[GU_ROWS * 64];
+    const int CN = S.CN, n_el = GU_ROWS * CN;
+    const int64_t p0 = S.off + ((int64_t)kk * S.CK + cb * GU_ROWS) * CN;   // a multiple of 4
+    for (int e = 4 * threadIdx.x; e < n_el; e += 4 * 256) {
+        const int64_t i = p0 + e;
+        f32x4 g;
+        if (a.finish) {
+            g = finish4(a, i);
+            *reinterpret_cast<f32x4 *>(a.grad + i) = g;
+        } else {
+            g = *reinterpret_cast<const f32x4 *>(a.grad + i);
+        }
+        if (!a.apply) continue;
+        const f32x4 ac = *reinterpret_cast<const f32x4 *>(a.u.acc + i);
+        const f32x4 th = *reinterpret_cast<const f32x4 *>(a.u.theta + i);
+        f32x4 qd, tn;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {   // rms_one's arithmetic, component by component
+            qd[c] = a.u.rho * ac[c] + omr * (g[c] * g[c]);
+            tn[c] = th[c] - (g[c] * a.u.lr) / (__builtin_sqrtf(qd[c]) + a.u.eps);
+        }
+        *reinterpret_cast<f32x4 *>(a.u.acc + i) = qd;
+        *reinterpret_cast<f32x4 *>(a.u.theta + i) = tn;
+        if (due) *reinterpret_cast<f32x4 *>(a.u.theta_t + i) = tn;
+        *reinterpret_cast<f32x4 *>(&th_s[e]) = tn;
     }
-    if (due) {
-        a.u.theta_t[i] = th;
-        if (t >= 0) {
-            a.u.wt_t[t] = th;
-            if (a.u.wtb_t)
-                for (int p = 0; p < 3; ++p) a.u.wtb_t[x6 + p * ps] = split_part(th, p);
+    if (!a.apply) return;
+    __syncthreads();
+    // image element (kk, n, c) at base + kk*CK*CN + n*CK + c; x6 planes at
+    // 3*base + kk*3*CK*CN + p*CK*CN + n*CK + c
+    for (int it = threadIdx.x; it < CN * (GU_ROWS / 4); it += 256) {
+        const int n = it / (GU_ROWS / 4), c4 = (it % (GU_ROWS / 4)) * 4;
+        const float v0 = th_s[(c4 + 0) * CN + n], v1 = th_s[(c4 + 1) * CN + n];
+        const float v2 = th_s[(c4 + 2) * CN + n], v3 = th_s[(c4 + 3) * CN + n];
+        const int64_t t = S.base + (int64_t)kk * S.CK * CN + (int64_t)n * S.CK + cb * GU_ROWS + c4;
+        const f32x4 w4 = {v0, v1, v2, v3};
+        *reinterpret_cast<f32x4 *>(a.u.wt + t) = w4;
+        if (due) *reinterpret_cast<f32x4 *>(a.u.wt_t + t) = w4;
+        if (a.u.wtb) {
+            const int64_t x6 = 3 * S.base + (int64_t)kk * 3 * S.CK * CN + (int64_t)n * S.CK + cb * GU_ROWS + c4;
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const uint32_t lo = (uint32_t)split_part(v0, pl) | ((uint32_t)split_part(v1, pl) << 16);
+                const uint32_t hi = (uint32_t)split_part(v2, pl) | ((uint32_t)split_part(v3, pl) << 16);
+                const u32x2 pc = {lo, hi};
+                *reinterpret_cast<u32x2 *>(a.u.wtb + x6 + (int64_t)pl * S.CK * CN) = pc;
+                if (due && a.u.wtb_t) *reinterpret_cast<u32x2 *>(a.u.wtb_t + x6 + (int64_t)pl * S.CK * CN) = pc;
+            }
         }
     }
 }
 
-// grid-stride over [0, off_d2w); the LAST block owns Dense2 (195 params): it
-// stages dq and h1 through LDS and reduces over the batch (d2_grad_kernel's order)
+// blocks: [0, nimg) image sections (gu_image_block); then GU_OTHER blocks grid-striding
+// over the parameters without an image (conv1, the conv2 / conv3 / Dense1 bias rows);
+// the LAST block owns Dense2 (195 params): it stages dq and h1 through LDS and reduces
+// over the batch (d2_grad_kernel's order)
+constexpr int GU_OTHER = 4;
 __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
     const QLayout &L = a.L;
     const bool due = a.apply && a.u.counter && (*a.u.counter % a.u.rate) == 0;   // utils.jl:469-472
     const float omr = 1.0f - a.u.rho;
-    if (blockIdx.x == gridDim.x - 1) {
+    const int nb2 = gu_blocks(16, 9), nb3 = gu_blocks(32, 36), nbd = gu_blocks(64, L.Wo * L.Wo);
+    const int nimg = nb2 + nb3 + nbd;
+    const int b = (int)blockIdx.x;
+    if (b == (int)gridDim.x - 1) {
         const int t = threadIdx.x;
         float g = 0.0f;
         const int64_t i = L.off_d2w + t;
@@ -1392,36 +1498,32 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
         } else if (t < 195) {
             g = a.grad[i];
         }
-        if (a.apply && t < 195) apply_one(a, L, i, g, due, omr);
+        if (a.apply && t < 195) rms_one(a, i, g, due, omr);
+    } else if (b < nimg) {
+        const int sec = b < nb2 ? 0 : b < nb2 + nb3 ? 1 : 2;
+        const int bl = b - (sec == 0 ? 0 : sec == 1 ? nb2 : nb2 + nb3);
+        const GuSec S = gu_sec(L, sec);
+        const int per = S.CK / GU_ROWS;
+        gu_image_block(a, S, bl / per, bl % per, due, omr);
     } else {
-        const int64_t nthreads = (int64_t)(gridDim.x - 1) * blockDim.x;
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < L.off_d2w; i += nthreads) {
-            float g = a.grad[i];
+        // conv1 [off_w1, off_w2), conv2 bias [off_b2, off_w3), conv3 bias [off_b3, off_d1w),
+        // Dense1 bias [off_d1b, off_d2w): one index space over the four runs
+        const int64_t r0 = L.off_w2 - L.off_w1, r1 = L.off_w3 - L.off_b2, r2 = L.off_d1w - L.off_b3,
+                      r3 = L.off_d2w - L.off_d1b;
+        const int64_t tot = r0 + r1 + r2 + r3;
+        for (int64_t e = (int64_t)(b - nimg) * 256 + threadIdx.x; e < tot; e += (int64_t)GU_OTHER * 256) {
+            const int64_t i = e < r0 ? L.off_w1 + e
+                            : e < r0 + r1 ? L.off_b2 + (e - r0)
+                            : e < r0 + r1 + r2 ? L.off_b3 + (e - r0 - r1)
+                                               : L.off_d1b + (e - r0 - r1 - r2);
+            float g;
             if (a.finish) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int64_t j = i - a.g.off[k];
-                    if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
-                        // slab_reduce order; the loads of 8 slabs go out together
-                        const float *sl = a.g.slab[k] + j;
-                        const int64_t n = a.g.n[k];
-                        const int zc = a.g.z[k];
-                        float v = 0.0f;
-                        int z = 0;
-                        for (; z + 8 <= zc; z += 8) {
-                            float x[8];
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) x[u] = sl[(int64_t)(z + u) * n];
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) v += x[u];
-                        }
-                        for (; z < zc; ++z) v += sl[(int64_t)z * n];
-                        g = v;
-                    }
-                }
+                g = finish_one(a, i);
                 a.grad[i] = g;
+            } else {
+                g = a.grad[i];
             }
-            if (a.apply) apply_one(a, L, i, g, due, omr);
+            if (a.apply) rms_one(a, i, g, due, omr);
         }
     }
     // every block read *counter (nb) above; the last to arrive advances it. The bookkeeping
@@ -1447,6 +1549,16 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
     if (!s_last) return;
     post_update_block(a.post);
     if (threadIdx.x == 0) __hip_atomic_store(a.post.ticket + 8 * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!a.post.next.out) return;
+    __shared__ int64_t s_draw;
+    if (threadIdx.x == 0) s_draw = *a.post.updates;   // this thread's own store above
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        SampleRider r = a.post.next;
+        r.draw_dev = nullptr;
+        r.draw = (uint64_t)s_draw;
+        sample_wave(r);
+    }
 }
 
 void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
@@ -1464,7 +1576,8 @@ void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad,
     a.apply = apply != nullptr;
     if (!a.finish && !a.apply) return;
     if (a.apply && !a.u.counter) a.u.rate = 1;
-    grad_update_kernel<<<(unsigned)std::min<int64_t>(ceil_div(L.off_d2w, 256), 1024) + 1, 256, 0, s>>>(a);
+    const int nimg = gu_blocks(16, 9) + gu_blocks(32, 36) + gu_blocks(64, L.Wo * L.Wo);
+    grad_update_kernel<<<(unsigned)(nimg + GU_OTHER + 1), 256, 0, s>>>(a);
     launch_check("grad_update_kernel");
 }
 

@@ -173,6 +173,8 @@ struct PostUpdate {
     float *epsilon;
     float decay, eps_end;
     uint32_t *ticket;      // [9 * 32] arrival counters (8 shards + top), 0 between launches
+    SampleRider next;      // out != nullptr: the last block also draws the NEXT update's batch
+                           // (draw = the advanced update count; one launch fewer per update)
 };
 // tr.losses / epsilon decay / nb += 1 after an update (utils.jl:456-481), the Huber
 // mean over the batch in a fixed order (256-thread strided sums, then a tree)

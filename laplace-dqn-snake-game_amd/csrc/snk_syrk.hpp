@@ -337,7 +337,6 @@ struct SyrkArgs {
     const uint16_t *xh, *xl;
     const int32_t *xe;
     int64_t ldh;
-    int direct;              // tiles[] is indexed by blockIdx.x itself (a per-XCD table: syrk_xcd_table)
 };
 
 // h3 operands for the Gram (snk_conv_h3.hpp's split, one scale per ROW):
@@ -593,7 +592,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     __shared__ __attribute__((aligned(16))) uint16_t lds[NB * 2 * 2 * SY_T * SH_ROW];
     int bi, bj;
     {
-        const int64_t t = a.direct ? (int64_t)blockIdx.x : a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
+        const int64_t t = a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
         if (a.tiles) {
             const int2 tb = a.tiles[t];
             bi = tb.x;
@@ -742,13 +741,31 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     };
     // U = lcm(NB, 2) steps per loop trip: buffer and B-fragment roles are constants
     constexpr int U = NB % 2 ? 2 * NB : NB;
+    auto one = [&](int st0, bool tail, auto ic) {
+        constexpr int I = decltype(ic)::value;
+        if (!tail || st0 + I < nst)
+            step(st0 + I, std::integral_constant<int, I % NB>{}, I % 2 ? b1 : b0, I % 2 ? b0 : b1);
+    };
     auto trip = [&](int st0, bool tail) {
-        [&]<int... I>(std::integer_sequence<int, I...>) {
-            ((!tail || st0 + I < nst
-                  ? step(st0 + I, std::integral_constant<int, I % NB>{}, I % 2 ? b1 : b0, I % 2 ? b0 : b1)
-                  : void()),
-             ...);
-        }(std::make_integer_sequence<int, U>{});
+        static_assert(U <= 10, "unrolled trip");
+        one(st0, tail, std::integral_constant<int, 0>{});
+        one(st0, tail, std::integral_constant<int, 1>{});
+        if constexpr (U > 2) {
+            one(st0, tail, std::integral_constant<int, 2>{});
+            one(st0, tail, std::integral_constant<int, 3>{});
+        }
+        if constexpr (U > 4) {
+            one(st0, tail, std::integral_constant<int, 4>{});
+            one(st0, tail, std::integral_constant<int, 5>{});
+        }
+        if constexpr (U > 6) {
+            one(st0, tail, std::integral_constant<int, 6>{});
+            one(st0, tail, std::integral_constant<int, 7>{});
+        }
+        if constexpr (U > 8) {
+            one(st0, tail, std::integral_constant<int, 8>{});
+            one(st0, tail, std::integral_constant<int, 9>{});
+        }
     };
     int st = 0;
     for (; st + U <= nst; st += U) trip(st, false);

@@ -112,7 +112,8 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s, &acc);
     if (!upd) return;
     for (int u = 0; u < n_upd; ++u) {
-        if (u > 0) replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s);
+        // update u > 0 of the non-deep net: drawn by update u-1's grad_update_kernel (PostUpdate::next)
+        if (u > 0 && q->deep) replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s);
         HeadArgs m;
         m.idx = h->idx;
         m.rew = R.reward;
@@ -124,9 +125,13 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
         lo.defer = &pend;
         lo.loss_mean = false;
         dqn_loss_grad(q, src_replay(R, h->idx, 0), src_replay(R, h->idx, 1), m, h->B, h->cfg.gamma, s, lo);
-        const PostUpdate post{q->deep ? deep_batch_losses(q) : q->trn.loss, h->B, q->loss_dev, &h->stats->last_loss,
-                              h->loss_log, h->log_cap, &h->stats->updates, &h->stats->nb, &h->stats->epsilon,
-                              h->cfg.decay, h->cfg.epsilon_end, h->ticket};
+        PostUpdate post{q->deep ? deep_batch_losses(q) : q->trn.loss, h->B, q->loss_dev, &h->stats->last_loss,
+                        h->loss_log, h->log_cap, &h->stats->updates, &h->stats->nb, &h->stats->epsilon,
+                        h->cfg.decay, h->cfg.epsilon_end, h->ticket, SampleRider{}};
+        if (!q->deep && u + 1 < n_upd) {   // the next update's replay draw (utils.jl:442), count unchanged
+            post.next.count = R.count; post.next.cap = R.cap; post.next.pending = 0; post.next.batch = h->B;
+            post.next.seed = sseed; post.next.out = h->idx;
+        }
         if (q->deep) {   // the deeper bf16 net: finished gradient, [mean over ranks], RMSProp + images + target
             if (h->comm) comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
             deep_apply(q, &h->stats->nb, h->cfg.target_update_rate, s);
