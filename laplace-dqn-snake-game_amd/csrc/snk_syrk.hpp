@@ -621,7 +621,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
         ddst = ((op * 2 + pl) * SY_T + rb * 16) * SH_ROW;
     }
     const int64_t qstride = 16 * 2 * a.ldh;
-    auto dma = [&](int st, int buf) {
+    auto dma = [&](int st, int buf) __attribute__((always_inline)) {
         if (VAR == 2 && st > NB - 2) return;
         const int64_t k = (int64_t)min(st, nst - 1) * 2 * SY_KS;
 #pragma unroll
@@ -635,7 +635,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     // stage's and the next's): [tile][plane]
     typedef f16x8 FA[2][2];
     typedef f16x8 FB[2][2];
-    auto frag_a = [&](int buf, int t0, FA &f) {
+    auto frag_a = [&](int buf, int t0, FA &f) __attribute__((always_inline)) {
         const uint16_t *base = lds + buf * (4 * SY_T * SH_ROW);
 #pragma unroll
         for (int pn = 0; pn < 2; ++pn)
@@ -646,7 +646,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
                     base + ((0 * 2 + pn) * SY_T + row) * SH_ROW + 8 * (g ^ syrk_swz16(row))));
             }
     };
-    auto frag_b = [&](int buf, FB &f) {
+    auto frag_b = [&](int buf, FB &f) __attribute__((always_inline)) {
         const uint16_t *base = lds + buf * (4 * SY_T * SH_ROW);
 #pragma unroll
         for (int pn = 0; pn < 2; ++pn)
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     // tile pair l*h, h*l, then h*h (small products first)
     // part 0: only the first MFMA (tile t0 x column 0, l*h); part 1: the other 11;
     // part 2: all 12
-    auto mfma_half = [&](const FA &fa, const FB &fb, int t0, int part) {
+    auto mfma_half = [&](const FA &fa, const FB &fb, int t0, int part) __attribute__((always_inline)) {
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
@@ -692,7 +692,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
                 }
             }
     };
-    auto flush = [&]() {
+    auto flush = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -717,7 +717,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     // the buffer of stage st-1, whose last readers passed step st-1's barrier),
     // wait for stage st+1 and the barrier, read stage st+1's tiles 0-1 and B
     // (lo is free now), MFMAs of tiles 2-3
-    auto step = [&](int st, auto bc_, FB &bc, FB &bn) {
+    auto step = [&](int st, auto bc_, FB &bc, FB &bn) __attribute__((always_inline)) {
         constexpr int B = decltype(bc_)::value;
         // the compiler's waitcnt pass drains lgkmcnt to 0 before the first MFMA of
         // the step: issue the row-tile 2-3 reads after it
@@ -741,12 +741,12 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     };
     // U = lcm(NB, 2) steps per loop trip: buffer and B-fragment roles are constants
     constexpr int U = NB % 2 ? 2 * NB : NB;
-    auto one = [&](int st0, bool tail, auto ic) {
+    auto one = [&](int st0, bool tail, auto ic) __attribute__((always_inline)) {
         constexpr int I = decltype(ic)::value;
         if (!tail || st0 + I < nst)
             step(st0 + I, std::integral_constant<int, I % NB>{}, I % 2 ? b1 : b0, I % 2 ? b0 : b1);
     };
-    auto trip = [&](int st0, bool tail) {
+    auto trip = [&](int st0, bool tail) __attribute__((always_inline)) {
         static_assert(U <= 10, "unrolled trip");
         one(st0, tail, std::integral_constant<int, 0>{});
         one(st0, tail, std::integral_constant<int, 1>{});
