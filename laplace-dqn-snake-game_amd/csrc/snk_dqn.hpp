@@ -27,6 +27,9 @@ struct snk_dqn_s {
     uint16_t *jplanes = nullptr;    // h3 Gram: jbuf rows as scaled fp16 parts [n][ldh/32][h 32 | l 32]
     int32_t *jexp = nullptr;        //   and their per-row power-of-two exponents
     int64_t jplanes_halves = 0, jexp_cap = 0;
+    uint16_t *dplanes = nullptr;    // the Dense-section Gram operands a3 | dz1 | h1 as h3 segments
+    int32_t *dexp = nullptr;        //   (h3_seg_rows_kernel) and their exponents [3][dexp_cap]
+    int64_t dplanes_halves = 0, dexp_cap = 0;
     int64_t *jidx = nullptr;
     uint8_t *jact = nullptr;
     // snk_dqn_create_deep: the deeper bf16 net; L then holds its head offsets and P only

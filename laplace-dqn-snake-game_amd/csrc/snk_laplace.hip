@@ -245,14 +245,28 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s, int r
             else if (var == 2) syrk_h3_kernel<8, 2><<<grid, 512, 0, s>>>(a);
             else syrk_h3_kernel<8><<<grid, 512, 0, s>>>(a);
         }
-    } else {      // fp32 rows: bf16 x6 split in the kernel
-        switch (out) {
-            case SYRK_F32: syrk_kernel<SYRK_F32, SY_X6><<<grid, 256, 0, s>>>(a); break;
-            case SYRK_SLAB64: syrk_kernel<SYRK_SLAB64, SY_X6><<<grid, 256, 0, s>>>(a); break;
-            default: syrk_kernel<SYRK_DENSE_ADD, SY_X6><<<grid, 256, 0, s>>>(a); break;
-        }
+    } else {      // D'D: fp32 rows, bf16 x6 split in the kernel, one fp64 slab per z
+        SNK_CHECK(out == SYRK_SLAB64 && a.g64, SNK_ERR_INTERNAL, "syrk: fp32 rows only for the slab Gram");
+        syrk_slab_kernel<<<grid, 256, 0, s>>>(a);
     }
     launch_check("syrk_kernel");
+}
+
+// G += the Dense-section Gram terms (syrk_h3q_kernel<0, 4, true>) over the
+// lower-triangle tiles of shard rank / nranks
+static void syrk_dense_launch(const SyrkArgs &a0, hipStream_t s, int rank, int nranks) {
+    SyrkArgs a = a0;
+    int64_t t1 = 0;
+    gram_tile_range(a.N, rank, nranks, a.t0, t1);
+    a.ntiles = t1 - a.t0;
+    a.tiles = syrk_tile_order(a.N);
+    if (a.ntiles == 0) return;
+    SNK_CHECK(a.xh && a.xe && a.act && a.g32 && a.ldh % SY_KS == 0 && 0 < a.s1 && a.s1 < a.s2 &&
+                  a.s2 < a.ldh / SY_KS && a.xes >= a.N,
+              SNK_ERR_INTERNAL, "syrk dense arguments");
+    SNK_CHECK(a.ntiles < (int64_t)1 << 31, SNK_ERR_INVALID, "syrk: problem too large");
+    syrk_h3q_kernel<0, 4, true><<<dim3((unsigned)a.ntiles), 512, 0, s>>>(a);
+    launch_check("syrk_h3q_kernel<dense>");
 }
 
 // make sure the dqn's Jacobian workspace holds n samples (and a Jacobian
@@ -487,10 +501,35 @@ static void jacobian_gram_tiles(snk_dqn m, snk_replay rb, int64_t n, float *G_de
         }
         syrk_launch(SYRK_F32, a, 1, s, rank, nranks);
         if (ms_out) SNK_HIP(hipEventRecord(ev[3], s));
-        SyrkArgs d{};
-        d.x = m->jw.a3; d.ld = L.K1; d.K = L.K1; d.kchunk = L.K1; d.N = (int)n; d.g32 = G_dev; d.ldg = n;
-        d.z = m->jw.dz1; d.hh = m->jw.h1; d.act = m->jact; d.ldz = 64;
-        syrk_launch(SYRK_DENSE_ADD, d, 1, s, rank, nranks);
+        {   // Dense-section terms: a3 | dz1 | h1 pre-split into h3 segments, one DENSE h3q pass
+            const int64_t st1 = ceil_div(L.K1, SY_KS), st2 = st1 + 64 / SY_KS, ldd = (st2 + 64 / SY_KS) * SY_KS;
+            const int64_t npad = (n + SW_ROWS_B - 1) / SW_ROWS_B * SW_ROWS_B;
+            SNK_CHECK(L.K1 % 4 == 0, SNK_ERR_INTERNAL, "Dense1 fan-in not a multiple of 4");
+            if (2 * npad * ldd > m->dplanes_halves) {
+                (void)hipStreamSynchronize(s);
+                dfree(m->dplanes);
+                m->dplanes = dalloc<uint16_t>(2 * npad * ldd);
+                m->dplanes_halves = 2 * npad * ldd;
+            }
+            if (n > m->dexp_cap) {
+                (void)hipStreamSynchronize(s);
+                dfree(m->dexp);
+                m->dexp = dalloc<int32_t>(3 * n);
+                m->dexp_cap = n;
+            }
+            H3Segs sg{};
+            sg.x[0] = m->jw.a3; sg.x[1] = m->jw.dz1; sg.x[2] = m->jw.h1;
+            sg.ld[0] = sg.K[0] = L.K1; sg.ld[1] = sg.K[1] = sg.ld[2] = sg.K[2] = 64;
+            sg.st[0] = 0; sg.st[1] = st1; sg.st[2] = st2;
+            sg.nst[0] = st1; sg.nst[1] = sg.nst[2] = 64 / SY_KS;
+            h3_seg_rows_kernel<<<dim3((unsigned)ceil_div(npad, 4), 3), 256, 0, s>>>(sg, n, npad, m->dplanes, m->dexp,
+                                                                                   m->dexp_cap, ldd);
+            launch_check("h3_seg_rows_kernel");
+            SyrkArgs d{};
+            d.xh = m->dplanes; d.xe = m->dexp; d.xes = m->dexp_cap; d.ldh = ldd; d.s1 = (int)st1; d.s2 = (int)st2;
+            d.N = (int)n; d.g32 = G_dev; d.ldg = n; d.act = m->jact;
+            syrk_dense_launch(d, s, rank, nranks);
+        }
         if (nranks == 1) {
             const unsigned nb = (unsigned)ceil_div(n, 64);
             mirror_kernel<<<dim3(nb, nb), 256, 0, s>>>(G_dev, (int)n, n);

@@ -1,35 +1,26 @@
-// snk_syrk.hpp — symmetric Gram G = X X^T on v_mfma_f32_32x32x2_f32.
+// snk_syrk.hpp — symmetric Gram G = X X^T on the matrix cores.
 //
-// X is row-major [N][ld] fp32 (a row = one snapshot column of the reference's
-// D, or one per-sample Jacobian row), reduction over k < K (K, ld and every
-// k-range boundary multiples of 4 so a float4 never straddles the end).
-// Only lower-triangle 128 x 128 tiles (bj <= bi) are launched; a mirror pass
-// fills the upper triangle bit-identically.
-//
-// Workgroup = 4 waves, each owning a 64 x 64 quarter of the tile (2 x 2 MFMA
-// tiles, 64 accumulator registers). Per 32-k stage the workgroup stages the
-// 128 x 32 row blocks of both operands into LDS ([row][k], rows padded to 36
-// floats: conflict-free ds_read_b128), double buffered with one barrier per
-// stage; the next stage's global float4 loads are issued before the current
-// stage's 64 MFMAs per wave (sched_barrier keeps them there) and land in LDS
-// after them. A lane's float4 covers 4 MFMA k-steps (lane half h holds
-// k = 8*kb + 4h + j at step j) identically for both operands, so the k
-// permutation cancels.
-//
-// Accuracy: the fp32 accumulators are flushed into fp64 every 32 stages
-// (1024 k), so the error is that of 1024-long fp32 dot products summed in
-// fp64, independent of K (K is ~79k for the Jacobian Gram).
+// X is row-major [N][ld] (a row = one snapshot column of the reference's D, or
+// one per-sample Jacobian row), reduction over k < K. Only lower-triangle
+// 128 x 128 tiles (bj <= bi) are launched; a mirror pass fills the upper
+// triangle bit-identically. Three kernels:
+//   - syrk_h3q_kernel: the Jacobian Gram (conv sections, and with DENSE the
+//     Dense-section terms) on rows pre-split into power-of-two-scaled fp16
+//     hi/lo planes, v_mfma_f32_16x16x32_f16, LDS-DMA staging;
+//   - syrk_h3_kernel: its round-2 predecessor on v_mfma_f32_32x32x16_f16
+//     (measurement build, SNK_SYRK=h3);
+//   - syrk_kernel<SYRK_SLAB64>: the snapshot Gram D'D on fp32 rows split in the
+//     kernel into three bf16 planes (6 products of v_mfma_f32_32x32x16_bf16),
+//     one fp64 slab per split of the reduction.
+// The fp32 accumulators are flushed into fp64 every SY_FLUSH stages (1024 k),
+// so the error is that of 1024-long fp32 dot products summed in fp64,
+// independent of K (K is ~79k for the Jacobian Gram).
 #pragma once
 #include "snk_conv_h3.hpp"
 
 namespace snk {
 
-constexpr int SY_T = 128, SY_KS = 32, SY_LD = 36, SY_FLUSH = 32;
-
-struct SyrkLds {
-    float a[2][SY_T * SY_LD];
-    float b[2][SY_T * SY_LD];
-};
+constexpr int SY_T = 128, SY_KS = 32, SY_FLUSH = 32;
 
 // lower-triangle tile t -> (bi, bj), bj <= bi
 __device__ __forceinline__ void syrk_tile(int64_t t, int &bi, int &bj) {
@@ -49,99 +40,7 @@ __device__ __forceinline__ int64_t syrk_xcd_remap(int64_t w, int64_t ntiles) {
     return (w % 8) * per + w / 8;
 }
 
-struct SyrkRows {  // the 4 staging rows of this thread for one operand
-    const float *p[4];
-    float m[4];
-};
-
-__device__ __forceinline__ SyrkRows syrk_rows(const float *x, int64_t ld, int N, int blk, int tid) {
-    SyrkRows r;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int row = blk * SY_T + (tid >> 3) + 32 * q;
-        const bool ok = row < N;
-        r.p[q] = x + (int64_t)(ok ? row : N - 1) * ld;
-        r.m[q] = ok ? 1.0f : 0.0f;
-    }
-    return r;
-}
-
-// acc (+)= X[bi block][k0:k1] X[bj block][k0:k1]^T; with FLUSH the fp32
-// accumulators are folded into accd every SY_FLUSH stages and at the end
-template <bool FLUSH>
-__device__ __forceinline__ void syrk_loop(const float *__restrict__ x, int64_t ld, int N, int64_t k0, int64_t k1,
-                                          int bi, int bj, SyrkLds &s, f32x16 (&acc)[2][2],
-                                          double (&accd)[2][2][16]) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
-    const SyrkRows ra = syrk_rows(x, ld, N, bi, tid), rb = syrk_rows(x, ld, N, bj, tid);
-    const int c4 = 4 * (tid & 7);
-    const int sdst = (tid >> 3) * SY_LD + c4;
-    const int nst = (int)((k1 - k0 + SY_KS - 1) / SY_KS);
-    f32x4 va[4], vb[4];
-    float km = 1.0f;
-    auto issue = [&](int st) {
-        const int64_t k = k0 + (int64_t)st * SY_KS + c4;
-        const bool v = k < k1;
-        const int64_t kk = v ? k : k0;   // k1 - k0 >= 4: the fallback float4 is in range
-        km = v ? 1.0f : 0.0f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            va[q] = *reinterpret_cast<const f32x4 *>(ra.p[q] + kk);
-            vb[q] = *reinterpret_cast<const f32x4 *>(rb.p[q] + kk);
-        }
-    };
-    auto park = [&](int buf, float kmask) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            *reinterpret_cast<f32x4 *>(&s.a[buf][sdst + 32 * q * SY_LD]) = va[q] * (ra.m[q] * kmask);
-            *reinterpret_cast<f32x4 *>(&s.b[buf][sdst + 32 * q * SY_LD]) = vb[q] * (rb.m[q] * kmask);
-        }
-    };
-    issue(0);
-    park(0, km);
-    __syncthreads();
-    for (int st = 0; st < nst; ++st) {
-        const int buf = st & 1;
-        const bool more = st + 1 < nst;
-        issue(more ? st + 1 : st);
-        const float km_n = km;
-        __builtin_amdgcn_sched_barrier(0);
-        const float *pa = &s.a[buf][(wr + r) * SY_LD + 4 * h];
-        const float *pb = &s.b[buf][(wc + r) * SY_LD + 4 * h];
-#pragma unroll
-        for (int kb = 0; kb < SY_KS / 8; ++kb) {
-            const f32x4 a0 = *reinterpret_cast<const f32x4 *>(pa + kb * 8);
-            const f32x4 a1 = *reinterpret_cast<const f32x4 *>(pa + 32 * SY_LD + kb * 8);
-            const f32x4 b0 = *reinterpret_cast<const f32x4 *>(pb + kb * 8);
-            const f32x4 b1 = *reinterpret_cast<const f32x4 *>(pb + 32 * SY_LD + kb * 8);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], b0[j], acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], b1[j], acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], b0[j], acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], b1[j], acc[1][1], 0, 0, 0);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (FLUSH && (st % SY_FLUSH == SY_FLUSH - 1 || !more)) {
-#pragma unroll
-            for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-                for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-                    for (int g = 0; g < 16; ++g) {
-                        accd[mi][ni][g] += (double)acc[mi][ni][g];
-                        acc[mi][ni][g] = 0.0f;
-                    }
-        }
-        if (more) park(buf ^ 1, km_n);
-        __syncthreads();
-    }
-}
-
-// The same tile on the bf16 x6 split (snk_conv_x6.hpp): each 32-k stage of
+// A 128 x 128 tile on the bf16 x6 split (snk_conv_x6.hpp): each 32-k stage of
 // both 128-row blocks is loaded as fp32 (two float4 per row chunk of 8 k),
 // split once into h/m/l bf16 planes while parked in LDS ([op][plane][row][40]:
 // 80-byte rows, conflict-free ds_read_b128 for both lane halves), and each
@@ -150,8 +49,8 @@ __device__ __forceinline__ void syrk_loop(const float *__restrict__ x, int64_t l
 // 32x32x2 f32 form, with the error class of an fp32 dot product. Double
 // buffered (120 KB: the fp64 flush accumulators hold the kernel to one
 // workgroup per CU anyway): the next stage is split and parked right after
-// this stage's MFMAs, one barrier per stage. Accumulator layout and fp64
-// flushing as syrk_loop.
+// this stage's MFMAs, one barrier per stage. Each wave owns a 64 x 64 quarter
+// of the tile (2 x 2 MFMA tiles of 32 x 32).
 constexpr int SX_LD = 40;
 struct SyrkX6Lds {
     uint16_t p[2][2][3][SY_T * SX_LD];   // [buffer][operand][plane]
@@ -177,14 +76,15 @@ __device__ __forceinline__ void syrk_loop_x6(const float *__restrict__ x, int64_
         mb[q] = rb < N ? 1.0f : 0.0f;
     }
     const int nst = (int)((k1 - k0 + SY_KS - 1) / SY_KS);
-    // three register sets: stages st+1 .. st+3 in flight while stage st computes
-    // (one 32 KB stage per CU in flight left the loads latency-bound)
+    // two register sets: stage st+1 waits parked in one while stage st computes,
+    // the loads of stage st+2 go into the other (three sets, with stage st+3 also
+    // in flight, spilled the fp64 accumulators to scratch)
     struct Stage {
         f32x4 va[2][2], vb[2][2];
         float km[2];
     };
-    Stage rs[3];
-    auto issue = [&](int st, Stage &g) {
+    Stage rs[2];
+    auto issue = [&](int st, Stage &g) __attribute__((always_inline)) {
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int64_t k = k0 + (int64_t)st * SY_KS + c8 + 4 * hf;
@@ -198,7 +98,7 @@ __device__ __forceinline__ void syrk_loop_x6(const float *__restrict__ x, int64_
             }
         }
     };
-    auto park = [&](int buf, const Stage &g) {
+    auto park = [&](int buf, const Stage &g) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int off = ((tid >> 2) + 64 * q) * SX_LD + c8;
@@ -213,7 +113,7 @@ __device__ __forceinline__ void syrk_loop_x6(const float *__restrict__ x, int64_
         }
     };
     // one quarter of park(): operand op (0: A rows, 1: B rows), row group q
-    auto park_piece = [&](int buf, const Stage &g, int op, int q) {
+    auto park_piece = [&](int buf, const Stage &g, int op, int q) __attribute__((always_inline)) {
         const int off = ((tid >> 2) + 64 * q) * SX_LD + c8;
         const float m = op == 0 ? ma[q] : mb[q];
         const f32x4 *v = op == 0 ? g.va[q] : g.vb[q];
@@ -223,7 +123,7 @@ __device__ __forceinline__ void syrk_loop_x6(const float *__restrict__ x, int64_
         *reinterpret_cast<u32x4 *>(&s.p[buf][op][2][off]) = sp.l;
     };
     // the MFMAs of one stage with the park of the next woven in (source order)
-    auto compute_park = [&](int buf, bool pk, const Stage &nx) {
+    auto compute_park = [&](int buf, bool pk, const Stage &nx) __attribute__((always_inline)) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             bf16x8 fa[2][3], fb[2][3];
@@ -252,7 +152,7 @@ __device__ __forceinline__ void syrk_loop_x6(const float *__restrict__ x, int64_
                 }
         }
     };
-    auto flush = [&]() {
+    auto flush = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -263,18 +163,18 @@ __device__ __forceinline__ void syrk_loop_x6(const float *__restrict__ x, int64_
                     acc[mi][ni][g] = 0.0f;
                 }
     };
-    // stage st: loads of st+3 go out into set st % 3 (whose stage st was
-    // parked at st-1), stage st+1 (set (st+1) % 3) is parked after the MFMAs.
+    // stage st: the loads of st+2 go out into set st % 2 (whose stage st was
+    // parked at st-1), stage st+1 (set (st+1) % 2) is parked after the MFMAs.
     // Stage indices past the end clamp (the loads are masked by km and unused).
-    // BUF = st & 1 is a template constant (the loop is unrolled by 6), so the
+    // BUF = st & 1 is a template constant (the loop is unrolled by 2), so the
     // compiler sees that the park's LDS stores and this stage's fragment
     // reads touch different buffers; the split VALU work and the stores are
     // woven between the MFMAs in source order to fill their issue slots
     // (one wave per SIMD: nothing else would hide them).
-    auto step = [&](int st, auto bufc, Stage &ld3, Stage &nx) {
+    auto step = [&](int st, auto bufc, Stage &ld2, Stage &nx) __attribute__((always_inline)) {
         constexpr int BUF = decltype(bufc)::value;
         const bool more = st + 1 < nst;
-        issue(st + 3 < nst ? st + 3 : nst - 1, ld3);
+        issue(st + 2 < nst ? st + 2 : nst - 1, ld2);
         __builtin_amdgcn_sched_barrier(0);
         // park of stage st+1 into the other buffer (last read in stage st-1,
         // before the barrier), woven between the second k-step's MFMAs
@@ -286,24 +186,14 @@ __device__ __forceinline__ void syrk_loop_x6(const float *__restrict__ x, int64_
     using B1 = std::integral_constant<int, 1>;
     issue(0, rs[0]);
     if (nst > 1) issue(1, rs[1]);
-    if (nst > 2) issue(2, rs[2]);
     park(0, rs[0]);
     __syncthreads();
     int st = 0;
-    for (; st + 6 <= nst; st += 6) {
+    for (; st + 2 <= nst; st += 2) {
         step(st, B0{}, rs[0], rs[1]);
-        step(st + 1, B1{}, rs[1], rs[2]);
-        step(st + 2, B0{}, rs[2], rs[0]);
-        step(st + 3, B1{}, rs[0], rs[1]);
-        step(st + 4, B0{}, rs[1], rs[2]);
-        step(st + 5, B1{}, rs[2], rs[0]);
+        step(st + 1, B1{}, rs[1], rs[0]);
     }
-    // tail (< 6 stages): the same rotation
     if (st < nst) step(st, B0{}, rs[0], rs[1]);
-    if (st + 1 < nst) step(st + 1, B1{}, rs[1], rs[2]);
-    if (st + 2 < nst) step(st + 2, B0{}, rs[2], rs[0]);
-    if (st + 3 < nst) step(st + 3, B1{}, rs[0], rs[1]);
-    if (st + 4 < nst) step(st + 4, B0{}, rs[1], rs[2]);
 }
 
 __device__ __forceinline__ void syrk_zero(f32x16 (&acc)[2][2]) {
@@ -315,7 +205,7 @@ __device__ __forceinline__ void syrk_zero(f32x16 (&acc)[2][2]) {
             for (int g = 0; g < 16; ++g) acc[mi][ni][g] = 0.0f;
 }
 
-enum SyrkOut { SYRK_F32 = 0, SYRK_SLAB64 = 1, SYRK_DENSE_ADD = 2 };
+enum SyrkOut { SYRK_F32 = 0, SYRK_SLAB64 = 1 };
 
 struct SyrkArgs {
     const float *x;
@@ -324,19 +214,21 @@ struct SyrkArgs {
     int64_t ntiles;          // tiles of this launch: [t0, t0 + ntiles) of the order
     int64_t t0;
     const int2 *tiles;       // optional tile order (bi, bj), indexed by the XCD remap; null: row-major
-    float *g32;              // SYRK_F32 / SYRK_DENSE_ADD: G [N][ldg]
+    float *g32;              // SYRK_F32 (h3q): G [N][ldg]
     double *g64;             // SYRK_SLAB64: slab [z][N][N]
     int64_t ldg;
-    // SYRK_DENSE_ADD: G += (x_i.x_j + 1)(z_i.z_j) + [a_i == a_j](h_i.h_j + 1)
-    const float *z, *hh;
-    const uint8_t *act;
-    int64_t ldz;
+    const uint8_t *act;      // DENSE h3q: replay actions of the N samples
     // syrk_h3_kernel: x pre-split by h3_rows_kernel into xh [N][ldh/32][2][32] fp16
     // (per row and 32-k stage: the h part, then the l part: one 128-byte line;
     // ldh a multiple of SY_KS, zero tail), row i scaled by 2^xe[i]
     const uint16_t *xh, *xl;
     const int32_t *xe;
     int64_t ldh;
+    // syrk_h3q_kernel<.., DENSE = true>: xh holds three h3 segments per row,
+    // a3 (stages [0, s1)), dz1 ([s1, s2)), h1 ([s2, ldh/32)), each with its own
+    // row exponent xe[seg * xes + row] (h3_seg_rows_kernel)
+    int s1, s2;
+    int64_t xes;
 };
 
 // h3 operands for the Gram (snk_conv_h3.hpp's split, one scale per ROW):
@@ -368,6 +260,41 @@ static __global__ __launch_bounds__(256) void h3_rows_kernel(const float *__rest
         u32x2 h, l;
         h3_split4(v, e, h, l);
         const int64_t q = (i >> 3) * 16 + (i & 7);   // stage i / 8, 4-half piece i % 8
+        o[q] = h;
+        o[q + 8] = l;
+    }
+}
+
+// The Dense-section operands of the Jacobian Gram, pre-split like h3_rows_kernel
+// but one wave per (row, segment): segment g of row i is x_g[i][0, K_g) (K_g a
+// multiple of 4), zero-padded to nst_g stages, stored at stage offset st_g of the row's plane line
+// (row stride 2 * ldh halves), scaled by 2^xe[g * xes + i]. Rows n <= i < npad
+// are zero.
+struct H3Segs {
+    const float *x[3];
+    int64_t ld[3], K[3], st[3], nst[3];
+};
+static __global__ __launch_bounds__(256) void h3_seg_rows_kernel(H3Segs sg, int64_t n, int64_t npad, uint16_t *__restrict__ xhl,
+                                                          int32_t *__restrict__ xe, int64_t xes, int64_t ldh) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int seg = blockIdx.y, lane = threadIdx.x & 63;
+    if (row >= npad) return;
+    const int64_t n4 = sg.K[seg] / 4, np4 = sg.nst[seg] * (SY_KS / 4);
+    const bool live = row < n;
+    const f32x4 *src = reinterpret_cast<const f32x4 *>(sg.x[seg] + (live ? row : 0) * sg.ld[seg]);
+    float m = 0.0f;
+    for (int64_t i = lane; i < n4 && live; i += 64) {
+        const f32x4 v = src[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+    const int e = h3_exp(wave_max(m));
+    if (lane == 0 && live) xe[seg * xes + row] = e;
+    u32x2 *o = reinterpret_cast<u32x2 *>(xhl + row * 2 * ldh + sg.st[seg] * 2 * SY_KS);
+    for (int64_t i = lane; i < np4; i += 64) {
+        const f32x4 v = live && i < n4 ? src[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        u32x2 h, l;
+        h3_split4(v, e, h, l);
+        const int64_t q = (i >> 3) * 16 + (i & 7);
         o[q] = h;
         o[q + 8] = l;
     }
@@ -586,7 +513,14 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
 __device__ __forceinline__ int syrk_swz16(int row) { return (-(row >> 2)) & 3; }
 
 // NB stage buffers (32 KB each): NB - 1 stages in flight
-template <int VAR = 0, int NB = 4>
+// DENSE: the Dense-section terms of the Jacobian Gram over the three segments
+// of h3_seg_rows_kernel, added into G (lower-triangle tiles):
+//   G_ij += (a3_i.a3_j + 1)(dz1_i.dz1_j) + [act_i == act_j](h1_i.h1_j + 1)
+// (the Dense1 weight+bias and Dense2 weight+bias Jacobian blocks; the fp32
+// accumulators are folded at the segment ends, hook_a / hook_z below; the
+// a3 segment (K1 = 576 at 12x12) accumulates in fp32 like one flush interval of
+// the conv Gram)
+template <int VAR = 0, int NB = 4, bool DENSE = false>
 __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     constexpr int NJ = 4;   // DMA jobs per wave and stage (32 KB / 8 waves / 1 KB)
     __shared__ __attribute__((aligned(16))) uint16_t lds[NB * 2 * 2 * SY_T * SH_ROW];
@@ -703,6 +637,54 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
                     acc[i][j][e] = 0.0f;
                 }
     };
+    // DENSE segment ends: the exponents of the tile's rows and columns per segment,
+    // staged in LDS before the prologue barrier ([seg][128 rows | 128 columns],
+    // clamped to N - 1: rows past N are never stored). Read at the hooks, so no
+    // addresses stay live across the stage loop.
+    __shared__ __attribute__((aligned(16))) int ex_s[DENSE ? 3 * 2 * SY_T : 4];
+    if constexpr (DENSE) {
+        for (int t = tid; t < 3 * 2 * SY_T; t += 512) {
+            const int seg = t / (2 * SY_T), k = t % (2 * SY_T);
+            const int idx = k < SY_T ? bi * SY_T + k : bj * SY_T + k - SY_T;
+            ex_s[t] = a.xe[seg * a.xes + min(idx, N - 1)];
+        }
+    }
+    auto rowe = [&](int seg, int i, int e) __attribute__((always_inline)) {
+        return ex_s[seg * 2 * SY_T + wr + 16 * i + 4 * g + e];
+    };
+    auto cole = [&](int seg, int j) __attribute__((always_inline)) {
+        return ex_s[seg * 2 * SY_T + SY_T + wc + 16 * j + r];
+    };
+    // DENSE keeps fp32 partial terms instead of the fp64 flush accumulators (each
+    // segment is at most a few hundred k long; G is fp32): after the a3 segment
+    // pd = a3_i.a3_j + 1, after the dz1 segment pd *= dz1_i.dz1_j
+    float pd[4][2][4];
+    auto hook_a = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int ec = cole(0, j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    pd[i][j][e] = __builtin_ldexpf(acc[i][j][e], -(rowe(0, i, e) + ec)) + 1.0f;
+                    acc[i][j][e] = 0.0f;
+                }
+        }
+    };
+    auto hook_z = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int ec = cole(1, j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    pd[i][j][e] *= __builtin_ldexpf(acc[i][j][e], -(rowe(1, i, e) + ec));
+                    acc[i][j][e] = 0.0f;
+                }
+        }
+    };
 #pragma unroll
     for (int q = 0; q < NB - 1; ++q) dma(q, q);
     __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));
@@ -737,7 +719,12 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         mfma_half(hi, bc, 2, 2);
         __builtin_amdgcn_sched_barrier(0);
-        if (st % SY_FLUSH == SY_FLUSH - 1) flush();
+        if constexpr (DENSE) {
+            if (st == a.s1 - 1) hook_a();
+            else if (st == a.s2 - 1) hook_z();
+        } else if (st % SY_FLUSH == SY_FLUSH - 1) {
+            flush();
+        }
     };
     // U = lcm(NB, 2) steps per loop trip: buffer and B-fragment roles are constants
     constexpr int U = NB % 2 ? 2 * NB : NB;
@@ -771,6 +758,27 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     for (; st + U <= nst; st += U) trip(st, false);
     if (st < nst) trip(st, true);
     __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    if constexpr (DENSE) {   // the h1 segment: + [act_i == act_j](h1_i.h1_j + 1)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = bj * SY_T + wc + 16 * j + r;
+            if (col >= N) continue;
+            const int ec = cole(2, j);
+            const uint8_t ac = a.act[col];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = bi * SY_T + wr + 16 * i + 4 * g + e;
+                    if (row >= N) continue;
+                    double v = (double)pd[i][j][e];
+                    if (a.act[row] == ac) v += (double)__builtin_ldexpf(acc[i][j][e], -(rowe(2, i, e) + ec)) + 1.0;
+                    float *o = a.g32 + (int64_t)row * a.ldg + col;
+                    *o = (float)((double)*o + v);
+                }
+        }
+        return;
+    }
     flush();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -789,16 +797,10 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
 
 constexpr int SW_ROWS_B = 256;   // Jacobian-plane rows are padded to a multiple of this
 
-union SyrkSmem {
-    SyrkLds f32;
-    SyrkX6Lds x6;
-};
-enum SyrkMode { SY_F32 = 0, SY_X6 = 1 };
-
-template <int OUT, int MODE>
-__global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
-    __shared__ __attribute__((aligned(16))) SyrkSmem sm;
-    SyrkLds &s = sm.f32;
+// D'D: slab[z] = X[:, z-th k chunk] X[:, z-th k chunk]^T (lower-triangle
+// tiles), fp32 rows split into bf16 x6 in the kernel
+__global__ __launch_bounds__(256) void syrk_slab_kernel(SyrkArgs a) {
+    __shared__ __attribute__((aligned(16))) SyrkX6Lds sm;
     int bi, bj;
     {
         const int64_t t = a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
@@ -812,34 +814,18 @@ __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
     }
     f32x16 acc[2][2];
     double accd[2][2][16];
-    syrk_zero(acc);
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-            for (int g = 0; g < 16; ++g) accd[mi][ni][g] = 0.0;
+            for (int g = 0; g < 16; ++g) {
+                acc[mi][ni][g] = 0.0f;
+                accd[mi][ni][g] = 0.0;
+            }
     const int64_t k0 = (int64_t)blockIdx.y * a.kchunk;
     const int64_t k1 = k0 + a.kchunk < a.K ? k0 + a.kchunk : a.K;
-    if (k0 < k1) {
-        if (MODE == SY_X6)
-            syrk_loop_x6<true>(a.x, a.ld, a.N, k0, k1, bi, bj, sm.x6, acc, accd);
-        else
-            syrk_loop<true>(a.x, a.ld, a.N, k0, k1, bi, bj, s, acc, accd);
-    }
-    if (OUT == SYRK_DENSE_ADD) {
-        // (A3 Gram + 1) * (dz1 Gram)
-        syrk_zero(acc);
-        syrk_loop<false>(a.z, a.ldz, a.N, 0, 64, bi, bj, s, acc, accd);
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-                for (int g = 0; g < 16; ++g) accd[mi][ni][g] = (accd[mi][ni][g] + 1.0) * (double)acc[mi][ni][g];
-        syrk_zero(acc);
-        syrk_loop<false>(a.hh, a.ldz, a.N, 0, 64, bi, bj, s, acc, accd);
-    }
+    if (k0 < k1) syrk_loop_x6<true>(a.x, a.ld, a.N, k0, k1, bi, bj, sm, acc, accd);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = (wave >> 1) * 64, wc = (wave & 1) * 64;
 #pragma unroll
@@ -848,21 +834,11 @@ __global__ __launch_bounds__(256) void syrk_kernel(SyrkArgs a) {
         for (int ni = 0; ni < 2; ++ni) {
             const int col = bj * SY_T + wc + ni * 32 + (lane & 31);
             if (col >= a.N) continue;
-            const uint8_t ac = OUT == SYRK_DENSE_ADD ? a.act[col] : 0;
 #pragma unroll
             for (int g = 0; g < 16; ++g) {
                 const int row = bi * SY_T + wr + mi * 32 + acc_row(g, lane);
                 if (row >= a.N) continue;
-                if (OUT == SYRK_F32) {
-                    a.g32[(int64_t)row * a.ldg + col] = (float)accd[mi][ni][g];
-                } else if (OUT == SYRK_SLAB64) {
-                    a.g64[(int64_t)blockIdx.y * a.N * a.N + (int64_t)row * a.N + col] = accd[mi][ni][g];
-                } else {
-                    double v = accd[mi][ni][g];
-                    if (a.act[row] == ac) v += (double)acc[mi][ni][g] + 1.0;
-                    float *o = a.g32 + (int64_t)row * a.ldg + col;
-                    *o = (float)((double)*o + v);
-                }
+                a.g64[(int64_t)blockIdx.y * a.N * a.N + (int64_t)row * a.N + col] = accd[mi][ni][g];
             }
         }
 }
