@@ -170,10 +170,13 @@ def configs2(args, snk, graph) -> dict:
     wo, nc = bs - 5, bs * bs
     flop = [2.0 * n * nc * 32 * 9 * C, 2.0 * n * nc * 32 * 288, 2.0 * n * nc * 64 * 288,
             2.0 * n * wo * wo * 64 * 2304, 2.0 * n * wo * wo * 64 * 64, 2.0 * n * 64 * 3]
-    names = ["L0 conv 3x3 C->32 (deep_conv0_kernel, VALU)", "L1 conv 3x3 32->32 (deep_conv_kernel, bf16 MFMA)",
-             "L2 conv 3x3 32->64 (deep_conv_kernel, bf16 MFMA)", "L3 conv 6x6 64->64 (deep_conv_kernel, bf16 MFMA)",
+    # L0..L2 run as one launch (deep_front_kernel): its time is ms[0], ms[1] = ms[2] = 0
+    names = ["L0+L1+L2 conv 3x3 C->32->32->64 (deep_front_kernel, bf16 MFMA, fused in LDS)",
+             "L1 (inside deep_front_kernel)", "L2 (inside deep_front_kernel)",
+             "L3 conv 6x6 64->64 (deep_conv_kernel, bf16 MFMA)",
              "Dense1 (deep_dense1_kernel, bf16 MFMA)", "head (Dense2 + epsilon-greedy)"]
-    d = int(np.argmax(ms[1:5])) + 1
+    flop = [flop[0] + flop[1] + flop[2], 0.0, 0.0] + flop[3:]
+    d = int(np.argmax(ms[:5]))
     tf = flop[d] / (ms[d] * 1e-3) / 1e12
     fwd_flop = sum(flop)
     st = tr.stats()
@@ -182,7 +185,7 @@ def configs2(args, snk, graph) -> dict:
             "value": n * steps / el, "unit": "env-steps/s", "ms_per_step": 1000.0 * el / steps,
             "windows_ms": [1000.0 * w for w in windows], "steps": steps, "dtype": "bf16",
             "n_params": tr.model.P, "forward_flop_per_env_step": fwd_flop / n,
-            "act_forward_ms": {nm: float(t) for nm, t in zip(names, ms)},
+            "act_forward_ms": {nm: float(t) for nm, t in zip(names, ms) if t > 0},
             "act_forward_total_ms": float(ms.sum()),
             "act_forward_tflops": fwd_flop / (ms.sum() * 1e-3) / 1e12,
             "roofline": dict({"bound": "mfma", "kernel": names[d], "achieved": tf, "peak": PEAK_BF16_TFLOPS,
@@ -292,6 +295,7 @@ def d_build_gram(args, snk, model, dist, rank, world) -> dict:
         _, ms = snk.jacobian_gram(model, rb, n, out=G, host=False)
         wall = time.perf_counter() - t0
         t_gather = 0.0
+        gather_check = None
     else:
         import torch
         comm = snk.Comm(world, rank, snk.dist.broadcast_bytes(dist, snk.Comm.unique_id() if rank == 0 else None,
@@ -311,6 +315,22 @@ def d_build_gram(args, snk, model, dist, rank, world) -> dict:
         sync()
         t_gather = time.perf_counter() - t0
         del comm
+        gather_check = None
+        if rank == 0:   # the assembled G against one whole-matrix launch on rank 0 (untimed)
+            G1 = snk.DeviceArray((n, n), np.float32)
+            snk.jacobian_gram(model, rb, n, out=G1, host=False)
+            rows = np.sort(np.random.default_rng(7).choice(n, 16, replace=False))
+            bad, dmax = 0, 0.0
+            for r in rows:
+                a = _lib.view_numpy(G.ptr.value + int(r) * n * 4, (n,), np.float32)
+                b = _lib.view_numpy(G1.ptr.value + int(r) * n * 4, (n,), np.float32)
+                bad += int(np.count_nonzero(a != b))
+                dmax = max(dmax, float(np.max(np.abs(a.astype(np.float64) - b))))
+            gather_check = {"rows_compared": len(rows), "entries_compared": len(rows) * n,
+                            "mismatched_entries": bad, "max_abs_diff": dmax,
+                            "against": "single-launch snk_jacobian_gram on rank 0 (bit-exact expected)"}
+            del G1
+        sync()
     T = (n + 127) // 128
     tiles = len(snk.gram_tiles(n, rank, world))
     flop_gram = float(n) * (n + 1) * Kc * tiles / (T * (T + 1) // 2)   # this rank's share, 2 flop / MAC
@@ -322,6 +342,7 @@ def d_build_gram(args, snk, model, dist, rank, world) -> dict:
                                                         f"send/recv gather to rank 0" if world > 1 else ""),
                        "n_samples": n, "n_params": model.P, "conv_columns": Kc, "ranks": world,
                        "shard_sec_max_over_ranks": wall, "gather_sec": t_gather,
+                       **({"gather_check": gather_check} if gather_check else {}),
                        "phase_ms": {"forward_and_data_grads": ms[0], "per_sample_conv_jacobians": ms[1],
                                     "conv_gram": ms[2], "dense_terms_and_mirror": ms[3]},
                        "naive_flop": 2.0 * n * n * model.P, "executed_gram_flop_this_rank": flop_gram,

@@ -40,7 +40,6 @@ namespace snk {
 
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f16x8 as_h(const u32x4 &v) { return __builtin_bit_cast(f16x8, v); }
 

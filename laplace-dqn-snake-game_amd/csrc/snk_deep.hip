@@ -157,6 +157,17 @@ static void work_ensure(DeepNet &N, DeepWork &w, int64_t S, bool train) {
 }
 
 // ---------------------------------------------------------------- forward
+// compute units of the current device (persistent launches: one workgroup per CU)
+static int cu_count() {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        SNK_HIP(hipGetDevice(&dev));
+        SNK_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+        return std::max(n, 1);
+    }();
+    return cus;
+}
+
 template <int CIN, int COUT, int KS, int PAD, int H>
 static void conv_layer(const uint16_t *x, const uint16_t *img, const float *bias, uint16_t *y, int64_t S,
                        hipStream_t s) {
@@ -173,14 +184,63 @@ static void conv_layers_bs(const DeepNet &N, const float *th, const uint16_t *im
     const DeepLayout &D = N.D;
     if (lo <= 1 && hi >= 1) conv_layer<32, 32, 3, 1, BS>(w.a[0], img + D.img_w[1], th + D.off_b[1], w.a[1], S, s);
     if (lo <= 2 && hi >= 2) conv_layer<32, 64, 3, 1, BS>(w.a[1], img + D.img_w[2], th + D.off_b[2], w.a[2], S, s);
-    if (lo <= 3 && hi >= 3) conv_layer<64, 64, 6, 0, BS>(w.a[2], img + D.img_w[3], th + D.off_b[3], w.a[3], S, s);
+    if (lo <= 3 && hi >= 3) {   // two samples per step of a persistent workgroup (deep_conv3_kernel)
+        using Sh = DeepL3Shape<BS>;
+        static_assert(Sh::LDS <= 160 * 1024, "deep L3 LDS");
+        set_lds_limit((const void *)deep_conv3_kernel<BS>, Sh::LDS);
+        const unsigned grid = (unsigned)std::min<int64_t>((S + 1) / 2, cu_count());
+        deep_conv3_kernel<BS><<<grid, 512, Sh::LDS, s>>>(w.a[2], img + D.img_w[3], th + D.off_b[3], w.a[3], S);
+        launch_check("deep_conv3_kernel");
+    }
 }
 
-// layers lo..hi of the forward (0..3 convs, 4 Dense1) into w; returns the Dense1 split count
+// L0 + L1 + L2 in one persistent launch (deep_front_kernel): one workgroup per CU
+template <int C, int H>
+static void front_launch(const DeepNet &N, const float *th, const uint16_t *img, const float *img0, const BoardSrc &src,
+                         int64_t S, DeepWork &w, bool keep, hipStream_t s) {
+    using Sh = DeepFrontShape<H>;
+    static_assert(Sh::LDS <= 160 * 1024, "deep front LDS");
+    const DeepLayout &D = N.D;
+    const unsigned grid = (unsigned)std::min<int64_t>(S, cu_count());
+    if (keep) {
+        set_lds_limit((const void *)deep_front_kernel<C, H, true>, Sh::LDS);
+        deep_front_kernel<C, H, true><<<grid, 512, Sh::LDS, s>>>(src, img0, img + D.img_w[1], th + D.off_b[1],
+                                                                  img + D.img_w[2], th + D.off_b[2], w.a[0], w.a[1],
+                                                                  w.a[2], S);
+    } else {
+        set_lds_limit((const void *)deep_front_kernel<C, H, false>, Sh::LDS);
+        deep_front_kernel<C, H, false><<<grid, 512, Sh::LDS, s>>>(src, img0, img + D.img_w[1], th + D.off_b[1],
+                                                                   img + D.img_w[2], th + D.off_b[2], nullptr, nullptr,
+                                                                   w.a[2], S);
+    }
+    launch_check("deep_front_kernel");
+}
+
+// layers lo..hi of the forward (0..3 convs, 4 Dense1) into w; returns the Dense1 split count.
+// L0..L2 run fused (deep_front_kernel) whenever the range covers all three; keep: also
+// store the L0 / L1 outputs (the training forward)
 static int deep_layers(const DeepNet &N, const float *th, const uint16_t *img, const float *img0,
-                       const BoardSrc &src, int64_t S, DeepWork &w, hipStream_t s, int lo = 0, int hi = 4) {
+                       const BoardSrc &src, int64_t S, DeepWork &w, hipStream_t s, int lo = 0, int hi = 4,
+                       bool keep = false) {
     const DeepLayout &D = N.D;
     SNK_CHECK(S <= w.cap && S <= INT32_MAX, SNK_ERR_INTERNAL, "deep forward batch");
+    if (lo <= 0 && hi >= 2) {
+        auto go = [&](auto cc, auto hh) {
+            front_launch<decltype(cc)::value, decltype(hh)::value>(N, th, img, img0, src, S, w, keep, s);
+        };
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        switch (D.bs * 4 + D.C) {
+            case 10 * 4 + 1: go(I1{}, std::integral_constant<int, 10>{}); break;
+            case 10 * 4 + 2: go(I2{}, std::integral_constant<int, 10>{}); break;
+            case 12 * 4 + 1: go(I1{}, std::integral_constant<int, 12>{}); break;
+            case 12 * 4 + 2: go(I2{}, std::integral_constant<int, 12>{}); break;
+            case 20 * 4 + 1: go(I1{}, std::integral_constant<int, 20>{}); break;
+            case 20 * 4 + 2: go(I2{}, std::integral_constant<int, 20>{}); break;
+            default: SNK_CHECK(false, SNK_ERR_INVALID, "deep net: board side %d not built (10, 12, 20)", D.bs);
+        }
+        lo = 3;
+    }
     if (lo <= 0 && hi >= 0) {
         const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(8, S / 1024));
         const size_t lds = (size_t)(9 * D.C * 32 + 32 + ns * D.C * (D.bs + 2) * (D.bs + 2)) * sizeof(float);
@@ -415,10 +475,14 @@ void deep_time_layers(snk_dqn_s *h, const BoardSrc &src, int64_t S, const HeadAr
     SNK_HIP(hipEventCreate(&a));
     SNK_HIP(hipEventCreate(&b));
     for (int layer = 0; layer < 6; ++layer) {
+        if (layer == 1 || layer == 2) {   // inside layer 0's fused launch
+            ms[layer] = 0.0;
+            continue;
+        }
         SNK_HIP(hipEventRecord(a, s));
         for (int r = 0; r < reps; ++r) {
             if (layer < 5) {
-                deep_layers(N, h->theta_q, N.img_q, N.img0_q, src, S, N.act, s, layer, layer);
+                deep_layers(N, h->theta_q, N.img_q, N.img0_q, src, S, N.act, s, layer, layer == 0 ? 2 : layer);
             } else {
                 int kc;
                 head_launch(h->L, h->theta_q, N.act.slab, d1_splits(N.D, S, kc), S, N.act.h1, N.act.q, HEAD_ACT, ha, s);
@@ -439,7 +503,7 @@ void deep_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src,
     DeepNet &N = *h->deep;
     deep_prepare(h, 0, B);
     const int zt = deep_layers(N, h->theta_t, N.img_t, N.img0_t, sn_src, B, N.tgt, s);
-    const int zq = deep_layers(N, h->theta_q, N.img_q, N.img0_q, s_src, B, N.trn, s);
+    const int zq = deep_layers(N, h->theta_q, N.img_q, N.img0_q, s_src, B, N.trn, s, 0, 4, true);
     SNK_CHECK(zt == zq, SNK_ERR_INTERNAL, "deep head splits");
     HeadArgs la = meta;
     la.gamma = gamma;
