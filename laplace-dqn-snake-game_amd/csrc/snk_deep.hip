@@ -106,9 +106,12 @@ struct DeepNet {
     int64_t gen = 0;                               // bumped on every workspace reallocation
 };
 
+// Dense1 row tiles per wave (deep_dense1_kernel<NR>)
+static int d1_rows(int64_t S) { return S >= 16384 ? 4 : 1; }
+
 // Dense1 K splits: about 256 workgroups in all, each split a multiple of 32 features
 static int d1_splits(const DeepLayout &D, int64_t S, int &kchunk) {
-    const int64_t bx = (S + 63) / 64;
+    const int64_t bx = (S + 64 * d1_rows(S) - 1) / (64 * d1_rows(S));
     int z = (int)std::max<int64_t>(1, std::min<int64_t>(64, 256 / bx));
     kchunk = ((D.K1 + z - 1) / z + 31) & ~31;
     return (D.K1 + kchunk - 1) / kchunk;
@@ -262,8 +265,12 @@ static int deep_layers(const DeepNet &N, const float *th, const uint16_t *img, c
     int kc;
     const int z = d1_splits(D, S, kc);
     if (lo <= 4 && hi >= 4) {
-        deep_dense1_kernel<<<dim3((unsigned)((S + 63) / 64), (unsigned)z), 256, 0, s>>>(w.a[3], img + D.img_d1, S,
-                                                                                      D.K1, kc, w.slab);
+        if (d1_rows(S) == 4)
+            deep_dense1_kernel<4><<<dim3((unsigned)((S + 255) / 256), (unsigned)z), 256, 0, s>>>(w.a[3], img + D.img_d1,
+                                                                                                S, D.K1, kc, w.slab);
+        else
+            deep_dense1_kernel<1><<<dim3((unsigned)((S + 63) / 64), (unsigned)z), 256, 0, s>>>(w.a[3], img + D.img_d1,
+                                                                                               S, D.K1, kc, w.slab);
         launch_check("deep_dense1_kernel");
     }
     return z;

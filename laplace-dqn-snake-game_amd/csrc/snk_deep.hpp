@@ -635,52 +635,69 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
 }
 
 // ---------------------------------------------------------------- Dense1
-// slab[z][s][o] = sum_{f in split z} a4[s][f] * W1[f][o]; 4 waves x 16 samples
-// per workgroup, all 64 outputs (4 column tiles); A and B fragments straight
-// from global (the 1.8 MB bf16 image stays L2-resident), two k-steps in flight.
+// slab[z][s][o] = sum_{f in split z} a4[s][f] * W1[f][o]; 4 waves x 16*NR
+// samples per workgroup, all 64 outputs (4 column tiles); A and B fragments
+// straight from global (the 1.8 MB bf16 image stays L2-resident), two k-steps
+// in flight. NR row tiles per wave reuse each B fragment NR times: the B
+// stream from L2 is 1.8 MB per wave, so at 65,536 samples NR = 4 cuts it from
+// 7.4 GB (NR = 1) to 1.8 GB; small batches keep NR = 1 and split K instead.
+template <int NR>
 __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__restrict__ a4,
                                                           const uint16_t *__restrict__ w1img, int64_t S, int K1,
                                                           int kchunk, float *__restrict__ slab) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 15, g = lane >> 4;
-    const int64_t row0 = (int64_t)blockIdx.x * 64 + wave * 16;
-    const int64_t srow = min(row0 + r, S - 1);
+    const int64_t row0 = (int64_t)blockIdx.x * 64 * NR + wave * 16 * NR;
     const int k0 = blockIdx.y * kchunk, k1 = min(K1, k0 + kchunk);
-    const uint16_t *pa = a4 + srow * K1 + g * 8;
-    const uint16_t *pb = w1img + (int64_t)r * K1 + g * 8;
-    f32x4 acc[4];
+    const uint16_t *pa[NR];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NR; ++t) pa[t] = a4 + min(row0 + 16 * t + r, S - 1) * K1 + g * 8;
+    const uint16_t *pb = w1img + (int64_t)r * K1 + g * 8;
+    f32x4 acc[NR][4];
+#pragma unroll
+    for (int t = 0; t < NR; ++t)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     int k = k0;
     for (; k + 64 <= k1; k += 64) {
-        u32x4 a[2], b[2][4];
+        u32x4 a[NR][2], b[2][4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            a[u] = *reinterpret_cast<const u32x4 *>(pa + k + 32 * u);
+#pragma unroll
+            for (int t = 0; t < NR; ++t) a[t][u] = *reinterpret_cast<const u32x4 *>(pa[t] + k + 32 * u);
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) b[u][nt] = *reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + k + 32 * u);
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt)
-                acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a[u]), as_bf(b[u][nt]), acc[nt], 0, 0, 0);
+            for (int t = 0; t < NR; ++t)
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt)
+                    acc[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a[t][u]), as_bf(b[u][nt]), acc[t][nt], 0, 0, 0);
     }
     for (; k < k1; k += 32) {
-        const u32x4 a = *reinterpret_cast<const u32x4 *>(pa + k);
+        u32x4 b[4];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                as_bf(a), as_bf(*reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + k)), acc[nt], 0, 0, 0);
+        for (int nt = 0; nt < 4; ++nt) b[nt] = *reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + k);
+#pragma unroll
+        for (int t = 0; t < NR; ++t) {
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(pa[t] + k);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+                acc[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a), as_bf(b[nt]), acc[t][nt], 0, 0, 0);
+        }
     }
     float *o = slab + (int64_t)blockIdx.y * S * 64;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+    for (int t = 0; t < NR; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int64_t row = row0 + 4 * g + e;
-            if (row < S) o[row * 64 + nt * 16 + r] = acc[nt][e];
-        }
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t row = row0 + 16 * t + 4 * g + e;
+                if (row < S) o[row * 64 + nt * 16 + r] = acc[t][nt][e];
+            }
 }
 
 // ---------------------------------------------------------------- backward engine (bf16)

@@ -886,6 +886,11 @@ bool qnet_fused23(const QLayout &L, const float *th, const float *wt, const uint
 static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi,
                            const SampleRider *rider = nullptr) {
     const int bs = L.bs, nc = L.ncell;
+    bool fresh_in[2] = {false, false};   // QWork::wmax_fresh holds for this forward only
+    for (int g = 0; g < ng; ++g) {
+        fresh_in[g] = net[g].w->wmax_fresh != 0;
+        net[g].w->wmax_fresh = 0;
+    }
     const bool h3 = h3s_ok(L, net, ng, S);
     // h3 also for conv2 (conv_h3c2_kernel): conv1 then writes fp32 a1 only. SNK_H3C2=0: x6 conv2.
     const bool h3c2 = h3 && h3c2_on();
@@ -900,7 +905,10 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             const FwdNet &n = net[g];
             QWork &w = *n.w;
             const float *img = n.wt + L.off_t3;
-            if ((lo <= 0 && hi >= 0) || !w.wmax_n || w.wmax_img != img) {
+            // a full forward rescans the image (it may have changed in place) unless the
+            // trainer's previous grad_update wrote its partials (and no sample rides the scan)
+            const bool fresh = fresh_in[g] && w.wmax_n && w.wmax_img == img && !(rider && g == 0);
+            if (((lo <= 0 && hi >= 0) && !fresh) || !w.wmax_n || w.wmax_img != img) {
                 const SampleRider rd = (rider && g == 0) ? *rider : SampleRider{};
                 wmax_scan_kernel<<<256 + (rd.out ? 1 : 0), 256, 0, s>>>(img, n3, w.wmax_part, rd);
                 launch_check("wmax_scan_kernel");
@@ -1410,11 +1418,16 @@ __device__ __forceinline__ GuSec gu_sec(const QLayout &L, int s) {
     return GuSec{L.off_d1w, L.off_td, 64, 64, L.Wo * L.Wo};
 }
 __host__ __device__ inline int gu_blocks(int CK, int nkk) { return nkk * (CK / GU_ROWS); }
+static_assert(GU_WMAX_BLOCKS == 36 * (32 / GU_ROWS), "conv3 image blocks");
 
-__device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb, bool due, float omr) {
+// wmax: where this block's max |new theta| goes (the conv3 section, UpdateTarget::wmax_out)
+__device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb, bool due, float omr,
+                               float *wmax = nullptr) {
     __shared__ __attribute__((aligned(16))) float th_s[GU_ROWS * 64];
+    __shared__ float red4[4];
     const int CN = S.CN, n_el = GU_ROWS * CN;
     const int64_t p0 = S.off + ((int64_t)kk * S.CK + cb * GU_ROWS) * CN;   // a multiple of 4
+    float m = 0.0f;
     for (int e = 4 * threadIdx.x; e < n_el; e += 4 * 256) {
         const int64_t i = p0 + e;
         f32x4 g;
@@ -1437,9 +1450,15 @@ __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb,
         *reinterpret_cast<f32x4 *>(a.u.theta + i) = tn;
         if (due) *reinterpret_cast<f32x4 *>(a.u.theta_t + i) = tn;
         *reinterpret_cast<f32x4 *>(&th_s[e]) = tn;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(tn[0]), fabsf(tn[1])), fmaxf(fabsf(tn[2]), fabsf(tn[3]))));
     }
     if (!a.apply) return;
+    if (wmax) {
+        m = wave_max(m);
+        if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+    }
     __syncthreads();
+    if (wmax && threadIdx.x == 0) *wmax = fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
     // image element (kk, n, c) at base + kk*CK*CN + n*CK + c; x6 planes at
     // 3*base + kk*3*CK*CN + p*CK*CN + n*CK + c
     for (int it = threadIdx.x; it < CN * (GU_ROWS / 4); it += 256) {
@@ -1504,7 +1523,7 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
         const int bl = b - (sec == 0 ? 0 : sec == 1 ? nb2 : nb2 + nb3);
         const GuSec S = gu_sec(L, sec);
         const int per = S.CK / GU_ROWS;
-        gu_image_block(a, S, bl / per, bl % per, due, omr);
+        gu_image_block(a, S, bl / per, bl % per, due, omr, sec == 1 && a.u.wmax_out ? a.u.wmax_out + bl : nullptr);
     } else {
         // conv1 [off_w1, off_w2), conv2 bias [off_b2, off_w3), conv3 bias [off_b3, off_d1w),
         // Dense1 bias [off_d1b, off_d2w): one index space over the four runs

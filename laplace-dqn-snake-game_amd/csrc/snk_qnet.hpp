@@ -70,6 +70,8 @@ struct QWork {
     float *wmax_part = nullptr;      // h3 conv3: per-block partial max |w| of the conv3 weight image
     int wmax_n = 0;                  //   valid partials (conv1_fwd_kernel / wmax_scan_kernel wrote them)
     const float *wmax_img = nullptr; //   of this image
+    int wmax_fresh = 0;              //   set by the trainer: the partials were written by the grad_update that
+                                     //   last changed the image (the next full forward skips its scan; reset there)
     double *target = nullptr, *loss = nullptr;
     int has_train = 0;
     int64_t gen = 0;          // bumped on every reallocation (captured graphs hold the old pointers)
@@ -161,7 +163,11 @@ struct UpdateTarget {
     const int64_t *counter;   // nullptr: no target copy
     int64_t rate;
     float lr, rho, eps;
+    // optional: per-block partial max |w| of the new conv3 image (one per conv3 image
+    // block of grad_update_kernel, gu_blocks(32, 36) of them) for the next h3 act forward
+    float *wmax_out = nullptr;
 };
+constexpr int GU_WMAX_BLOCKS = 36 * (32 / 16);   // conv3 image blocks of grad_update_kernel (gu_blocks(32, 36))
 // the trainer's bookkeeping after an update (utils.jl:456-481: track_loss!, epsilon decay,
 // nb += 1), done by the last workgroup of the update pass to arrive (ticket)
 struct PostUpdate {

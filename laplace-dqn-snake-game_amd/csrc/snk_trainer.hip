@@ -80,20 +80,29 @@ struct snk_trainer_s {
 // One iteration's launch sequence (capturable: no host sync, no allocation),
 // with n_upd DQN updates after the env step. The first update's replay draw
 // counts the n transitions this step stores.
-static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream_t s, int it = 0) {
+// chain: the previous iteration of this launch sequence (same learn / n_upd) ran
+// just before, so its last grad_update already drew this iteration's first
+// sample (pending = the n stores to come) and wrote the conv3 weight-max
+// partials of the image the act forward reads; next_chain: the next one will.
+static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream_t s, int it = 0, bool chain = false,
+                              bool next_chain = false) {
     const EnvDev &E = env_dev(h->env);
     const ReplayDev &R = replay_dev(h->rb);
     snk_dqn_s *q = h->dqn;
     const bool upd = learn && n_upd > 0;
     const uint64_t sseed = h->cfg.seed ^ 0x5A4D504C45ULL;
+    chain = chain && upd && !q->deep;
+    next_chain = next_chain && upd && !q->deep;
     // the first update's sample (counting the n transitions this step stores) rides in a
-    // spare workgroup of the act forward's conv1 launch (small net, batch <= 64)
-    const bool ride = upd && !q->deep && h->B <= 64;
+    // spare workgroup of the act forward's weight-max scan (small net, batch <= 64), or
+    // was drawn by the previous iteration's last grad_update (chain)
+    const bool ride = upd && !q->deep && h->B <= 64 && !chain;
+    if (chain) q->act.wmax_fresh = 1;
     SampleRider rider;
     if (ride) {
         rider.count = R.count; rider.cap = R.cap; rider.pending = E.n; rider.batch = h->B; rider.seed = sseed;
         rider.draw_dev = &h->stats->updates; rider.out = h->idx;
-    } else if (upd) {
+    } else if (upd && !chain) {
         replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s, E.n);
     }
     HeadArgs ha;
@@ -128,9 +137,11 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
         PostUpdate post{q->deep ? deep_batch_losses(q) : q->trn.loss, h->B, q->loss_dev, &h->stats->last_loss,
                         h->loss_log, h->log_cap, &h->stats->updates, &h->stats->nb, &h->stats->epsilon,
                         h->cfg.decay, h->cfg.epsilon_end, h->ticket, SampleRider{}};
-        if (!q->deep && u + 1 < n_upd) {   // the next update's replay draw (utils.jl:442), count unchanged
-            post.next.count = R.count; post.next.cap = R.cap; post.next.pending = 0; post.next.batch = h->B;
-            post.next.seed = sseed; post.next.out = h->idx;
+        const bool last = u + 1 == n_upd;
+        if (!q->deep && (!last || next_chain)) {   // the next update's replay draw (utils.jl:442); for the next
+            // iteration's first update it counts the n transitions that iteration's step stores
+            post.next.count = R.count; post.next.cap = R.cap; post.next.pending = last ? E.n : 0;
+            post.next.batch = h->B; post.next.seed = sseed; post.next.out = h->idx;
         }
         if (q->deep) {   // the deeper bf16 net: finished gradient, [mean over ranks], RMSProp + images + target
             if (h->comm) comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
@@ -140,13 +151,18 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
         } else {
             // one pass: finish the gradient, RMSProp, forward image, update_target_net! when
             // nb % rate == 0, and (last block to arrive) the post-update bookkeeping
-            const UpdateTarget ut = dqn_update_target(q, &h->stats->nb, h->cfg.target_update_rate);
+            UpdateTarget ut = dqn_update_target(q, &h->stats->nb, h->cfg.target_update_rate);
+            if (last && next_chain) ut.wmax_out = q->act.wmax_part;   // for the next iteration's act forward
             if (h->comm) {   // data-parallel replicas: mean gradient before the step
                 grad_update_launch(q->L, &pend, q->grad, nullptr, s);
                 comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
                 grad_update_launch(q->L, nullptr, q->grad, &ut, s, &post);
             } else {
                 grad_update_launch(q->L, &pend, q->grad, &ut, s, &post);
+            }
+            if (ut.wmax_out) {
+                q->act.wmax_n = GU_WMAX_BLOCKS;
+                q->act.wmax_img = q->wt_q + q->L.off_t3;
             }
         }
         if (h->trace) {
@@ -277,7 +293,7 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
             if (h->exec[slot]) return;
             SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             try {
-                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s, i);
+                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s, i, i > 0, i + 1 < n);
             } catch (...) {
                 hipGraph_t dummy;
                 (void)hipStreamEndCapture(s, &dummy);
@@ -287,7 +303,8 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
             SNK_HIP(hipGraphInstantiate(&h->exec[slot], h->graph[slot], nullptr, nullptr, 0));
         };
         if (!use_graph) {
-            for (int64_t i = 0; i < iters; ++i) trainer_iteration(h, learn != 0, upi, s, (int)(i % (1 << 20)));
+            for (int64_t i = 0; i < iters; ++i)
+                trainer_iteration(h, learn != 0, upi, s, (int)(i % (1 << 20)), i > 0, i + 1 < iters);
             return;
         }
         const int U = h->unroll;
