@@ -289,22 +289,42 @@ __global__ __launch_bounds__(64 * NW) void deep_conv_kernel(const uint16_t *__re
 }
 
 // ---------------------------------------------------------------- L0..L2 fused (MFMA)
+// two floats -> two bf16 (round to nearest even: v_cvt_pk_bf16_f32, gfx950)
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
+}
+// relu(v + b) of four channels as four bf16
+__device__ __forceinline__ u32x2 relu_bf16x4(const f32x4 &v, const f32x4 &b) {
+    return u32x2{pk_bf16(fmaxf(v[0] + b[0], 0.f), fmaxf(v[1] + b[1], 0.f)),
+                 pk_bf16(fmaxf(v[2] + b[2], 0.f), fmaxf(v[3] + b[3], 0.f))};
+}
+
 // deep_front_kernel: L0 -> L1 -> L2 of one sample at a time inside one
 // workgroup, the activations never leaving LDS. Persistent: one workgroup per
-// CU (151 KB of LDS at 20x20) walks samples blockIdx.x, + gridDim.x, ...; the
-// L0, L1 and L2 weight images are staged into LDS once per workgroup.
-// LDS (halves): W1 [9][32 co][ST], W2 [9][64 co][ST], W0 [32 co][ST] (k < 9C,
-// zero above), X0 / X1 the bordered L0 / L1 outputs [(H+2)^2][ST], BD the
-// bordered boards [C][(H+2)^2] bf16; ST = 40 halves per row (32 + 8 pad: the
-// 16-byte fragment reads of 16 consecutive rows land on distinct bank quads).
+// CU walks samples blockIdx.x, + gridDim.x, ...; the L0, L1 and L2 weight
+// images are staged into LDS once per workgroup.
+// LDS (halves): W1 [9][32 co][32], W2 [9][64 co][32], W0 [32 co][32] (k < 9C,
+// zero above): 64-byte rows, chunk c of row `row` at slot c ^ ((row >> 1) & 3),
+// which depends only on the lane for the fragment reads (row = 16*tile + lane);
+// X, the bordered L0 output and then (after a barrier, in place) the bordered
+// L1 output: [(4*NB + 2) rows][PJ][48] (a 96-byte position stride, no
+// swizzle); BD the bordered boards [C][(H+2)^2] bf16.
+// Row tiles are 4 x 4 blocks of output positions (NB = ceil(H/4) blocks a side;
+// positions past H are computed on zeros and never stored). With the 96-byte
+// stride and PJ = 28 every fragment read of a tile, at every kernel offset,
+// puts each ds_read_b128 lane group on 16 distinct bank quads (the lane groups
+// simulated), and the address of a read is one lane-constant register plus a
+// wave-uniform offset (tile, kernel offset): no per-read address arithmetic.
 // Every MFMA is v_mfma_f32_16x16x32_bf16 with the WEIGHTS as the A operand
 // (rows = output channels) and the activations as B (columns = positions), so a
 // lane's accumulator holds 4 consecutive channels of one position: the
-// epilogues store 8 bytes per lane. Work split: row tile t (16 positions) goes
-// to SIMD t % 4 (waves w and w + 4 share a SIMD): L0 wave half h = w >> 2 takes
-// column tile h of the SIMD's tiles; L1 the two halves split the SIMD's tiles,
-// both column tiles each; L2 both halves run all the SIMD's tiles, column tiles
-// 2h, 2h + 1 each. At 20x20: 25 tiles = 7/6/6/6 per SIMD.
+// epilogues store 8 bytes per lane. Work split: row tile t goes to SIMD t % 4
+// (waves w and w + 4 share a SIMD): L0 wave half h = w >> 2 takes column tile
+// h of the SIMD's tiles; L1 the two halves split the SIMD's tiles, both column
+// tiles each; L2 both halves run all the SIMD's tiles, column tiles 2h, 2h + 1.
+// At 20x20: 25 tiles = 7/6/6/6 per SIMD.
 // L0 on the matrix cores: the boards (-1 .. 2) and the bf16-rounded weights are
 // exact bf16, so every product is exact; only the fp32 summation order differs
 // from the VALU form (bias added last).
@@ -312,11 +332,15 @@ __global__ __launch_bounds__(64 * NW) void deep_conv_kernel(const uint16_t *__re
 // them); L2's output always goes to a2 [S][H^2][64].
 template <int H>
 struct DeepFrontShape {
-    static constexpr int HB = H + 2, M = H * H, TILES = (M + 15) / 16, TPS = (TILES + 3) / 4, HALF = (TPS + 1) / 2;
-    static constexpr int ST = 40;
-    static constexpr int W1 = 9 * 32 * ST, W2 = 9 * 64 * ST, W0 = 32 * ST, X = HB * HB * ST, BD = 2 * HB * HB;
-    static constexpr int LDS = (W1 + W2 + W0 + 2 * X + BD) * 2;
+    static constexpr int HB = H + 2, M = H * H, NB = (H + 3) / 4, TILES = NB * NB, TPS = (TILES + 3) / 4;
+    static constexpr int HALF = (TPS + 1) / 2;
+    static constexpr int XR = 4 * NB + 2, PJ = XR + (12 - XR % 8) % 8;   // the smallest pitch >= XR, = 4 (mod 8)
+    static constexpr int XST = 48;                                        // halves per X position
+    static constexpr int W1 = 9 * 32 * 32, W2 = 9 * 64 * 32, W0 = 32 * 32, X = XR * PJ * XST, BD = 2 * HB * HB;
+    static constexpr int LDS = (W1 + W2 + W0 + X + BD) * 2;
 };
+// 16-byte chunk c of a 64-byte weight row
+__device__ __forceinline__ int dfr_slot(int row, int c) { return row * 32 + 8 * (c ^ ((row >> 1) & 3)); }
 
 template <int C, int H, bool KEEP>
 __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const float *__restrict__ img0,
@@ -327,46 +351,52 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                                                          uint16_t *__restrict__ a1, uint16_t *__restrict__ a2,
                                                          int64_t S) {
     using Sh = DeepFrontShape<H>;
-    constexpr int HB = Sh::HB, M = Sh::M, TILES = Sh::TILES, TPS = Sh::TPS, HALF = Sh::HALF, ST = Sh::ST;
-    constexpr int PL = HB * HB, NBV = (C * M + 511) / 512;
+    constexpr int HB = Sh::HB, M = Sh::M, NB = Sh::NB, TILES = Sh::TILES, TPS = Sh::TPS, HALF = Sh::HALF;
+    constexpr int PJ = Sh::PJ, XST = Sh::XST, PL = HB * HB, NBV = (C * M + 511) / 512;
     static_assert(9 * C <= 32, "L0 fan-in beyond one k step");
+    static_assert(PJ % 8 == 4 && PJ >= Sh::XR, "image pitch");
     extern __shared__ __attribute__((aligned(16))) uint16_t fsm[];
-    uint16_t *W1s = fsm, *W2s = W1s + Sh::W1, *W0s = W2s + Sh::W2, *X0 = W0s + Sh::W0, *X1 = X0 + Sh::X,
-             *BD = X1 + Sh::X;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint16_t *W1s = fsm, *W2s = W1s + Sh::W1, *W0s = W2s + Sh::W2, *X = W0s + Sh::W0, *BD = X + Sh::X;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: tile offsets stay scalar
     const int r = lane & 15, g = lane >> 4, simd = wave & 3, half = wave >> 2;
-    // ---- weights, zero borders
+    // ---- weights (rows of 32 ci: four swizzled chunks), zeroed image and boards
     for (int q = tid; q < 9 * 32 * 4; q += 512)
-        *reinterpret_cast<u32x4 *>(W1s + (q >> 2) * ST + (q & 3) * 8) = reinterpret_cast<const u32x4 *>(wimg1)[q];
+        *reinterpret_cast<u32x4 *>(W1s + dfr_slot(q >> 2, q & 3)) = reinterpret_cast<const u32x4 *>(wimg1)[q];
     for (int q = tid; q < 9 * 64 * 4; q += 512)
-        *reinterpret_cast<u32x4 *>(W2s + (q >> 2) * ST + (q & 3) * 8) = reinterpret_cast<const u32x4 *>(wimg2)[q];
+        *reinterpret_cast<u32x4 *>(W2s + dfr_slot(q >> 2, q & 3)) = reinterpret_cast<const u32x4 *>(wimg2)[q];
     for (int q = tid; q < 32 * 32; q += 512) {
         const int co = q >> 5, k = q & 31;
-        W0s[co * ST + k] = k < 9 * C ? f2bf(img0[k * 32 + co]) : (uint16_t)0;
+        W0s[dfr_slot(co, k >> 3) + (k & 7)] = k < 9 * C ? f2bf(img0[k * 32 + co]) : (uint16_t)0;
     }
-    for (int q = tid; q < (2 * Sh::X + Sh::BD) / 8; q += 512)   // X0, X1, BD are contiguous
-        *reinterpret_cast<u32x4 *>(X0 + q * 8) = u32x4{0u, 0u, 0u, 0u};
+    for (int q = tid; q < (Sh::X + Sh::BD) / 8; q += 512)   // X, BD are contiguous
+        *reinterpret_cast<u32x4 *>(X + q * 8) = u32x4{0u, 0u, 0u, 0u};
     // per-lane biases of the channels this lane's accumulators hold (4g + e of a column tile)
-    float b0[4], b1[2][4], b2[2][4];
+    const f32x4 b0 = *reinterpret_cast<const f32x4 *>(img0 + 9 * C * 32 + half * 16 + 4 * g);
+    f32x4 b1[2], b2[2];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        b0[e] = img0[9 * C * 32 + half * 16 + 4 * g + e];
-#pragma unroll
-        for (int c2 = 0; c2 < 2; ++c2) {
-            b1[c2][e] = bias1[c2 * 16 + 4 * g + e];
-            b2[c2][e] = bias2[(2 * half + c2) * 16 + 4 * g + e];
-        }
+    for (int c2 = 0; c2 < 2; ++c2) {
+        b1[c2] = *reinterpret_cast<const f32x4 *>(bias1 + c2 * 16 + 4 * g);
+        b2[c2] = *reinterpret_cast<const f32x4 *>(bias2 + (2 * half + c2) * 16 + 4 * g);
     }
-    // bordered base of this lane's position in row tile t (clamped past M)
-    auto xbase = [&](int t) __attribute__((always_inline)) {
-        const int p = min(t * 16 + r, M - 1);
-        return ((p % H) + (p / H) * HB) * ST + 8 * g;
-    };
-    auto pack4 = [](const f32x4 &v, const float (&b)[4]) __attribute__((always_inline)) {
-        u32x2 o;
-        o[0] = (uint32_t)f2bf(fmaxf(v[0] + b[0], 0.f)) | ((uint32_t)f2bf(fmaxf(v[1] + b[1], 0.f)) << 16);
-        o[1] = (uint32_t)f2bf(fmaxf(v[2] + b[2], 0.f)) | ((uint32_t)f2bf(fmaxf(v[3] + b[3], 0.f)) << 16);
-        return o;
+    // lane-constant parts of the addresses: weight fragment (row 16*tile + r, chunk g);
+    // X fragment (position (r & 3, r >> 2) of a tile, chunk g); the L0 board gather
+    // (k = 8g + e -> channel k % C, kernel offset k / C; -1 past 9C)
+    const int wl = r * 32 + 8 * (g ^ ((r >> 1) & 3));
+    const int xl = ((r & 3) + (r >> 2) * PJ) * XST + 8 * g;
+    int bofs[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int k = 8 * g + e, kk = k / C, c = k - kk * C;
+        bofs[e] = k < 9 * C ? c * PL + kk % 3 + (kk / 3) * HB : -1;
+    }
+    static_assert(4 * (TPS - 1) < TILES, "tiles 0 .. TPS-2 of every SIMD exist");
+    const bool last_ok = simd + 4 * (TPS - 1) < TILES;   // only a SIMD's last tile can be missing
+    // wave-uniform top-left position (bordered image) of row tile t
+    auto tbase = [&](int t) __attribute__((always_inline)) { return 4 * (t % NB) + 4 * (t / NB) * PJ; };
+    auto tpos = [&](int t, int &i, int &j) __attribute__((always_inline)) {
+        i = 4 * (t % NB) + (r & 3);
+        j = 4 * (t / NB) + (r >> 2);
     };
     float bv[NBV];
     auto bload = [&](int64_t s) __attribute__((always_inline)) {
@@ -388,74 +418,70 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                 BD[c * PL + (cell % H + 1) + (cell / H + 1) * HB] = f2bf(bv[u]);
             }
         }
-        __syncthreads();   // boards in; X0 free (last read by the previous sample's L1)
+        __syncthreads();   // boards in; X free (last read by the previous sample's L2)
         // ---- L0: column tile `half` of the SIMD's row tiles
         {
-            const bf16x8 wa = as_bf(*reinterpret_cast<const u32x4 *>(W0s + (half * 16 + r) * ST + 8 * g));
+            const bf16x8 wa = as_bf(*reinterpret_cast<const u32x4 *>(W0s + half * 16 * 32 + wl));
 #pragma unroll
-            for (int i = 0; i < TPS; ++i) {
-                const int t = simd + 4 * i;
-                if (t >= TILES) continue;
-                const int pr = t * 16 + r, p = min(pr, M - 1), pi = p % H, pj = p / H;
+            for (int ii = 0; ii < TPS; ++ii) {
+                const int t = simd + 4 * ii;
+                if (ii == TPS - 1 && !last_ok) continue;
+                int i, j;
+                tpos(t, i, j);
+                const int bb = min(i, H - 1) + min(j, H - 1) * HB;
                 uint32_t w[4];
 #pragma unroll
                 for (int e2 = 0; e2 < 4; ++e2) {
-                    uint32_t v2 = 0;
-#pragma unroll
-                    for (int o = 0; o < 2; ++o) {
-                        const int k = 8 * g + 2 * e2 + o;
-                        const int kk = k / C, c = k - kk * C;
-                        const uint32_t v = k < 9 * C ? BD[c * PL + (pi + kk % 3) + (pj + kk / 3) * HB] : 0u;
-                        v2 |= v << (16 * o);
-                    }
-                    w[e2] = v2;
+                    const uint32_t v0 = bofs[2 * e2] >= 0 ? BD[bb + bofs[2 * e2]] : 0u;
+                    const uint32_t v1 = bofs[2 * e2 + 1] >= 0 ? BD[bb + bofs[2 * e2 + 1]] : 0u;
+                    w[e2] = v0 | (v1 << 16);
                 }
                 const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, as_bf(u32x4{w[0], w[1], w[2], w[3]}),
                                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                if (pr < M) {
-                    const u32x2 o = pack4(acc, b0);
-                    *reinterpret_cast<u32x2 *>(X0 + ((pi + 1) + (pj + 1) * HB) * ST + half * 16 + 4 * g) = o;
-                    if (KEEP) *reinterpret_cast<u32x2 *>(a0 + (s * M + pr) * 32 + half * 16 + 4 * g) = o;
+                if (i < H && j < H) {
+                    const u32x2 o = relu_bf16x4(acc, b0);
+                    *reinterpret_cast<u32x2 *>(X + ((i + 1) + (j + 1) * PJ) * XST + half * 16 + 4 * g) = o;
+                    if (KEEP) *reinterpret_cast<u32x2 *>(a0 + (s * M + i + j * H) * 32 + half * 16 + 4 * g) = o;
                 }
             }
         }
         __syncthreads();
-        // ---- L1: this half's share of the SIMD's row tiles, both column tiles
+        // ---- L1: this half's share of the SIMD's row tiles, both column tiles; the
+        // result replaces L0's in X after a barrier
         {
             f32x4 acc[HALF][2];
-            int xb[HALF];
 #pragma unroll
-            for (int ii = 0; ii < HALF; ++ii) {
-                xb[ii] = xbase(simd + 4 * (half * HALF + ii));
-                acc[ii][0] = acc[ii][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll 1
+            for (int ii = 0; ii < HALF; ++ii) acc[ii][0] = acc[ii][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
             for (int kk = 0; kk < 9; ++kk) {
-                const int koff = ((kk % 3) + (kk / 3) * HB) * ST;
+                const int koff = ((kk % 3) + (kk / 3) * PJ) * XST;
                 bf16x8 wa[2];
 #pragma unroll
                 for (int c2 = 0; c2 < 2; ++c2)
-                    wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(W1s + (kk * 32 + c2 * 16 + r) * ST + 8 * g));
+                    wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(W1s + (kk * 32 + c2 * 16) * 32 + wl));
 #pragma unroll
                 for (int ii = 0; ii < HALF; ++ii) {
                     const int i = half * HALF + ii, t = simd + 4 * i;
-                    if (i >= TPS || t >= TILES) continue;
-                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(X0 + xb[ii] + koff));
+                    if (i >= TPS || (i == TPS - 1 && !last_ok)) continue;
+                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(X + xl + tbase(t) * XST + koff));
 #pragma unroll
                     for (int c2 = 0; c2 < 2; ++c2)
                         acc[ii][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[ii][c2], 0, 0, 0);
                 }
             }
+            __syncthreads();   // every wave's L1 reads of X are done: X takes the L1 output
 #pragma unroll
             for (int ii = 0; ii < HALF; ++ii) {
-                const int i = half * HALF + ii, t = simd + 4 * i, pr = t * 16 + r;
-                if (i >= TPS || t >= TILES || pr >= M) continue;
-                const int pi = pr % H, pj = pr / H;
+                const int i2 = half * HALF + ii, t = simd + 4 * i2;
+                if (i2 >= TPS || (i2 == TPS - 1 && !last_ok)) continue;
+                int i, j;
+                tpos(t, i, j);
+                if (i >= H || j >= H) continue;
 #pragma unroll
                 for (int c2 = 0; c2 < 2; ++c2) {
-                    const u32x2 o = pack4(acc[ii][c2], b1[c2]);
-                    *reinterpret_cast<u32x2 *>(X1 + ((pi + 1) + (pj + 1) * HB) * ST + c2 * 16 + 4 * g) = o;
-                    if (KEEP) *reinterpret_cast<u32x2 *>(a1 + (s * M + pr) * 32 + c2 * 16 + 4 * g) = o;
+                    const u32x2 o = relu_bf16x4(acc[ii][c2], b1[c2]);
+                    *reinterpret_cast<u32x2 *>(X + ((i + 1) + (j + 1) * PJ) * XST + c2 * 16 + 4 * g) = o;
+                    if (KEEP) *reinterpret_cast<u32x2 *>(a1 + (s * M + i + j * H) * 32 + c2 * 16 + 4 * g) = o;
                 }
             }
         }
@@ -464,36 +490,35 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
         // ---- L2: all the SIMD's row tiles, column tiles 2*half, 2*half + 1
         {
             f32x4 acc[TPS][2];
-            int xb[TPS];
 #pragma unroll
-            for (int i = 0; i < TPS; ++i) {
-                xb[i] = xbase(simd + 4 * i);
-                acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll 1
+            for (int ii = 0; ii < TPS; ++ii) acc[ii][0] = acc[ii][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
             for (int kk = 0; kk < 9; ++kk) {
-                const int koff = ((kk % 3) + (kk / 3) * HB) * ST;
+                const int koff = ((kk % 3) + (kk / 3) * PJ) * XST;
                 bf16x8 wa[2];
 #pragma unroll
                 for (int c2 = 0; c2 < 2; ++c2)
-                    wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(W2s + (kk * 64 + (2 * half + c2) * 16 + r) * ST + 8 * g));
+                    wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(W2s + (kk * 64 + (2 * half + c2) * 16) * 32 + wl));
 #pragma unroll
-                for (int i = 0; i < TPS; ++i) {
-                    if (simd + 4 * i >= TILES) continue;
-                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(X1 + xb[i] + koff));
+                for (int ii = 0; ii < TPS; ++ii) {
+                    const int t = simd + 4 * ii;
+                    if (ii == TPS - 1 && !last_ok) continue;
+                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(X + xl + tbase(t) * XST + koff));
 #pragma unroll
                     for (int c2 = 0; c2 < 2; ++c2)
-                        acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[i][c2], 0, 0, 0);
+                        acc[ii][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[ii][c2], 0, 0, 0);
                 }
             }
 #pragma unroll
-            for (int i = 0; i < TPS; ++i) {
-                const int pr = (simd + 4 * i) * 16 + r;
-                if (simd + 4 * i >= TILES || pr >= M) continue;
+            for (int ii = 0; ii < TPS; ++ii) {
+                if (ii == TPS - 1 && !last_ok) continue;
+                int i, j;
+                tpos(simd + 4 * ii, i, j);
+                if (i >= H || j >= H) continue;
 #pragma unroll
                 for (int c2 = 0; c2 < 2; ++c2)
-                    *reinterpret_cast<u32x2 *>(a2 + (s * M + pr) * 64 + (2 * half + c2) * 16 + 4 * g) =
-                        pack4(acc[i][c2], b2[c2]);
+                    *reinterpret_cast<u32x2 *>(a2 + (s * M + i + j * H) * 64 + (2 * half + c2) * 16 + 4 * g) =
+                        relu_bf16x4(acc[ii][c2], b2[c2]);
             }
         }
     }
@@ -502,24 +527,33 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
 // ---------------------------------------------------------------- L3 (MFMA, two samples)
 // deep_conv3_kernel: L3 (6x6, 64 -> 64, valid) for TWO samples per step of a
 // persistent workgroup (one per CU, 8 waves), so each kernel offset's 8 KB of
-// weights, staged through LDS, serves both: the weight stream from L2 is half
-// of deep_conv_kernel's one-sample form (295 KB per sample there). LDS: the
-// pair's inputs [2][H*H][72] (115 KB at 20x20) and the weights of two offsets
-// [co][72] double buffered. The 2*WO^2 output positions of the pair are packed
-// into row tiles of 16 across the samples (29 tiles at 20x20 instead of 2 x 15);
-// row tile t goes to SIMD t % 4, wave half h takes column tiles 2h, 2h + 1.
-// The NEXT pair's inputs are loaded into registers during the first offsets of
-// this pair (one 16-byte piece per thread per offset, behind that offset's
-// weight load) and parked in LDS after the last offset's barrier.
+// weights, staged through LDS, serves both. LDS: the pair's inputs
+// [2][H rows][PJ = 24][64] and the weights of two stages of two kernel offsets
+// [2][co][64], double buffered (155 KB at 20x20: 18 barriers per pair); every
+// row is 128 bytes (eight 16-byte chunks) with chunk c of row `row` at slot
+// c ^ (row & 7). A row tile is one output row of one sample: 16 consecutive
+// output columns (WO = 15 at 20x20: the 16th is computed and dropped), so each
+// fragment read covers 16 consecutive LDS rows, which the swizzle puts on 16
+// distinct bank quads. PJ and H*PJ are multiples of 8, so row & 7 =
+// (lane + du) & 7: one lane-constant address per kernel offset and 32-channel
+// step, plus a wave-uniform tile offset.
+// Row tile t of the pair (2*WO of them) goes to SIMD t % 4, wave half h takes
+// column tiles 2h, 2h + 1: per 32-channel step 2 weight + up to 8 activation
+// fragment reads for 16 MFMAs per wave.
+// The NEXT pair's inputs are loaded into registers during the first stages of
+// this pair (one 16-byte piece per thread per stage, behind that stage's
+// weight loads; the pieces past the register budget at the end) and parked in
+// LDS after the last stage's barrier.
 // MFMA operands as deep_front_kernel: weights A (rows = channels), activations
 // B, 8-byte epilogue stores of 4 channels.
 template <int H>
 struct DeepL3Shape {
-    static constexpr int WO = H - 5, MS = WO * WO, M = 2 * MS, TILES = (M + 15) / 16, TPS = (TILES + 3) / 4;
-    static constexpr int CST = 72, XS = H * H * CST, B_ELEMS = 64 * CST;
+    static constexpr int WO = H - 5, TILES = 2 * WO, TPS = (TILES + 3) / 4, PJ = (H + 1 + 7) / 8 * 8;
+    static constexpr int XS = H * PJ * 64, B_ELEMS = 2 * 64 * 64;   // a stage: two kernel offsets
     static constexpr int LDS = (2 * XS + 2 * B_ELEMS) * 2;
     static constexpr int APIECES = 2 * H * H * 8, APT = (APIECES + 511) / 512;
 };
+__device__ __forceinline__ int dl3_slot(int row, int c) { return row * 64 + 8 * (c ^ (row & 7)); }
 
 template <int H>
 __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restrict__ x,
@@ -527,12 +561,14 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
                                                          const float *__restrict__ bias, uint16_t *__restrict__ y,
                                                          int64_t S) {
     using Sh = DeepL3Shape<H>;
-    constexpr int WO = Sh::WO, MS = Sh::MS, M = Sh::M, TILES = Sh::TILES, TPS = Sh::TPS, CST = Sh::CST;
-    constexpr int XS = Sh::XS, APT = Sh::APT, APIECES = Sh::APIECES;
-    static_assert(APT <= 36, "input prefetch spans more offsets than the layer has");
+    constexpr int WO = Sh::WO, TILES = Sh::TILES, TPS = Sh::TPS, PJ = Sh::PJ;
+    constexpr int APT = Sh::APT, APIECES = Sh::APIECES;
+    constexpr int APF = APT < 9 ? APT : 9;   // pieces prefetched into registers (the rest: at the end)
+    static_assert(WO <= 16 && PJ % 8 == 0 && PJ > H, "one output row per row tile");
     extern __shared__ __attribute__((aligned(16))) uint16_t l3sm[];
-    uint16_t *As = l3sm, *Bs = l3sm + 2 * XS;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint16_t *As = l3sm, *Bs = l3sm + 2 * Sh::XS;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 15, g = lane >> 4, simd = wave & 3, half = wave >> 2;
     const int64_t npairs = (S + 1) / 2;
     // input piece q of pair p: sample 2p + q / (H*H*8) (clamped to S - 1), position, 16-byte chunk
@@ -545,90 +581,108 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
     auto apark = [&](int u, const u32x4 &v) __attribute__((always_inline)) {
         const int q = tid + u * 512;
         const int smp = q / (H * H * 8), rem = q - smp * (H * H * 8);
-        *reinterpret_cast<u32x4 *>(As + smp * XS + (rem >> 3) * CST + (rem & 7) * 8) = v;
+        const int pos = rem >> 3;   // rows are numbered across the pair (the swizzle uses the pair-wide row)
+        *reinterpret_cast<u32x4 *>(As + dl3_slot(smp * (H * PJ) + (pos % H) + (pos / H) * PJ, rem & 7)) = v;
     };
-    // one offset's weights: 512 pieces of 16 bytes, one per thread
-    auto bload = [&](int kk) __attribute__((always_inline)) {
-        return reinterpret_cast<const u32x4 *>(wimg + (int64_t)kk * 64 * 64)[tid];
+    // one stage (kernel offsets 2m, 2m+1): 1024 pieces of 16 bytes, two per thread
+    auto bload = [&](int m, u32x4 (&v)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) v[u] = reinterpret_cast<const u32x4 *>(wimg + (int64_t)(2 * m + u) * 64 * 64)[tid];
     };
-    auto bstore = [&](int buf, const u32x4 &v) __attribute__((always_inline)) {
-        *reinterpret_cast<u32x4 *>(Bs + buf * Sh::B_ELEMS + (tid >> 3) * CST + (tid & 7) * 8) = v;
+    auto bstore = [&](int buf, const u32x4 (&v)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            *reinterpret_cast<u32x4 *>(Bs + buf * Sh::B_ELEMS + u * 64 * 64 + dl3_slot(tid >> 3, tid & 7)) = v[u];
     };
-    float bb[2][4];
-#pragma unroll
-    for (int c2 = 0; c2 < 2; ++c2)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bb[c2][e] = bias[(2 * half + c2) * 16 + 4 * g + e];
-    // this lane's A row base per row tile (position packed across the pair, clamped past M)
-    int abase[TPS];
-#pragma unroll
-    for (int i = 0; i < TPS; ++i) {
-        const int q = min((simd + 4 * i) * 16 + r, M - 1);
-        const int smp = q / MS, o = q - smp * MS;
-        abase[i] = smp * XS + ((o % WO) + (o / WO) * H) * CST + 8 * g;
-    }
+    // weight fragment of column tile ct, 32-channel step c: row ct*16 + r, chunk 4c + g
+    const int wl0 = r * 64 + 8 * (g ^ (r & 7)), wl1 = r * 64 + 8 * ((4 + g) ^ (r & 7));
+    // wave-uniform first input row of row tile t (sample t / WO, output row t % WO)
+    auto trow = [&](int t) __attribute__((always_inline)) { return (t / WO) * (H * PJ) + (t % WO) * PJ; };
+    static_assert(4 * (TPS - 1) < TILES, "tiles 0 .. TPS-2 of every SIMD exist");
+    const bool last_ok = simd + 4 * (TPS - 1) < TILES;
     int64_t p = blockIdx.x;
     if (p < npairs) {
 #pragma unroll
         for (int u = 0; u < APT; ++u)
             if (tid + u * 512 < APIECES) apark(u, apiece(p, u));
-        bstore(0, bload(0));
+        u32x4 b0[2];
+        bload(0, b0);
+        bstore(0, b0);
     }
     __syncthreads();
     for (; p < npairs; p += gridDim.x) {
         const bool more = p + gridDim.x < npairs;
-        u32x4 apf[APT];
+        const int64_t pn = p + gridDim.x;
+        u32x4 apf[APF];
         f32x4 acc[TPS][2];
 #pragma unroll
         for (int i = 0; i < TPS; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-        for (int kk = 0; kk < 36; ++kk) {
-            const u32x4 bn = bload(kk + 1 < 36 ? kk + 1 : 0);   // the next offset (offset 0 of the next pair)
-#pragma unroll
-            for (int u = 0; u < APT; ++u)
-                if (u == kk && more && tid + u * 512 < APIECES) apf[u] = apiece(p + gridDim.x, u);
-            const int koff = ((kk % 6) + (kk / 6) * H) * CST;
-            const uint16_t *Bc = Bs + (kk & 1) * Sh::B_ELEMS;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                bf16x8 wa[2];
-#pragma unroll
-                for (int c2 = 0; c2 < 2; ++c2)
-                    wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(Bc + ((2 * half + c2) * 16 + r) * CST + c * 32 + 8 * g));
-#pragma unroll
-                for (int i = 0; i < TPS; ++i) {
-                    if (simd + 4 * i >= TILES) continue;
-                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(As + abase[i] + koff + c * 32));
-#pragma unroll
-                    for (int c2 = 0; c2 < 2; ++c2)
-                        acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[i][c2], 0, 0, 0);
+        for (int m = 0; m < 18; ++m) {
+            u32x4 bn[2];
+            bload(m + 1 < 18 ? m + 1 : 0, bn);   // the next stage (stage 0 of the next pair)
+            if (more) {   // the next pair's inputs, one piece per thread per stage
+                switch (m) {
+#define DL3_PF(U) \
+    case U:       \
+        if (U < APF && tid + (U) * 512 < APIECES) apf[U < APF ? U : 0] = apiece(pn, U); \
+        break;
+                    DL3_PF(0) DL3_PF(1) DL3_PF(2) DL3_PF(3) DL3_PF(4) DL3_PF(5) DL3_PF(6) DL3_PF(7) DL3_PF(8)
+#undef DL3_PF
+                    default: break;
                 }
             }
-            bstore((kk + 1) & 1, bn);
+#pragma unroll
+            for (int o = 0; o < 2; ++o) {
+                const int kk = 2 * m + o, du = kk % 6, dv = kk / 6;
+                const int sw = (r + du) & 7;
+                const int xl0 = (r + du) * 64 + 8 * (g ^ sw), xl1 = (r + du) * 64 + 8 * ((4 + g) ^ sw);
+                const uint16_t *Bc = Bs + (m & 1) * Sh::B_ELEMS + o * 64 * 64;
+                const uint16_t *Ak = As + dv * PJ * 64;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    bf16x8 wa[2];
+#pragma unroll
+                    for (int c2 = 0; c2 < 2; ++c2)
+                        wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(Bc + (2 * half + c2) * 16 * 64 + (c ? wl1 : wl0)));
+#pragma unroll
+                    for (int i = 0; i < TPS; ++i) {
+                        const int t = simd + 4 * i;
+                        if (i == TPS - 1 && !last_ok) continue;   // only the last tile can be missing
+                        const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(Ak + trow(t) * 64 + (c ? xl1 : xl0)));
+#pragma unroll
+                        for (int c2 = 0; c2 < 2; ++c2)
+                            acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[i][c2], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);   // the next step's reads after these MFMAs (registers)
+                }
+            }
+            bstore((m + 1) & 1, bn);
             __syncthreads();
         }
         // epilogue: bias + relu + bf16, 4 channels per lane
 #pragma unroll
         for (int i = 0; i < TPS; ++i) {
-            const int q = (simd + 4 * i) * 16 + r;
-            if (simd + 4 * i >= TILES || q >= M) continue;
-            const int smp = q / MS, o = q - smp * MS;
-            const int64_t sg = 2 * p + smp;
+            const int t = simd + 4 * i;
+            if ((i == TPS - 1 && !last_ok) || r >= WO) continue;
+            const int64_t sg = 2 * p + t / WO;
             if (sg >= S) continue;
+            const int o = r + (t % WO) * WO;
 #pragma unroll
             for (int c2 = 0; c2 < 2; ++c2) {
-                const f32x4 v = acc[i][c2];
-                u32x2 w;
-                w[0] = (uint32_t)f2bf(fmaxf(v[0] + bb[c2][0], 0.f)) | ((uint32_t)f2bf(fmaxf(v[1] + bb[c2][1], 0.f)) << 16);
-                w[1] = (uint32_t)f2bf(fmaxf(v[2] + bb[c2][2], 0.f)) | ((uint32_t)f2bf(fmaxf(v[3] + bb[c2][3], 0.f)) << 16);
-                *reinterpret_cast<u32x2 *>(y + (sg * MS + o) * 64 + (2 * half + c2) * 16 + 4 * g) = w;
+                const f32x4 bb = *reinterpret_cast<const f32x4 *>(bias + (2 * half + c2) * 16 + 4 * g);
+                *reinterpret_cast<u32x2 *>(y + (sg * WO * WO + o) * 64 + (2 * half + c2) * 16 + 4 * g) =
+                    relu_bf16x4(acc[i][c2], bb);
             }
         }
-        // the next pair's inputs (every wave passed the last offset's barrier: A is free)
+        // the next pair's inputs (every wave passed the last stage's barrier: A is free)
         if (more) {
 #pragma unroll
-            for (int u = 0; u < APT; ++u)
+            for (int u = 0; u < APF; ++u)
                 if (tid + u * 512 < APIECES) apark(u, apf[u]);
+#pragma unroll
+            for (int u = APF; u < APT; ++u)   // the pieces past the register budget: loaded here
+                if (tid + u * 512 < APIECES) apark(u, apiece(pn, u));
         }
         __syncthreads();
     }

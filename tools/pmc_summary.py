@@ -6,7 +6,9 @@ usage: python tools/pmc_summary.py <pmc dir> <out.json> [kernel substrings...]
 
 mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x 2.4 GHz x the dispatch's
 duration in the same pass (End - Start timestamps)): the fraction of the
-nominal dense MFMA peak;
+nominal dense MFMA peak; clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / duration and
+mfma_busy_at_clock the same fraction at that clock; wait_*_frac = the SQ wait
+counters over SQ_WAVE_CYCLES;
 hbm_bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB; FETCH_SIZE doubled per
 MI355X_MICROARCH.md's gfx950 note); all per launch (mean over launches).
 """
@@ -43,6 +45,14 @@ def main():
         cyc = c.get("duration_ns", 0) * 2.4
         if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
             row["mfma_busy"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc)
+        if cyc and "GRBM_GUI_ACTIVE" in c:   # summed over the 8 XCDs (pass p2; duration from p1)
+            row["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8.0 / c["duration_ns"]
+            if "mfma_busy" in row:
+                row["mfma_busy_at_clock"] = row["mfma_busy"] * 2.4 / row["clock_ghz"]
+        if "SQ_WAVE_CYCLES" in c and c["SQ_WAVE_CYCLES"]:
+            row["wait_inst_any_frac"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+            row["wait_lds_frac"] = c.get("SQ_WAIT_INST_LDS", 0) / c["SQ_WAVE_CYCLES"]
+            row["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             row["hbm_bytes"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
         if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c and c["SQ_LDS_IDX_ACTIVE"]:
