@@ -526,31 +526,32 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
 
 // ---------------------------------------------------------------- L3 (MFMA, two samples)
 // deep_conv3_kernel: L3 (6x6, 64 -> 64, valid) for TWO samples per step of a
-// persistent workgroup (one per CU, 8 waves), so each kernel offset's 8 KB of
-// weights, staged through LDS, serves both. LDS: the pair's inputs
-// [2][H rows][PJ = 24][64] and the weights of two stages of two kernel offsets
-// [2][co][64], double buffered (155 KB at 20x20: 18 barriers per pair); every
-// row is 128 bytes (eight 16-byte chunks) with chunk c of row `row` at slot
-// c ^ (row & 7). A row tile is one output row of one sample: 16 consecutive
-// output columns (WO = 15 at 20x20: the 16th is computed and dropped), so each
+// persistent workgroup (one per CU, 8 waves). LDS holds only the pair's
+// inputs [2][H rows][PJ = 24][64] (123 KB at 20x20); every row is 128 bytes
+// (eight 16-byte chunks) with chunk c of row `row` at slot c ^ (row & 7). The
+// weights go straight from global (L2-resident, 295 KB) into registers, two
+// kernel offsets ahead, so the 36 offsets run without a single barrier (the
+// LDS-staged form paid one per stage: 36 barriers per pair -> 5.7 ms, 18 ->
+// 5.1 ms). A row tile is one output row of one sample: 16 consecutive output
+// columns (WO = 15 at 20x20: the 16th is computed and dropped), so each
 // fragment read covers 16 consecutive LDS rows, which the swizzle puts on 16
 // distinct bank quads. PJ and H*PJ are multiples of 8, so row & 7 =
 // (lane + du) & 7: one lane-constant address per kernel offset and 32-channel
 // step, plus a wave-uniform tile offset.
 // Row tile t of the pair (2*WO of them) goes to SIMD t % 4, wave half h takes
-// column tiles 2h, 2h + 1: per 32-channel step 2 weight + up to 8 activation
-// fragment reads for 16 MFMAs per wave.
-// The NEXT pair's inputs are loaded into registers during the first stages of
-// this pair (one 16-byte piece per thread per stage, behind that stage's
-// weight loads; the pieces past the register budget at the end) and parked in
-// LDS after the last stage's barrier.
+// column tiles 2h, 2h + 1: per kernel offset 4 weight fragments (global) and
+// 2 x up to 8 activation fragments (LDS) for 32 MFMAs per wave.
+// The next pair's inputs are loaded and parked between the pair's two barriers
+// (prefetching them into registers during the offsets cost more than it hid:
+// 5.05 against 4.95 ms, the slow HBM loads holding up the in-order vmcnt waits
+// of the weight loads queued behind them).
 // MFMA operands as deep_front_kernel: weights A (rows = channels), activations
 // B, 8-byte epilogue stores of 4 channels.
 template <int H>
 struct DeepL3Shape {
     static constexpr int WO = H - 5, TILES = 2 * WO, TPS = (TILES + 3) / 4, PJ = (H + 1 + 7) / 8 * 8;
-    static constexpr int XS = H * PJ * 64, B_ELEMS = 2 * 64 * 64;   // a stage: two kernel offsets
-    static constexpr int LDS = (2 * XS + 2 * B_ELEMS) * 2;
+    static constexpr int XS = H * PJ * 64;
+    static constexpr int LDS = 2 * XS * 2;
     static constexpr int APIECES = 2 * H * H * 8, APT = (APIECES + 511) / 512;
 };
 __device__ __forceinline__ int dl3_slot(int row, int c) { return row * 64 + 8 * (c ^ (row & 7)); }
@@ -563,10 +564,9 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
     using Sh = DeepL3Shape<H>;
     constexpr int WO = Sh::WO, TILES = Sh::TILES, TPS = Sh::TPS, PJ = Sh::PJ;
     constexpr int APT = Sh::APT, APIECES = Sh::APIECES;
-    constexpr int APF = APT < 9 ? APT : 9;   // pieces prefetched into registers (the rest: at the end)
     static_assert(WO <= 16 && PJ % 8 == 0 && PJ > H, "one output row per row tile");
     extern __shared__ __attribute__((aligned(16))) uint16_t l3sm[];
-    uint16_t *As = l3sm, *Bs = l3sm + 2 * Sh::XS;
+    uint16_t *As = l3sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 15, g = lane >> 4, simd = wave & 3, half = wave >> 2;
@@ -584,18 +584,16 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         const int pos = rem >> 3;   // rows are numbered across the pair (the swizzle uses the pair-wide row)
         *reinterpret_cast<u32x4 *>(As + dl3_slot(smp * (H * PJ) + (pos % H) + (pos / H) * PJ, rem & 7)) = v;
     };
-    // one stage (kernel offsets 2m, 2m+1): 1024 pieces of 16 bytes, two per thread
-    auto bload = [&](int m, u32x4 (&v)[2]) __attribute__((always_inline)) {
+    // the 4 weight fragments of kernel offset kk this wave uses: [c][c2], row (2h + c2)*16 + r,
+    // channels 32c + 8g .. +7 of the image [kk][co][ci]
+    const uint16_t *wl = wimg + ((2 * half) * 16 + r) * 64 + 8 * g;
+    auto wload = [&](int kk, u32x4 (&f)[4]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) v[u] = reinterpret_cast<const u32x4 *>(wimg + (int64_t)(2 * m + u) * 64 * 64)[tid];
-    };
-    auto bstore = [&](int buf, const u32x4 (&v)[2]) __attribute__((always_inline)) {
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-            *reinterpret_cast<u32x4 *>(Bs + buf * Sh::B_ELEMS + u * 64 * 64 + dl3_slot(tid >> 3, tid & 7)) = v[u];
+            for (int c2 = 0; c2 < 2; ++c2)
+                f[2 * c + c2] = *reinterpret_cast<const u32x4 *>(wl + (int64_t)kk * 64 * 64 + c2 * 16 * 64 + 32 * c);
     };
-    // weight fragment of column tile ct, 32-channel step c: row ct*16 + r, chunk 4c + g
-    const int wl0 = r * 64 + 8 * (g ^ (r & 7)), wl1 = r * 64 + 8 * ((4 + g) ^ (r & 7));
     // wave-uniform first input row of row tile t (sample t / WO, output row t % WO)
     auto trow = [&](int t) __attribute__((always_inline)) { return (t / WO) * (H * PJ) + (t % WO) * PJ; };
     static_assert(4 * (TPS - 1) < TILES, "tiles 0 .. TPS-2 of every SIMD exist");
@@ -605,46 +603,27 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
 #pragma unroll
         for (int u = 0; u < APT; ++u)
             if (tid + u * 512 < APIECES) apark(u, apiece(p, u));
-        u32x4 b0[2];
-        bload(0, b0);
-        bstore(0, b0);
     }
+    u32x4 wf[2][4];   // offsets kk, kk + 1
+    wload(0, wf[0]);
+    wload(1, wf[1]);
     __syncthreads();
     for (; p < npairs; p += gridDim.x) {
         const bool more = p + gridDim.x < npairs;
         const int64_t pn = p + gridDim.x;
-        u32x4 apf[APF];
         f32x4 acc[TPS][2];
 #pragma unroll
         for (int i = 0; i < TPS; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-        for (int m = 0; m < 18; ++m) {
-            u32x4 bn[2];
-            bload(m + 1 < 18 ? m + 1 : 0, bn);   // the next stage (stage 0 of the next pair)
-            if (more) {   // the next pair's inputs, one piece per thread per stage
-                switch (m) {
-#define DL3_PF(U) \
-    case U:       \
-        if (U < APF && tid + (U) * 512 < APIECES) apf[U < APF ? U : 0] = apiece(pn, U); \
-        break;
-                    DL3_PF(0) DL3_PF(1) DL3_PF(2) DL3_PF(3) DL3_PF(4) DL3_PF(5) DL3_PF(6) DL3_PF(7) DL3_PF(8)
-#undef DL3_PF
-                    default: break;
-                }
-            }
+        for (int k2 = 0; k2 < 36; k2 += 2) {
 #pragma unroll
             for (int o = 0; o < 2; ++o) {
-                const int kk = 2 * m + o, du = kk % 6, dv = kk / 6;
+                const int kk = k2 + o, du = kk % 6, dv = kk / 6;
                 const int sw = (r + du) & 7;
                 const int xl0 = (r + du) * 64 + 8 * (g ^ sw), xl1 = (r + du) * 64 + 8 * ((4 + g) ^ sw);
-                const uint16_t *Bc = Bs + (m & 1) * Sh::B_ELEMS + o * 64 * 64;
                 const uint16_t *Ak = As + dv * PJ * 64;
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    bf16x8 wa[2];
-#pragma unroll
-                    for (int c2 = 0; c2 < 2; ++c2)
-                        wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(Bc + (2 * half + c2) * 16 * 64 + (c ? wl1 : wl0)));
 #pragma unroll
                     for (int i = 0; i < TPS; ++i) {
                         const int t = simd + 4 * i;
@@ -652,13 +631,14 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
                         const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(Ak + trow(t) * 64 + (c ? xl1 : xl0)));
 #pragma unroll
                         for (int c2 = 0; c2 < 2; ++c2)
-                            acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[i][c2], 0, 0, 0);
+                            acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wf[o][2 * c + c2]), xv,
+                                                                                 acc[i][c2], 0, 0, 0);
                     }
                     __builtin_amdgcn_sched_barrier(0);   // the next step's reads after these MFMAs (registers)
                 }
+                const int kn = kk + 2 < 36 ? kk + 2 : kk - 34;   // two offsets ahead (wrapping to the next pair)
+                wload(kn, wf[o]);
             }
-            bstore((m + 1) & 1, bn);
-            __syncthreads();
         }
         // epilogue: bias + relu + bf16, 4 channels per lane
 #pragma unroll
@@ -675,13 +655,10 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
                     relu_bf16x4(acc[i][c2], bb);
             }
         }
-        // the next pair's inputs (every wave passed the last stage's barrier: A is free)
-        if (more) {
+        __syncthreads();   // every wave is done reading this pair's inputs
+        if (more) {   // the next pair's inputs
 #pragma unroll
-            for (int u = 0; u < APF; ++u)
-                if (tid + u * 512 < APIECES) apark(u, apf[u]);
-#pragma unroll
-            for (int u = APF; u < APT; ++u)   // the pieces past the register budget: loaded here
+            for (int u = 0; u < APT; ++u)
                 if (tid + u * 512 < APIECES) apark(u, apiece(pn, u));
         }
         __syncthreads();
