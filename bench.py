@@ -135,12 +135,13 @@ def cpu_baseline(args) -> dict:
 
 def _deep_traffic(d: int, n: int, bs: int) -> dict:
     """PMC bytes per launch of the configs[2] dominant layer (the 6x6 64->64 conv,
-    deep_conv_kernel<64, 64, 6, ...>) from profiles/*_deep_traffic.json (tools/pmc_traffic.sh
+    deep_conv3_kernel<20>) from profiles/*_deep_traffic.json (tools/pmc_traffic.sh
     <tag> deep + tools/traffic.py), when this run's dominant layer is that one at 65,536 x 20x20."""
     if d != 3 or n != 65536 or bs != 20:
         return {}
-    t = _latest_traffic("deep_conv_kernel<64, 64, 6", "*_deep_traffic.json")
-    return {"traffic": t["bytes_per_launch"], "traffic_source": t["source"]} if t else {}
+    t = _latest_traffic("deep_conv3_kernel<20>", "*_deep_traffic.json")
+    return ({"traffic": t["bytes_per_launch"], "traffic_source": t["source"],
+             "traffic_over_algorithmic": t["bytes_per_launch"] / t["algorithmic_bytes_per_launch"]} if t else {})
 
 
 def configs2(args, snk, graph) -> dict:

@@ -2,8 +2,8 @@
 # HBM traffic of the two MFMA kernels the bench line prices, from separate counter-only
 # rocprofv3 passes (FETCH_SIZE | WRITE_SIZE): bash tools/pmc_traffic.sh <tag>
 #   act forward at 4096 x 12x12 (conv_h3f_kernel)      -> gpurun_out/<tag>_h3f/p2, p3
-#   Jacobian-Gram D build at n = 50,000 (syrk_h3_kernel) -> gpurun_out/<tag>_syrk/p2, p3
-#   configs[2] act forward at 65,536 x 20x20 (deep_conv_kernel) -> gpurun_out/<tag>_deep/p2, p3
+#   Jacobian-Gram D build at n = 50,000 (syrk_h3q_kernel) -> gpurun_out/<tag>_syrk/p2, p3
+#   configs[2] act forward at 65,536 x 20x20 (deep_conv3_kernel, deep_front_kernel) -> gpurun_out/<tag>_deep/p2, p3
 #   (a second argument restricts the run to one of h3f | syrk | deep)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
