@@ -533,6 +533,10 @@ __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ sla
                                                    const float *__restrict__ theta, QLayout L,
                                                    float *__restrict__ h1o, float *__restrict__ qo, HeadArgs ha) {
     const int lane = threadIdx.x & 63;
+    if (MODE == HEAD_ACT && ha.rider.out && blockIdx.x == gridDim.x - 1) {   // the rider's workgroup
+        if (threadIdx.x < 64) sample_wave(ha.rider);
+        return;
+    }
     const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= S) return;
     float h = theta[L.off_d1b + lane];
@@ -1080,7 +1084,7 @@ void qnet_head_pair(const QLayout &L, const float *th_t, QWork &wt_, const float
 
 void head_launch(const QLayout &L, const float *th, const float *slab, int ks, int64_t S, float *h1, float *qo,
                  HeadMode mode, const HeadArgs &ha, hipStream_t s) {
-    const int grid = ceil_div(S, 4);
+    const int grid = ceil_div(S, 4) + (mode == HEAD_ACT && ha.rider.out ? 1 : 0);
     switch (mode) {
         case HEAD_Q: head_kernel<HEAD_Q><<<grid, 256, 0, s>>>(slab, ks, S, th, L, h1, qo, ha); break;
         case HEAD_ACT: head_kernel<HEAD_ACT><<<grid, 256, 0, s>>>(slab, ks, S, th, L, h1, qo, ha); break;
@@ -1112,7 +1116,7 @@ void qnet_head(const QLayout &L, const float *th, int64_t S, QWork &w, HeadMode 
                hipStream_t s) {
     int kc;
     const int ks = d1_split(L, S, kc);
-    const int grid = ceil_div(S, 4);
+    const int grid = ceil_div(S, 4) + (mode == HEAD_ACT && ha.rider.out ? 1 : 0);
     switch (mode) {
         case HEAD_Q: head_kernel<HEAD_Q><<<grid, 256, 0, s>>>(w.slab, ks, S, th, L, w.h1, w.q, ha); break;
         case HEAD_ACT: head_kernel<HEAD_ACT><<<grid, 256, 0, s>>>(w.slab, ks, S, th, L, w.h1, w.q, ha); break;

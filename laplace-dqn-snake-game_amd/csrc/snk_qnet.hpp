@@ -101,6 +101,8 @@ struct HeadArgs {
     float *dq = nullptr;
     float *dz1 = nullptr;   // LOSS: also write Dense2's data gradient (the backward's first step)
     int64_t B = 0;
+    // ACT: an extra workgroup runs this replay draw (the trainer's next update sample)
+    SampleRider rider;
 };
 
 // forward: q[S][3] into w.q (and w.h1); mode-specific epilogue

@@ -81,9 +81,8 @@ struct snk_trainer_s {
 // with n_upd DQN updates after the env step. The first update's replay draw
 // counts the n transitions this step stores.
 // chain: the previous iteration of this launch sequence (same learn / n_upd) ran
-// just before, so its last grad_update already drew this iteration's first
-// sample (pending = the n stores to come) and wrote the conv3 weight-max
-// partials of the image the act forward reads; next_chain: the next one will.
+// just before, so its last grad_update wrote the conv3 weight-max partials of
+// the image the act forward reads (no scan); next_chain: the next one will.
 static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream_t s, int it = 0, bool chain = false,
                               bool next_chain = false) {
     const EnvDev &E = env_dev(h->env);
@@ -94,18 +93,17 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     chain = chain && upd && !q->deep;
     next_chain = next_chain && upd && !q->deep;
     // the first update's sample (counting the n transitions this step stores) rides in a
-    // spare workgroup of the act forward's weight-max scan (small net, batch <= 64), or
-    // was drawn by the previous iteration's last grad_update (chain)
-    const bool ride = upd && !q->deep && h->B <= 64 && !chain;
+    // spare workgroup of the act forward's head launch (batch <= 64)
+    const bool ride = upd && h->B <= 64;
     if (chain) q->act.wmax_fresh = 1;
-    SampleRider rider;
+    HeadArgs ha;
     if (ride) {
+        SampleRider &rider = ha.rider;
         rider.count = R.count; rider.cap = R.cap; rider.pending = E.n; rider.batch = h->B; rider.seed = sseed;
         rider.draw_dev = &h->stats->updates; rider.out = h->idx;
-    } else if (upd && !chain) {
+    } else if (upd) {
         replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s, E.n);
     }
-    HeadArgs ha;
     ha.act = h->act;
     ha.seed = h->cfg.seed;
     ha.tptr = &E.ctl->t;
@@ -113,8 +111,7 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     if (q->deep)
         deep_forward(q, SNK_NET_Q, src_env(E), E.n, HEAD_ACT, ha, s);
     else
-        qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q,
-                     ride ? &rider : nullptr);
+        qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q);
     // step! + virtual_step + store! + the episode statistics, one launch
     const EpisodeAcc acc{&h->stats->episodes, &h->stats->score_sum, &h->stats->env_steps, &h->stats->reward_sum,
                          &h->stats->reward_max, &h->stats->score_max};
@@ -138,10 +135,9 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
                         h->loss_log, h->log_cap, &h->stats->updates, &h->stats->nb, &h->stats->epsilon,
                         h->cfg.decay, h->cfg.epsilon_end, h->ticket, SampleRider{}};
         const bool last = u + 1 == n_upd;
-        if (!q->deep && (!last || next_chain)) {   // the next update's replay draw (utils.jl:442); for the next
-            // iteration's first update it counts the n transitions that iteration's step stores
-            post.next.count = R.count; post.next.cap = R.cap; post.next.pending = last ? E.n : 0;
-            post.next.batch = h->B; post.next.seed = sseed; post.next.out = h->idx;
+        if (!q->deep && !last) {   // the next update's replay draw (utils.jl:442), count unchanged
+            post.next.count = R.count; post.next.cap = R.cap; post.next.pending = 0; post.next.batch = h->B;
+            post.next.seed = sseed; post.next.out = h->idx;
         }
         if (q->deep) {   // the deeper bf16 net: finished gradient, [mean over ranks], RMSProp + images + target
             if (h->comm) comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
