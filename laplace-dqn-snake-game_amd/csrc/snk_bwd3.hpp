@@ -24,6 +24,7 @@
 //    kk ascending, relu-masked by a2. No wasted products, no slab, no reduce.
 #pragma once
 #include "snk_conv.hpp"
+#include "snk_qnet.hpp"
 
 namespace snk {
 
@@ -257,6 +258,11 @@ struct Conv2BwdArgs {
     float *slab;        // dW partials [S][145][32] (row 144: bias)
     float *dzc1;        // [S][bs*bs][16]
     int S, bs;
+    // conv1's weight gradient, fused into the data-gradient blocks (c1slab != nullptr):
+    // block (s, xb) writes the partial over its position tiles to c1slab[s*C2_NXB + xb][9C+1][16]
+    BoardSrc x;         // conv1's input planes (the forward's float copy or the replay frames)
+    float *c1slab;
+    int C;
 };
 constexpr int C2_DS = 48, C2_BS = 36, C2_WS = 36;   // LDS row strides (floats), conflict-free reads
 
@@ -403,6 +409,13 @@ __device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb
     __syncthreads();
     const int r = lane & 15, g = lane >> 4;
     const int nt = (bs2 + 15) / 16;
+    // conv1 weight gradient over this wave's tiles: C1[(kk, c) | bias][co] = sum over the
+    // tile's positions p of x[p + (du-1, dv-1)][c] * dzc1[p][co], as v_mfma_f32_16x16x4_f32
+    // with k = position: step m takes positions 4g + m, whose dzc1 this lane already holds
+    // in acc[m] (column co = r); rows 0..15 and 16..31 of (kk, c) (9C of them, then the bias
+    // row of ones, then zeros)
+    f32x4m c1acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int nrow = 9 * a.C;
     for (int t = xb + C2_NXB * wave; t < nt; t += 4 * C2_NXB) {
         const int p = min(t * 16 + r, bs2 - 1);
         const int j = p / bs, i = p - j * bs;
@@ -416,14 +429,54 @@ __device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb
 #pragma unroll
             for (int c = 0; c < 32; c += 4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[c], pb[c], acc, 0, 0, 0);
         }
+        f32x4m dzm;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int row = t * 16 + 4 * g + e;
+            dzm[e] = 0.0f;
             if (row < bs2) {
                 const int64_t o = ((int64_t)s * bs2 + row) * 16 + r;
-                a.dzc1[o] = a.a1[o] > 0.0f ? acc[e] : 0.0f;
+                dzm[e] = a.a1[o] > 0.0f ? acc[e] : 0.0f;
+                a.dzc1[o] = dzm[e];
             }
         }
+        if (!a.c1slab) continue;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int pos = t * 16 + 4 * g + m;   // k = g of this step
+            const int pj = pos / bs, pi = pos - pj * bs;
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                const int k1 = rt * 16 + r;           // row (kk, c) of this lane's A element
+                float xv = 0.0f;
+                if (pos < bs2) {
+                    if (k1 < nrow) {
+                        const int kk = k1 / a.C, c = k1 - kk * a.C;
+                        const int xi = pi + kk % 3 - 1, xj = pj + kk / 3 - 1;
+                        if (xi >= 0 && xi < bs && xj >= 0 && xj < bs) xv = a.x.load(s, c, xi + xj * bs);
+                    } else if (k1 == nrow) {
+                        xv = 1.0f;
+                    }
+                }
+                c1acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv, dzm[m], c1acc[rt], 0, 0, 0);
+            }
+        }
+    }
+    if (!a.c1slab) return;
+    // the block's four wave partials, summed in wave order through LDS (the staging is free)
+    __syncthreads();
+    float *red = sm;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[((wave * 2 + rt) * 4 + e) * 64 + lane] = c1acc[rt][e];
+    __syncthreads();
+    float *out = a.c1slab + ((int64_t)s * C2_NXB + xb) * (nrow + 1) * 16;
+    for (int q = tid; q < 2 * 4 * 64; q += 256) {
+        const float v = ((red[q] + red[512 + q]) + red[1024 + q]) + red[1536 + q];
+        const int ln = q & 63, e = (q >> 6) & 3, rt = q >> 8;
+        const int row = rt * 16 + 4 * (ln >> 4) + e;   // C[row][col = ln & 15]
+        if (row <= nrow) out[row * 16 + (ln & 15)] = v;
     }
 }
 

@@ -1176,7 +1176,11 @@ static SlabRegions slab_regions(const QLayout &L, int64_t S) {
     r.c3 = r.d1 + zslab(p.d1, (int64_t)(L.K1 + 1) * 64);
     r.c2 = r.c3 + zslab(p.c3, 1153 * 64);
     r.c1 = r.c2 + zslab(p.c2, 145 * 32);
-    r.total = std::max<int64_t>(r.c1 + zslab(p.c1, (int64_t)(9 * L.C + 1) * 16), 1);
+    // conv1's weight gradient: K-split slabs of the gemm, or one slab per data-gradient block of
+    // conv2_bwd_kernel (fused there)
+    const int64_t c1n = (int64_t)(9 * L.C + 1) * 16;
+    const int64_t c1 = c2bwd_ok(L, S) ? S * C2_NXB * c1n : zslab(p.c1, c1n);
+    r.total = std::max<int64_t>(r.c1 + c1, 1);
     return r;
 }
 int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S) { return slab_regions(L, S).total; }
@@ -1290,14 +1294,28 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             }
             fin(p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
         }
-        // conv2: dW | dX (relu mask on a1)
+        // conv1's input planes: the forward's float copy when it made one
+        BoardSrc xs = src;
+        if (w.x0_valid) {
+            xs = BoardSrc{};
+            xs.fbase = w.x0;
+            xs.C = L.C;
+            xs.ncell = nc;
+        }
+        const int64_t Mc1 = 9 * L.C + 1;
+        // conv2: dW | dX (relu mask on a1), and with it conv1's weight gradient
         float *c2d = dst(2, p.c2, L.off_w2, 145 * 32, slab + sr.c2);
-        if (c2bwd_ok(L, S)) {
-            const Conv2BwdArgs ca{w.a1, w.dz2, th + L.off_w2, c2d, w.dzc1, (int)S, bs};
+        const bool c2f = c2bwd_ok(L, S);
+        if (c2f) {
+            const GemmPlan c1p{1, (int)(S * C2_NXB), 0};   // one slab per data-gradient block
+            float *c1d = dst(3, c1p, L.off_w1, Mc1 * 16, slab + sr.c1);
+            Conv2BwdArgs ca{w.a1, w.dz2, th + L.off_w2, c2d, w.dzc1, (int)S, bs, xs, c1d, L.C};
             const size_t lds = (size_t)c2_bwd_lds_floats(bs) * sizeof(float);
             set_lds_limit((const void *)conv2_bwd_kernel, lds);
             conv2_bwd_kernel<<<(unsigned)((1 + C2_NXB) * S), 256, lds, s>>>(ca);
             launch_check("conv2_bwd_kernel");
+            fin(p.c2, L.off_w2, 145 * 32, slab + sr.c2);
+            fin(c1p, L.off_w1, Mc1 * 16, slab + sr.c1);
         } else
         pair_launch<512>(gemm_job<1, 8>(AConvDw<16, 3, 1>{w.a1, bs, bs, S * nc, FastDiv(nc), FastDiv(bs)},
                                         BRows{w.dz2, S * nc, 32}, EpSlab{c2d, 145, 32}, 145, 32, S * nc, p.c2),
@@ -1305,20 +1323,14 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
                                         BConvT<16, 32>{th + L.off_w2, 288}, EpReluMask{w.dzc1, w.a1, (int)(S * nc), 16},
                                         S * nc, 16, 288, p.c2x),
                          s);
-        fin(p.c2, L.off_w2, 145 * 32, slab + sr.c2);
-        // conv1: weights only
-        const int64_t Mc1 = 9 * L.C + 1;
-        float *c1d = dst(3, p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
-        BoardSrc xs = src;   // the forward's float copy of the input planes when it made one
-        if (w.x0_valid) {
-            xs = BoardSrc{};
-            xs.fbase = w.x0;
-            xs.C = L.C;
-            xs.ncell = nc;
+        if (!c2f) {
+            fin(p.c2, L.off_w2, 145 * 32, slab + sr.c2);
+            // conv1: weights only
+            float *c1d = dst(3, p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
+            gemm<1>(ABoardDw{xs, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
+                    EpSlab{c1d, (int)Mc1, 16}, Mc1, 16, S * nc, p.c1, s);
+            fin(p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
         }
-        gemm<1>(ABoardDw{xs, bs, L.C, S * nc, FastDiv(nc), FastDiv(bs)}, BRows{w.dzc1, S * nc, 16},
-                EpSlab{c1d, (int)Mc1, 16}, Mc1, 16, S * nc, p.c1, s);
-        fin(p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
     }
 }
 
