@@ -55,8 +55,16 @@ struct UpdFwdArgs {
     int S;
 };
 
-// LDS strides (halves): A1 position record 3 planes x 16 ch + 8 pad, A2 3 x 32 + 8
-constexpr int UPDF_A1S = 56, UPDF_A2S = 104;
+// LDS strides (halves): A1 position record 3 planes x 16 ch + 8 pad
+constexpr int UPDF_A1S = 56;
+// A2 (conv3's input, conv2's output): three plane images [pl][HIN rows][PJ][32 ch] of 64-byte
+// rows, chunk c (8 channels) of row R at slot c ^ ((R >> 1) & 3). conv3's row tiles are TW
+// output columns x 16 / TW output rows (TW = 8 while WO <= 8), so each fragment read covers
+// rows (qi + du) + (qj + dv) * PJ, which with PJ = 16 (TW = 8) land on distinct bank quads
+// (lane groups simulated; the round-2 layout, 104-half position records with tiles running
+// across output rows, was 2.25-way conflicted)
+__host__ __device__ constexpr int updf_tw(int hin) { return hin - 5 <= 8 ? 8 : 16; }
+__host__ __device__ constexpr int updf_pj(int hin) { return updf_tw(hin) == 8 ? 16 : 24; }
 constexpr int UPDF_NT = 512;   // 8 waves: two per SIMD, so one wave's LDS / MFMA latency hides under the other's
 
 // floats of the input planes + conv1 weights, rounded up to a 16-byte boundary
@@ -65,7 +73,7 @@ __host__ __device__ constexpr int updf_f32_words(int hin, int C) {
 }
 __host__ __device__ constexpr int updf_lds_bytes(int hin, int C) {
     return updf_f32_words(hin, C) * 4 + (hin + 2) * (hin + 2) * UPDF_A1S * 2 + 9 * 3 * 32 * 16 * 2 +
-           hin * hin * UPDF_A2S * 2;
+           3 * hin * updf_pj(hin) * 32 * 2;
 }
 
 // the three bf16 parts h, m, l of x (split_part's values, in one pass)
@@ -96,13 +104,16 @@ template <int HIN, int C>
 __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     constexpr int BP = HIN + 2, NB = BP * BP, NC = HIN * HIN;
     constexpr int WO = HIN - 5, NO = WO * WO;
-    constexpr int T2 = (NC + 15) / 16, T3 = (NO + 15) / 16;
+    constexpr int TW = updf_tw(HIN), PJ = updf_pj(HIN), RPT = 16 / TW;   // conv3 tile: TW columns x RPT rows
+    constexpr int T2 = (NC + 15) / 16, T3 = (WO + RPT - 1) / RPT;
+    constexpr int A2P = HIN * PJ * 32;                                   // halves per A2 plane image
+    static_assert(TW + 5 <= PJ && HIN <= PJ && WO <= TW, "conv3 tile geometry");
     extern __shared__ __attribute__((aligned(16))) uint8_t updf_lds[];
     float *xin = reinterpret_cast<float *>(updf_lds);                 // [C][NB]
     float *w1 = xin + C * NB;                                        // [9C*16] + bias [16]
     uint16_t *A1 = reinterpret_cast<uint16_t *>(xin + updf_f32_words(HIN, C));   // [NB][UPDF_A1S]
     uint16_t *B2 = A1 + NB * UPDF_A1S;                               // [9 kk][3][32 co][16 ci]
-    uint16_t *A2 = B2 + 9 * 3 * 32 * 16;                             // [NC][UPDF_A2S]
+    uint16_t *A2 = B2 + 9 * 3 * 32 * 16;                             // [3][HIN][PJ][32] (swizzled chunks)
     static_assert((NB * UPDF_A1S * 2) % 16 == 0, "16-B regions");
 
     UPD_CLK(0);
@@ -244,10 +255,11 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
                 if (wr && n.a2) n.a2[((int64_t)s * NC + row) * 32 + col] = v;
                 uint16_t h, m, l;
                 split3_scalar(v, h, m, l);
-                uint16_t *d = A2 + row * UPDF_A2S + col;
+                const int rj = row / HIN, R = (row - rj * HIN) + rj * PJ;
+                uint16_t *d = A2 + R * 32 + 8 * ((col >> 3) ^ ((R >> 1) & 3)) + (col & 7);
                 d[0] = h;
-                d[32] = m;
-                d[64] = l;
+                d[A2P] = m;
+                d[2 * A2P] = l;
             }
         }
     }
@@ -294,13 +306,12 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
                     *reinterpret_cast<u32x4 *>(B3 + buf * SPL + (q >> 2) * LDB + ((q & 3) ^ ((q >> 4) & 3)) * 8) = st[u];
             }
         };
-        int qb[NTW];
+        int qb[NTW];   // the lane's first A2 row in row tile rt0 + 4u: column r % TW, row clamped to WO - 1
         f32x4v acc[NTW][2];
 #pragma unroll
         for (int u = 0; u < NTW; ++u) {
-            const int q = min((rt0 + 4 * u) * 16 + r, NO - 1);
-            const int qj = q / WO, qi = q - qj * WO;
-            qb[u] = qi + qj * HIN;
+            const int qj = min((rt0 + 4 * u) * RPT + r / TW, WO - 1), qi = r % TW;
+            qb[u] = qi + qj * PJ;
             acc[u][0] = acc[u][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
         }
         auto compute = [&](int stg) {
@@ -314,10 +325,11 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
 #pragma unroll
                 for (int u = 0; u < NTW; ++u) {
                     if (rt0 + 4 * u < T3) {   // wave-uniform
-                        const uint16_t *pa = A2 + (qb[u] + du + dv * HIN) * UPDF_A2S + 8 * g;
+                        const int R = qb[u] + du + dv * PJ;
+                        const uint16_t *pa = A2 + R * 32 + 8 * (g ^ ((R >> 1) & 3));
                         u32x4 a[3];
 #pragma unroll
-                        for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const u32x4 *>(pa + pl * 32);
+                        for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const u32x4 *>(pa + pl * A2P);
                         acc[u][kl & 1] = mfma_x6(a, b, acc[u][kl & 1]);
                     }
                 }
@@ -347,8 +359,9 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
             if (t >= T3) continue;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int row = t * 16 + 4 * g + e;
-                if (row < NO) n.a3[((int64_t)s * NO + row) * 64 + col] = fmaxf((acc[u][0][e] + acc[u][1][e]) + bv, 0.f);
+                const int qi = (4 * g + e) % TW, qj = t * RPT + (4 * g + e) / TW;
+                if (qi < WO && qj < WO)
+                    n.a3[((int64_t)s * NO + qi + qj * WO) * 64 + col] = fmaxf((acc[u][0][e] + acc[u][1][e]) + bv, 0.f);
             }
         }
     }
