@@ -539,13 +539,31 @@ __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ sla
     }
     const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= S) return;
+    // the K-split slab loads all in flight at once (a runtime-bounded loop waited for each)
+    constexpr int KMAX = 16;
+    float zv[KMAX];
+#pragma unroll
+    for (int z = 0; z < KMAX; ++z)
+        if (z < ks) zv[z] = slab[((int64_t)z * S + s) * 64 + lane];
+    float w2[3], b2[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        w2[a] = theta[L.off_d2w + a * 64 + lane];
+        b2[a] = theta[L.off_d2b + a];
+    }
     float h = theta[L.off_d1b + lane];
-    for (int z = 0; z < ks; ++z) h += slab[((int64_t)z * S + s) * 64 + lane];
+    if (ks <= KMAX) {
+#pragma unroll
+        for (int z = 0; z < KMAX; ++z)
+            if (z < ks) h += zv[z];
+    } else {
+        for (int z = 0; z < ks; ++z) h += slab[((int64_t)z * S + s) * 64 + lane];
+    }
     h = h > 0.0f ? h : 0.0f;
     h1o[s * 64 + lane] = h;
     float q[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) q[a] = theta[L.off_d2b + a] + wave_sum(theta[L.off_d2w + a * 64 + lane] * h);
+    for (int a = 0; a < 3; ++a) q[a] = b2[a] + wave_sum(w2[a] * h);
     if (MODE == HEAD_LOSS && ha.dz1) {
         // head_bwd fused: dz1 = (h1 > 0) * sum_a dq[a] W2[a][o] with dq one-hot at the taken action
         const int64_t m = ha.idx ? ha.idx[s] : s;
@@ -553,7 +571,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ sla
         const double e = (double)q[a] - ha.target[s];
         const double ae = fabs(e);
         const float g = (float)((ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / (double)ha.B);
-        ha.dz1[s * 64 + lane] = h > 0.0f ? g * theta[L.off_d2w + a * 64 + lane] : 0.0f;
+        ha.dz1[s * 64 + lane] = h > 0.0f ? g * (a == 0 ? w2[0] : a == 1 ? w2[1] : w2[2]) : 0.0f;
     }
     if (lane != 0) return;
     qo[s * 3 + 0] = q[0];
@@ -610,22 +628,50 @@ __global__ __launch_bounds__(256) void head_pair_kernel(HeadNet tn, HeadNet qn, 
     const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= S) return;
     const int64_t m = ha.idx ? ha.idx[s] : s;
+    // every independent load of both nets up front (the kernel is load-latency bound: the
+    // q_net half used to start its loads only after the t_net half's reductions)
+    constexpr int KMAX = 16;
+    float zt[KMAX], zq[KMAX];
+#pragma unroll
+    for (int z = 0; z < KMAX; ++z) {
+        if (z < ks) {
+            zt[z] = tn.slab[((int64_t)z * S + s) * 64 + lane];
+            zq[z] = qn.slab[((int64_t)z * S + s) * 64 + lane];
+        }
+    }
+    float wt2[3], wq2[3], bt2[3], bq2[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        wt2[a] = tn.theta[L.off_d2w + a * 64 + lane];
+        wq2[a] = qn.theta[L.off_d2w + a * 64 + lane];
+        bt2[a] = tn.theta[L.off_d2b + a];
+        bq2[a] = qn.theta[L.off_d2b + a];
+    }
+    const float bt1 = tn.theta[L.off_d1b + lane], bq1 = qn.theta[L.off_d1b + lane];
+    const uint8_t mk = ha.mask[m], dn = ha.done[m];
+    const float rw = ha.rew[m];
+    const int a_taken = ha.act_idx[m] % 3;
     // t_net(s'): TD target (utils.jl:448-451)
-    float h = tn.theta[L.off_d1b + lane];
-    for (int z = 0; z < ks; ++z) h += tn.slab[((int64_t)z * S + s) * 64 + lane];
+    float h = bt1;
+    if (ks <= KMAX) {
+#pragma unroll
+        for (int z = 0; z < KMAX; ++z)
+            if (z < ks) h += zt[z];
+    } else {
+        for (int z = 0; z < ks; ++z) h += tn.slab[((int64_t)z * S + s) * 64 + lane];
+    }
     h = h > 0.0f ? h : 0.0f;
     tn.h1[s * 64 + lane] = h;
     float q[3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) q[a] = tn.theta[L.off_d2b + a] + wave_sum(tn.theta[L.off_d2w + a * 64 + lane] * h);
-    const uint8_t mk = ha.mask[m];
+    for (int a = 0; a < 3; ++a) q[a] = bt2[a] + wave_sum(wt2[a] * h);
     float mx = -INFINITY;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float v = ((mk >> a) & 1) ? -100.0f : q[a];
         mx = v > mx ? v : mx;
     }
-    const double tgt = (double)ha.rew[m] + ha.gamma * (double)mx * (double)(1 - (int)ha.done[m]);
+    const double tgt = (double)rw + ha.gamma * (double)mx * (double)(1 - (int)dn);
     if (lane == 0) {
         tn.q[s * 3 + 0] = q[0];
         tn.q[s * 3 + 1] = q[1];
@@ -633,17 +679,23 @@ __global__ __launch_bounds__(256) void head_pair_kernel(HeadNet tn, HeadNet qn, 
         ha.target[s] = tgt;
     }
     // q_net(s): Huber loss, dq and dz1 (utils.jl:453-464)
-    h = qn.theta[L.off_d1b + lane];
-    for (int z = 0; z < ks; ++z) h += qn.slab[((int64_t)z * S + s) * 64 + lane];
+    h = bq1;
+    if (ks <= KMAX) {
+#pragma unroll
+        for (int z = 0; z < KMAX; ++z)
+            if (z < ks) h += zq[z];
+    } else {
+        for (int z = 0; z < ks; ++z) h += qn.slab[((int64_t)z * S + s) * 64 + lane];
+    }
     h = h > 0.0f ? h : 0.0f;
     qn.h1[s * 64 + lane] = h;
 #pragma unroll
-    for (int a = 0; a < 3; ++a) q[a] = qn.theta[L.off_d2b + a] + wave_sum(qn.theta[L.off_d2w + a * 64 + lane] * h);
-    const int a = ha.act_idx[m] % 3;
+    for (int a = 0; a < 3; ++a) q[a] = bq2[a] + wave_sum(wq2[a] * h);
+    const int a = a_taken;
     const double e = (double)q[a] - tgt;
     const double ae = fabs(e);
     const double g = (ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / (double)ha.B;
-    if (ha.dz1) ha.dz1[s * 64 + lane] = h > 0.0f ? (float)g * qn.theta[L.off_d2w + a * 64 + lane] : 0.0f;
+    if (ha.dz1) ha.dz1[s * 64 + lane] = h > 0.0f ? (float)g * (a == 0 ? wq2[0] : a == 1 ? wq2[1] : wq2[2]) : 0.0f;
     if (lane != 0) return;
     qn.q[s * 3 + 0] = q[0];
     qn.q[s * 3 + 1] = q[1];
