@@ -37,6 +37,7 @@ struct H3FArgs {
     int nwmax;
     const float *b3;     // conv3 bias [64]
     float *out;          // a3 [S][ho^2][64]
+    SampleRider rider;   // rider.out: one extra workgroup runs this replay draw (the trainer's update sample)
 };
 
 // Profiling builds only (make clocks): per-workgroup phase timestamps, read back by
@@ -46,7 +47,7 @@ struct H3FArgs {
 __device__ uint64_t *g_h3f_clk;
 #define H3F_CLK(slot)                                                                                 \
     do {                                                                                              \
-        if (threadIdx.x == 0 && g_h3f_clk) g_h3f_clk[(int64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0 && g_h3f_clk) g_h3f_clk[((int64_t)blockIdx.x - rb) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define H3F_CLK(slot) do { } while (0)
@@ -79,6 +80,13 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     constexpr int R2 = NSG * hin2, T2 = (R2 + 15) / 16, U2 = (T2 + 7) / 8;
     constexpr int NW4 = 9 * 32 * 16 / 4, LW = (NW4 + 511) / 512, LA = (NSG * hin2 * 4 + 511) / 512;
     static_assert(XR % 8 == 0 && BR % 8 == 0, "16-byte pieces");
+    // the rider's workgroup is workgroup 0 (dispatched first: its serial draw overlaps the
+    // sample groups instead of trailing them); it touches no LDS and no barrier
+    const int rb = a.rider.out ? 1 : 0;
+    if (rb && blockIdx.x == 0) {
+        if (threadIdx.x < 64) sample_wave(a.rider);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) u32x4 h3f_lds[];
     __shared__ float red[8][7];
     u32x4 *Bs = h3f_lds;               // conv3 B [NBUF][NB]
@@ -88,7 +96,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     u32x2 *A1v = reinterpret_cast<u32x2 *>(A1), *B2v = reinterpret_cast<u32x2 *>(B2);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
-    const int s0 = blockIdx.x * NSG;
+    const int s0 = ((int)blockIdx.x - rb) * NSG;
     const int ns = min(NSG, S - s0);
     H3F_CLK(0);
 

@@ -10,6 +10,7 @@
 // B[k l>>5][col l&31]; accumulator register g of lane l is
 // C[(g&3) + 8*(g>>2) + 4*(l>>5)][l&31].
 #pragma once
+#include <type_traits>
 #include "snk_common.hpp"
 
 namespace snk {
@@ -44,8 +45,10 @@ __device__ __forceinline__ void gemm_body(const AL &al, const BL &bl, const EP &
 #pragma unroll
         for (int g = 0; g < 16; ++g) acc[nt][g] = 0.0f;
     const auto ctx = al.row(m0 + r, M);
-    float a_c[4], b_c[4][NT], a_n[4], b_n[4][NT];
-    auto load = [&](int k, float (&av)[4], float (&bv)[4][NT]) {
+    // 8-k steps in a 3-slot register ring, loads two steps ahead (these GEMMs are short and
+    // latency-bound: one step ahead left most of each load's latency exposed)
+    float a_r[3][4], b_r[3][4][NT];
+    auto load = [&](int k, float (&av)[4], float (&bv)[4][NT]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int kk = k + 2 * i + h;
@@ -55,23 +58,21 @@ __device__ __forceinline__ void gemm_body(const AL &al, const BL &bl, const EP &
             for (int nt = 0; nt < NT; ++nt) bv[i][nt] = v ? bl.load(kk, n0 + nt * 32 + r, we) : 0.0f;
         }
     };
-    if (wb < we) load(wb, a_c, b_c);
-    for (int k = wb; k < we; k += 8) {
-        const bool more = k + 8 < we;
-        if (more) load(k + 8, a_n, b_n);
+    auto step = [&](int k, auto slot_c) __attribute__((always_inline)) {
+        constexpr int SL = decltype(slot_c)::value;
+        if (k + 16 < we) load(k + 16, a_r[(SL + 2) % 3], b_r[(SL + 2) % 3]);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
-                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_c[i], b_c[i][nt], acc[nt], 0, 0, 0);
-        if (more) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                a_c[i] = a_n[i];
-#pragma unroll
-                for (int nt = 0; nt < NT; ++nt) b_c[i][nt] = b_n[i][nt];
-            }
-        }
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a_r[SL][i], b_r[SL][i][nt], acc[nt], 0, 0, 0);
+    };
+    if (wb < we) load(wb, a_r[0], b_r[0]);
+    if (wb + 8 < we) load(wb + 8, a_r[1], b_r[1]);
+    for (int k = wb; k < we; k += 24) {
+        step(k, std::integral_constant<int, 0>{});
+        if (k + 8 < we) step(k + 8, std::integral_constant<int, 1>{});
+        if (k + 16 < we) step(k + 16, std::integral_constant<int, 2>{});
     }
     if (KW > 1) {
         // every wave parks its tile in LDS; the workgroup then sums the KW

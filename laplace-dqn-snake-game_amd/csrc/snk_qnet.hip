@@ -877,7 +877,7 @@ static void h3f_launch_t(const H3FArgs &fa, int64_t S, hipStream_t s) {
     constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, 4>();
     static_assert(lds <= 160 * 1024, "conv_h3f LDS");
     set_lds_limit((const void *)conv_h3f_kernel<HIN, 4, CF>, lds);
-    conv_h3f_kernel<HIN, 4, CF><<<(unsigned)ceil_div(S, 4), 512, lds, s>>>(fa, (int)S);
+    conv_h3f_kernel<HIN, 4, CF><<<(unsigned)(ceil_div(S, 4) + (fa.rider.out ? 1 : 0)), 512, lds, s>>>(fa, (int)S);
     launch_check("conv_h3f_kernel");
 }
 template <int HIN>
@@ -963,16 +963,20 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             const float *img = n.wt + L.off_t3;
             // a full forward rescans the image (it may have changed in place) unless the
             // trainer's previous grad_update wrote its partials (and no sample rides the scan)
-            const bool fresh = fresh_in[g] && w.wmax_n && w.wmax_img == img && !(rider && g == 0);
+            const bool fresh = fresh_in[g] && w.wmax_n && w.wmax_img == img;
+            // the sample rider rides the weight-max scan when it runs, else the conv launch
+            SampleRider rd = (rider && g == 0) ? *rider : SampleRider{};
             if (((lo <= 0 && hi >= 0) && !fresh) || !w.wmax_n || w.wmax_img != img) {
-                const SampleRider rd = (rider && g == 0) ? *rider : SampleRider{};
                 wmax_scan_kernel<<<256 + (rd.out ? 1 : 0), 256, 0, s>>>(img, n3, w.wmax_part, rd);
                 launch_check("wmax_scan_kernel");
                 w.wmax_n = 256;
                 w.wmax_img = img;
+                rd = SampleRider{};
             }
+            SNK_CHECK(!rd.out || (lo <= 2 && hi >= 1), SNK_ERR_INTERNAL, "sample rider without a launch");
             if (lo <= 2 && hi >= 1) {
                 H3FArgs fa{};
+                fa.rider = rd;
                 fa.src = n.src; fa.w1 = n.th + L.off_w1; fa.b1 = n.th + L.off_b1;
                 fa.w2 = n.wt + L.off_t2; fa.b2 = n.th + L.off_b2; fa.w3 = img; fa.wmax = w.wmax_part;
                 fa.nwmax = w.wmax_n; fa.b3 = n.th + L.off_b3; fa.out = w.a3;
@@ -1237,10 +1241,6 @@ static SlabRegions slab_regions(const QLayout &L, int64_t S) {
 }
 int64_t qnet_backward_slab_floats(const QLayout &L, int64_t S) { return slab_regions(L, S).total; }
 
-static void reduce_into(const float *slab, int ks, int64_t MN, float *out, hipStream_t s) {
-    slab_reduce_kernel<<<(unsigned)std::min<int64_t>(ceil_div(MN, 256), 2048), 256, 0, s>>>(slab, ks, MN, out);
-    launch_check("slab_reduce_kernel");
-}
 
 // data-gradient chain shared by the loss backward and the per-sample Jacobian:
 // dz1 (from dq) -> dz3 -> dz2 -> dzc1, each relu-masked by its activation
@@ -1277,13 +1277,16 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
     const SlabRegions sr = slab_regions(L, S);
     SNK_CHECK(slab_cap >= sr.total, SNK_ERR_INTERNAL, "backward slab too small");
     const int bs = L.bs, nc = L.ncell, no = L.Wo * L.Wo;
-    GradSlabs *D = o.defer;
-    if (D) {
-        *D = GradSlabs{};
-        D->dq = w.dq;
-        D->h1 = w.h1;
-        D->S = S;
-    }
+    // the slabs and Dense2 are always finished by grad_update_kernel's summation (the caller's
+    // deferred pass, or one finish-only pass here): a gradient is bit-identical whichever path
+    // produced it
+    GradSlabs local;
+    const bool deferred = o.defer != nullptr;
+    GradSlabs *D = deferred ? o.defer : &local;
+    *D = GradSlabs{};
+    D->dq = w.dq;
+    D->h1 = w.h1;
+    D->S = S;
     {
         // each layer's weight gradient and data gradient in ONE launch
         auto dst = [&](int k, const GemmPlan &g, int64_t off, int64_t n, float *sl) -> float * {
@@ -1293,17 +1296,12 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             }
             return sl;
         };
-        auto fin = [&](const GemmPlan &g, int64_t off, int64_t n, float *sl) {
-            if (g.z > 1 && !D) reduce_into(sl, g.z, n, grad + off, s);
-        };
+        auto fin = [&](const GemmPlan &, int64_t, int64_t, float *) {};   // grad_update_kernel finishes
         if (!o.dz1_ready) {
             head_bwd_kernel<<<ceil_div(S, 4), 256, 0, s>>>(w.dq, w.h1, th, L, S, w.dz1);
             launch_check("head_bwd_kernel");
         }
-        if (!D) {
-            d2_grad_kernel<<<1, 256, 0, s>>>(w.dq, w.h1, S, L, grad);
-            launch_check("d2_grad_kernel");
-        }
+
         // Dense1: dW (+ bias row) | dX with the relu mask of a3
         const int64_t M1 = L.K1 + 1;
         float *d1d = dst(0, p.d1, L.off_d1w, M1 * 64, slab + sr.d1);
@@ -1384,6 +1382,7 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             fin(p.c1, L.off_w1, Mc1 * 16, slab + sr.c1);
         }
     }
+    if (!deferred) grad_update_launch(L, D, grad, nullptr, s);   // finish only
 }
 
 // ---------------------------------------------------------------- fused update
@@ -1397,36 +1396,9 @@ struct UpdArgs {
 };
 
 
-// the finished gradient of packed parameter i: the sum of its K-split slabs
-// (slab_reduce order, z ascending; eight loads in flight) or the value already there
-__device__ __forceinline__ float finish_one(const UpdArgs &a, int64_t i) {
-    float g = a.grad[i];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int64_t j = i - a.g.off[k];
-        if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
-            const float *sl = a.g.slab[k] + j;
-            const int64_t n = a.g.n[k];
-            const int zc = a.g.z[k];
-            float v = 0.0f;
-            int z = 0;
-            for (; z + 8 <= zc; z += 8) {
-                float x[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = sl[(int64_t)(z + u) * n];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v += x[u];
-            }
-            for (; z < zc; ++z) v += sl[(int64_t)z * n];
-            g = v;
-        }
-    }
-    return g;
-}
-
-// finish_one for the four parameters i0 .. i0+3 (i0 % 4 == 0, all in one section):
-// float4 slab loads, sixteen in flight per batch; per component the same z-ascending
-// sum as finish_one
+// the finished gradient of the four packed parameters i0 .. i0+3 (i0 % 4 == 0, all in one
+// section): the sum of their K-split slabs (z ascending, float4 slab loads, sixteen in
+// flight per batch) or the value already there
 __device__ __forceinline__ f32x4 finish4(const UpdArgs &a, int64_t i0) {
     f32x4 g = *reinterpret_cast<const f32x4 *>(a.grad + i0);
 #pragma unroll
@@ -1551,11 +1523,11 @@ __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb,
     }
 }
 
-// blocks: [0, nimg) image sections (gu_image_block); then GU_OTHER blocks grid-striding
+// blocks: [0, nimg) image sections (gu_image_block); then GU_OTHER blocks striding
 // over the parameters without an image (conv1, the conv2 / conv3 / Dense1 bias rows);
 // the LAST block owns Dense2 (195 params): it stages dq and h1 through LDS and reduces
 // over the batch (d2_grad_kernel's order)
-constexpr int GU_OTHER = 4;
+constexpr int GU_OTHER = 16;
 __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
     const QLayout &L = a.L;
     const bool due = a.apply && a.u.counter && (*a.u.counter % a.u.rate) == 0;   // utils.jl:469-472
@@ -1594,23 +1566,45 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
         gu_image_block(a, S, bl / per, bl % per, due, omr, sec == 1 && a.u.wmax_out ? a.u.wmax_out + bl : nullptr);
     } else {
         // conv1 [off_w1, off_w2), conv2 bias [off_b2, off_w3), conv3 bias [off_b3, off_d1w),
-        // Dense1 bias [off_d1b, off_d2w): one index space over the four runs
+        // Dense1 bias [off_d1b, off_d2w): one index space over the four runs. These finish from
+        // long slab runs (conv1: one slab per conv2 data-gradient block, 128 at B = 64; the conv2
+        // bias: one per sample), so 8 lanes share a parameter: lane `sub` sums slabs z = sub,
+        // sub + 8, ... (16 loads in flight), then a fixed xor tree over the 8 lanes
         const int64_t r0 = L.off_w2 - L.off_w1, r1 = L.off_w3 - L.off_b2, r2 = L.off_d1w - L.off_b3,
                       r3 = L.off_d2w - L.off_d1b;
         const int64_t tot = r0 + r1 + r2 + r3;
-        for (int64_t e = (int64_t)(b - nimg) * 256 + threadIdx.x; e < tot; e += (int64_t)GU_OTHER * 256) {
+        const int sub = threadIdx.x & 7;
+        for (int64_t e = (int64_t)(b - nimg) * 32 + (threadIdx.x >> 3); e < tot; e += (int64_t)GU_OTHER * 32) {
             const int64_t i = e < r0 ? L.off_w1 + e
                             : e < r0 + r1 ? L.off_b2 + (e - r0)
                             : e < r0 + r1 + r2 ? L.off_b3 + (e - r0 - r1)
                                                : L.off_d1b + (e - r0 - r1 - r2);
-            float g;
+            float g = a.grad[i];
             if (a.finish) {
-                g = finish_one(a, i);
-                a.grad[i] = g;
-            } else {
-                g = a.grad[i];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int64_t j = i - a.g.off[k];
+                    if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
+                        const float *sl = a.g.slab[k] + j;
+                        const int64_t n = a.g.n[k];
+                        const int zc = a.g.z[k];
+                        float v = 0.0f;
+                        for (int z0 = sub; z0 < zc; z0 += 8 * 16) {
+                            float x[16];
+#pragma unroll
+                            for (int u = 0; u < 16; ++u) x[u] = z0 + 8 * u < zc ? sl[(int64_t)(z0 + 8 * u) * n] : 0.0f;
+#pragma unroll
+                            for (int u = 0; u < 16; ++u) v += x[u];
+                        }
+                        v += __shfl_xor(v, 1, 64);
+                        v += __shfl_xor(v, 2, 64);
+                        v += __shfl_xor(v, 4, 64);
+                        g = v;
+                    }
+                }
+                if (sub == 0) a.grad[i] = g;
             }
-            if (a.apply) rms_one(a, i, g, due, omr);
+            if (a.apply && sub == 0) rms_one(a, i, g, due, omr);
         }
     }
     // every block read *counter (nb) above; the last to arrive advances it. The bookkeeping

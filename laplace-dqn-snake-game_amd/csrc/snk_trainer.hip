@@ -93,14 +93,16 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     chain = chain && upd && !q->deep;
     next_chain = next_chain && upd && !q->deep;
     // the first update's sample (counting the n transitions this step stores) rides in a
-    // spare workgroup of the act forward's head launch (batch <= 64)
+    // spare workgroup of a launch of the act forward (batch <= 64): the weight-max scan or the
+    // fused conv kernel (small net), the head (deep net)
     const bool ride = upd && h->B <= 64;
     if (chain) q->act.wmax_fresh = 1;
     HeadArgs ha;
+    SampleRider rider;
     if (ride) {
-        SampleRider &rider = ha.rider;
         rider.count = R.count; rider.cap = R.cap; rider.pending = E.n; rider.batch = h->B; rider.seed = sseed;
         rider.draw_dev = &h->stats->updates; rider.out = h->idx;
+        if (q->deep) ha.rider = rider;
     } else if (upd) {
         replay_launch_sample(R, h->B, sseed, 0, &h->stats->updates, h->idx, nullptr, s, E.n);
     }
@@ -111,7 +113,8 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     if (q->deep)
         deep_forward(q, SNK_NET_Q, src_env(E), E.n, HEAD_ACT, ha, s);
     else
-        qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q);
+        qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q,
+                     ride ? &rider : nullptr);
     // step! + virtual_step + store! + the episode statistics, one launch
     const EpisodeAcc acc{&h->stats->episodes, &h->stats->score_sum, &h->stats->env_steps, &h->stats->reward_sum,
                          &h->stats->reward_max, &h->stats->score_max};
