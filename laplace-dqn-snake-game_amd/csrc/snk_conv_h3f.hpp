@@ -299,7 +299,8 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     // written to conv3's image as one 8-byte piece per part. 16-row tiles
     // t = wave + 8u; offset pair p outermost so each weight fragment is read once
     f32x4v acc2[U2][2];
-    int rsl[U2], rpos[U2];   // this lane's row (column r of tile u): sample, A-image position
+    // this lane's row (column r of tile u): sample, A1-image position, conv3 image slot
+    int rsl[U2], rpos[U2], aslot[U2];
 #pragma unroll
     for (int u = 0; u < U2; ++u) {
         acc2[u][0] = acc2[u][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
@@ -307,6 +308,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         rsl[u] = q / hin2;
         const int pos = q - rsl[u] * hin2, j = pos / hin, i = pos - j * hin;
         rpos[u] = i + j * BP;
+        aslot[u] = rsl[u] * XS + (g >> 1) * GG + j * XW + i;
     }
 #pragma unroll
     for (int p = 0; p < 5; ++p) {
@@ -349,24 +351,28 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         for (int u = 0; u < UF; ++u) tile(u);
     }
     // acc2[u][ct][e]: channel co = 16 ct + 4 g + e of row (wave + 8u) * 16 + r.
-    // bias + relu in place; per-sample max (rows of absent samples excluded)
+    // bias + relu in place; per-sample max: the row's eight channels first, then one
+    // select per sample (the lane's row is one sample's). Rows past R2 in the last tile
+    // repeat row R2 - 1 (rsl is clamped), so they leave the maxima unchanged; rows of
+    // absent samples only reach their own maxima and image rows, which no stored output
+    // reads; a tile the wave does not have counts nothing
     float m2[NSG] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int u = 0; u < U2; ++u) {
-        const int row = (wave + 8 * u) * 16 + r;
         const int sr = rsl[u];
-        const bool live = wave + 8 * u < T2 && row < R2 && sr < ns;
         const int es = (sr == 0 ? ea1[0] : sr == 1 ? ea1[1] : sr == 2 ? ea1[2] : ea1[3]) + ew2;
+        float lm = 0.0f;
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                float v = __builtin_ldexpf(acc2[u][ct][e], -es) + b2v[ct][e];
-                v = (live && v > 0.0f) ? v : 0.0f;
+                const float v = fmaxf(__builtin_ldexpf(acc2[u][ct][e], -es) + b2v[ct][e], 0.0f);
                 acc2[u][ct][e] = v;
-#pragma unroll
-                for (int q = 0; q < NSG; ++q) m2[q] = sr == q ? fmaxf(m2[q], v) : m2[q];
+                lm = fmaxf(lm, v);
             }
+        if (wave + 8 * u >= T2) lm = 0.0f;
+#pragma unroll
+        for (int q = 0; q < NSG; ++q) m2[q] = sr == q ? fmaxf(m2[q], lm) : m2[q];
     }
 #pragma unroll
     for (int q = 0; q < NSG; ++q) m2[q] = wave_max(m2[q]);
@@ -391,12 +397,11 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     for (int u = 0; u < U2; ++u) {
         const int row = (wave + 8 * u) * 16 + r;
         if (wave + 8 * u < T2 && row < R2) {
-            const int sr = rsl[u], pos = row - sr * hin2;
-            const int j = pos / hin, i = pos - j * hin;
+            const int sr = rsl[u];
             const int es = sr == 0 ? ea[0] : sr == 1 ? ea[1] : sr == 2 ? ea[2] : ea[3];
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) {
-                const int slot = sr * XS + (ct * 2 + (g >> 1)) * GG + j * XW + i;
+                const int slot = aslot[u] + ct * 2 * GG;
                 u32x2 hh, ll;
                 h3_split4(f32x4{acc2[u][ct][0], acc2[u][ct][1], acc2[u][ct][2], acc2[u][ct][3]}, es, hh, ll);
                 Ah2[slot * 2 + (g & 1)] = hh;
