@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "snk_deep.hpp"
+#include "snk_deep_bwd.hpp"
 #include "snk_dqn.hpp"
 
 namespace snk {
@@ -38,6 +39,8 @@ DeepLayout deep_layout(int bs, int C) {
     }
     D.img_d1 = t;
     t += (int64_t)D.K1 * 64;
+    D.img_w3t = t;
+    t += 36LL * 64 * 64;
     D.img_n = t;
     D.img0_n = 9LL * C * 32 + 32;
     return D;
@@ -316,8 +319,8 @@ static void wgrad(DeepNet &Nn, const AL &al, const float *dz, int64_t R, int M, 
 }
 
 template <int BS>
-static void deep_backward_bs(DeepNet &Nn, const float *th, const BoardSrc &src, int64_t B, DeepWork &w, float *grad,
-                             hipStream_t s) {
+static void deep_backward_bs(DeepNet &Nn, const float *th, const uint16_t *wimg, const BoardSrc &src, int64_t B,
+                             DeepWork &w, float *grad, hipStream_t s) {
     const DeepLayout &D = Nn.D;
     constexpr int NC = BS * BS, WO = BS - 5, NO = WO * WO, K1 = NO * 64;
     const QLayout H = deep_head_layout(D);
@@ -326,12 +329,21 @@ static void deep_backward_bs(DeepNet &Nn, const float *th, const BoardSrc &src, 
     wgrad<2>(Nn, ADenseDw<uint16_t>{w.a[3], K1, B}, w.dz1, B, K1 + 1, 64, grad, D.off_d1w, s);
     gemm_bf16<2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + D.off_d1w, 64, K1, 64}, EpReluMaskB{w.dz[3], w.a[3], B, K1},
                  B, K1, 64, plan_gemm(B, K1, 2, 64, false), s);
-    // L3: 6x6, 64 -> 64, valid
-    wgrad<2>(Nn, AConvDw<64, 6, 0, uint16_t>{w.a[2], BS, WO, B * NO, FastDiv(NO), FastDiv(WO)}, w.dz[3], B * NO,
-             36 * 64 + 1, 64, grad, D.off_w[3], s);
-    gemm_bf16<2>(AConvDx<64, 6, 0>{w.dz[3], BS, WO, FastDiv(NC), FastDiv(BS)}, BConvT<64, 64>{th + D.off_w[3], 36 * 64},
-                 EpReluMaskB{w.dz[2], w.a[2], B * NC, 64}, B * NC, 64, 36 * 64, plan_gemm(B * NC, 64, 2, 36 * 64, false),
-                 s);
+    // L3: 6x6, 64 -> 64, valid (snk_deep_bwd.hpp): weight gradient into pair slabs, data gradient per tile row
+    {
+        using Sw = DeepL3DwShape<BS>;
+        using Sx = DeepL3DxShape<BS>;
+        const int64_t Z = (B + 1) / 2;
+        SNK_CHECK(Z * Sw::MN <= Nn.bslab_floats, SNK_ERR_INTERNAL, "deep backward slab too small");
+        set_lds_limit((const void *)deep_conv3_dw_kernel<BS>, Sw::LDS);
+        deep_conv3_dw_kernel<BS><<<dim3(6, (unsigned)Z), 512, Sw::LDS, s>>>(w.dz[3], w.a[2], Nn.bslab, B);
+        launch_check("deep_conv3_dw_kernel");
+        slab_reduce_launch(Nn.bslab, (int)Z, Sw::MN, grad + D.off_w[3], s);
+        set_lds_limit((const void *)deep_conv3_dx_kernel<BS>, Sx::LDS);
+        deep_conv3_dx_kernel<BS><<<dim3(Sx::NB, (unsigned)B), 512, Sx::LDS, s>>>(w.dz[3], wimg + D.img_w3t, w.a[2],
+                                                                                 w.dz[2], B);
+        launch_check("deep_conv3_dx_kernel");
+    }
     // L2: 3x3, 32 -> 64
     wgrad<2>(Nn, AConvDw<32, 3, 1, uint16_t>{w.a[1], BS, BS, B * NC, FastDiv(NC), FastDiv(BS)}, w.dz[2], B * NC,
              9 * 32 + 1, 64, grad, D.off_w[2], s);
@@ -348,14 +360,14 @@ static void deep_backward_bs(DeepNet &Nn, const float *th, const BoardSrc &src, 
 }
 
 static int64_t backward_slab_floats(const DeepLayout &D, int64_t B) {
-    const int64_t nc = (int64_t)D.bs * D.bs, no = (int64_t)D.Wo * D.Wo;
+    const int64_t nc = (int64_t)D.bs * D.bs;
     int64_t need = 0;
     auto add = [&](int64_t M, int N, int NT, int64_t R) {
         const GemmPlan p = wgrad_plan(M, N, NT, R);
         if (p.z > 1) need = std::max(need, (int64_t)p.z * M * N);
     };
     add(D.K1 + 1, 64, 2, B);
-    add(36 * 64 + 1, 64, 2, B * no);
+    need = std::max(need, (B + 1) / 2 * ((36 * 64 + 1) * 64));   // deep_conv3_dw_kernel's pair slabs
     add(9 * 32 + 1, 64, 2, B * nc);
     add(9 * 32 + 1, 32, 1, B * nc);
     add(9 * D.C + 1, 32, 1, B * nc);
@@ -523,9 +535,9 @@ void deep_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src,
                      la, s);
     if (loss_mean) loss_mean_launch(N.trn.loss, B, h->loss_dev, s);
     switch (N.D.bs) {
-        case 10: deep_backward_bs<10>(N, h->theta_q, s_src, B, N.trn, h->grad, s); break;
-        case 12: deep_backward_bs<12>(N, h->theta_q, s_src, B, N.trn, h->grad, s); break;
-        default: deep_backward_bs<20>(N, h->theta_q, s_src, B, N.trn, h->grad, s); break;
+        case 10: deep_backward_bs<10>(N, h->theta_q, N.img_q, s_src, B, N.trn, h->grad, s); break;
+        case 12: deep_backward_bs<12>(N, h->theta_q, N.img_q, s_src, B, N.trn, h->grad, s); break;
+        default: deep_backward_bs<20>(N, h->theta_q, N.img_q, s_src, B, N.trn, h->grad, s); break;
     }
 }
 

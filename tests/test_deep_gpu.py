@@ -104,6 +104,21 @@ def test_deep_loss_grad_and_update_vs_oracle(snk, bs, C):
     print(f"deep bs {bs}: loss {loss:.6f} vs {lref:.6f}; gradient normwise err {gerr:.2e}")
     assert abs(loss - lref) <= 2e-3 * abs(lref)
     assert gerr <= 1e-3
+    # every layer's block on its own (a wrong L3 weight or bias gradient must not hide
+    # inside the Dense1 block's norm): the Flux.destructure order of structs.jl:127-139
+    o, blocks = 0, []
+    for ks, ci, co in ((3, C, 32), (3, 32, 32), (3, 32, 64), (6, 64, 64)):
+        blocks += [(f"conv{len(blocks) // 2}.w", o, o + ks * ks * ci * co)]
+        o += ks * ks * ci * co
+        blocks += [(f"conv{len(blocks) // 2}.b", o, o + co)]
+        o += co
+    K1 = (bs - 5) ** 2 * 64
+    blocks += [("d1.w", o, o + K1 * 64), ("d1.b", o + K1 * 64, o + K1 * 64 + 64)]
+    assert o + K1 * 64 + 64 + 3 * 64 + 3 == m.P
+    for name, a, b_ in blocks:
+        e = np.linalg.norm(g[a:b_] - gref[a:b_]) / max(np.linalg.norm(gref[a:b_]), 1e-30)
+        print(f"  {name}: normwise err {e:.2e}")
+        assert e <= 2e-3, name
     m.apply_grad()
     th1, _ = oracle.rmsprop(p, np.zeros_like(p), g)
     assert np.array_equal(m.get_params(), th1)
