@@ -693,25 +693,43 @@ __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__rest
     for (int t = 0; t < NR; ++t)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int k = k0;
-    for (; k + 64 <= k1; k += 64) {
-        u32x4 a[NR][2], b[2][4];
+    // 64-k steps through a ring of RING register sets, loaded RING - 1 steps ahead: the A
+    // stream comes from HBM (a4 is written by L3 just before and is far larger than the
+    // MALL), and two steps in flight per wave (one ahead) left it latency-bound
+    constexpr int RING = 4;
+    const int nst = (k1 - k0) / 64;
+    u32x4 a[RING][NR][2], b[RING][2][4];
+    auto load = [&](int st, u32x4 (&ar)[NR][2], u32x4 (&br)[2][4]) __attribute__((always_inline)) {
+        const int kk = k0 + 64 * st;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
-            for (int t = 0; t < NR; ++t) a[t][u] = *reinterpret_cast<const u32x4 *>(pa[t] + k + 32 * u);
+            for (int t = 0; t < NR; ++t) ar[t][u] = *reinterpret_cast<const u32x4 *>(pa[t] + kk + 32 * u);
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) b[u][nt] = *reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + k + 32 * u);
+            for (int nt = 0; nt < 4; ++nt) br[u][nt] = *reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + kk + 32 * u);
         }
+    };
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+    for (int o = 0; o < RING - 1; ++o)
+        if (o < nst) load(o, a[o], b[o]);
+#pragma unroll 1
+    for (int st = 0; st < nst; st += RING) {
 #pragma unroll
-            for (int t = 0; t < NR; ++t)
+        for (int o = 0; o < RING; ++o) {
+            if (st + o < nst) {   // wave-uniform
+                if (st + o + RING - 1 < nst) load(st + o + RING - 1, a[(o + RING - 1) % RING], b[(o + RING - 1) % RING]);
 #pragma unroll
-                for (int nt = 0; nt < 4; ++nt)
-                    acc[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a[t][u]), as_bf(b[u][nt]), acc[t][nt], 0, 0, 0);
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int t = 0; t < NR; ++t)
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt)
+                            acc[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a[o][t][u]), as_bf(b[o][u][nt]),
+                                                                                 acc[t][nt], 0, 0, 0);
+            }
+        }
     }
-    for (; k < k1; k += 32) {
+    for (int k = k0 + 64 * nst; k < k1; k += 32) {
         u32x4 b[4];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) b[nt] = *reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + k);
