@@ -39,8 +39,11 @@ DeepLayout deep_layout(int bs, int C) {
     }
     D.img_d1 = t;
     t += (int64_t)D.K1 * 64;
-    D.img_w3t = t;
-    t += 36LL * 64 * 64;
+    D.img_wt[0] = -1;
+    for (int l = 1; l < 4; ++l) {
+        D.img_wt[l] = t;
+        t += (int64_t)ks[l] * ks[l] * ci[l] * co[l];
+    }
     D.img_n = t;
     D.img0_n = 9LL * C * 32 + 32;
     return D;
@@ -318,6 +321,26 @@ static void wgrad(DeepNet &Nn, const AL &al, const float *dz, int64_t R, int M, 
     if (p.z > 1) slab_reduce_launch(Nn.bslab, p.z, (int64_t)M * N, grad + off, s);
 }
 
+// a conv layer's weight gradient (deep_conv_dw_kernel, NS samples per chunk) into grad_w (weights, then bias)
+template <int CI, int CO, int KS, int PAD, int H, int NS>
+static void conv_dw(DeepNet &Nn, const float *dz, const uint16_t *x, int64_t B, float *grad_w, hipStream_t s) {
+    using Sw = DeepDwShape<CI, CO, KS, PAD, H, NS>;
+    const int64_t Z = (B + NS - 1) / NS;
+    SNK_CHECK(Z * Sw::MN <= Nn.bslab_floats, SNK_ERR_INTERNAL, "deep backward slab too small");
+    set_lds_limit((const void *)deep_conv_dw_kernel<CI, CO, KS, PAD, H, NS>, Sw::LDS);
+    deep_conv_dw_kernel<CI, CO, KS, PAD, H, NS><<<dim3(KS, (unsigned)Z), 512, Sw::LDS, s>>>(dz, x, Nn.bslab, B);
+    launch_check("deep_conv_dw_kernel");
+    slab_reduce_launch(Nn.bslab, (int)Z, Sw::MN, grad_w, s);
+}
+// its data gradient (deep_conv_dx_kernel), relu-masked by the layer input x
+template <int CI, int CO, int KS, int PAD, int H>
+static void conv_dx(const float *dz, const uint16_t *wt, const uint16_t *x, float *dx, int64_t B, hipStream_t s) {
+    using Sx = DeepDxShape<CI, CO, KS, PAD, H>;
+    set_lds_limit((const void *)deep_conv_dx_kernel<CI, CO, KS, PAD, H>, Sx::LDS);
+    deep_conv_dx_kernel<CI, CO, KS, PAD, H><<<dim3(Sx::NB, (unsigned)B), 512, Sx::LDS, s>>>(dz, wt, x, dx, B);
+    launch_check("deep_conv_dx_kernel");
+}
+
 template <int BS>
 static void deep_backward_bs(DeepNet &Nn, const float *th, const uint16_t *wimg, const BoardSrc &src, int64_t B,
                              DeepWork &w, float *grad, hipStream_t s) {
@@ -329,31 +352,14 @@ static void deep_backward_bs(DeepNet &Nn, const float *th, const uint16_t *wimg,
     wgrad<2>(Nn, ADenseDw<uint16_t>{w.a[3], K1, B}, w.dz1, B, K1 + 1, 64, grad, D.off_d1w, s);
     gemm_bf16<2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + D.off_d1w, 64, K1, 64}, EpReluMaskB{w.dz[3], w.a[3], B, K1},
                  B, K1, 64, plan_gemm(B, K1, 2, 64, false), s);
-    // L3: 6x6, 64 -> 64, valid (snk_deep_bwd.hpp): weight gradient into pair slabs, data gradient per tile row
-    {
-        using Sw = DeepL3DwShape<BS>;
-        using Sx = DeepL3DxShape<BS>;
-        const int64_t Z = (B + 1) / 2;
-        SNK_CHECK(Z * Sw::MN <= Nn.bslab_floats, SNK_ERR_INTERNAL, "deep backward slab too small");
-        set_lds_limit((const void *)deep_conv3_dw_kernel<BS>, Sw::LDS);
-        deep_conv3_dw_kernel<BS><<<dim3(6, (unsigned)Z), 512, Sw::LDS, s>>>(w.dz[3], w.a[2], Nn.bslab, B);
-        launch_check("deep_conv3_dw_kernel");
-        slab_reduce_launch(Nn.bslab, (int)Z, Sw::MN, grad + D.off_w[3], s);
-        set_lds_limit((const void *)deep_conv3_dx_kernel<BS>, Sx::LDS);
-        deep_conv3_dx_kernel<BS><<<dim3(Sx::NB, (unsigned)B), 512, Sx::LDS, s>>>(w.dz[3], wimg + D.img_w3t, w.a[2],
-                                                                                 w.dz[2], B);
-        launch_check("deep_conv3_dx_kernel");
-    }
-    // L2: 3x3, 32 -> 64
-    wgrad<2>(Nn, AConvDw<32, 3, 1, uint16_t>{w.a[1], BS, BS, B * NC, FastDiv(NC), FastDiv(BS)}, w.dz[2], B * NC,
-             9 * 32 + 1, 64, grad, D.off_w[2], s);
-    gemm_bf16<1>(AConvDx<64, 3, 1>{w.dz[2], BS, BS, FastDiv(NC), FastDiv(BS)}, BConvT<32, 64>{th + D.off_w[2], 9 * 64},
-                 EpReluMaskB{w.dz[1], w.a[1], B * NC, 32}, B * NC, 32, 9 * 64, plan_gemm(B * NC, 32, 1, 9 * 64, false), s);
-    // L1: 3x3, 32 -> 32
-    wgrad<1>(Nn, AConvDw<32, 3, 1, uint16_t>{w.a[0], BS, BS, B * NC, FastDiv(NC), FastDiv(BS)}, w.dz[1], B * NC,
-             9 * 32 + 1, 32, grad, D.off_w[1], s);
-    gemm_bf16<1>(AConvDx<32, 3, 1>{w.dz[1], BS, BS, FastDiv(NC), FastDiv(BS)}, BConvT<32, 32>{th + D.off_w[1], 9 * 32},
-                 EpReluMaskB{w.dz[0], w.a[0], B * NC, 32}, B * NC, 32, 9 * 32, plan_gemm(B * NC, 32, 1, 9 * 32, false), s);
+    // L3 (6x6, 64 -> 64, valid), L2 and L1 (3x3 pad 1) on snk_deep_bwd.hpp: weight gradients into
+    // chunk slabs (summed in chunk order), data gradients per tile row
+    conv_dw<64, 64, 6, 0, BS, 2>(Nn, w.dz[3], w.a[2], B, grad + D.off_w[3], s);
+    conv_dx<64, 64, 6, 0, BS>(w.dz[3], wimg + D.img_wt[3], w.a[2], w.dz[2], B, s);
+    conv_dw<32, 64, 3, 1, BS, 1>(Nn, w.dz[2], w.a[1], B, grad + D.off_w[2], s);
+    conv_dx<32, 64, 3, 1, BS>(w.dz[2], wimg + D.img_wt[2], w.a[1], w.dz[1], B, s);
+    conv_dw<32, 32, 3, 1, BS, 1>(Nn, w.dz[1], w.a[0], B, grad + D.off_w[1], s);
+    conv_dx<32, 32, 3, 1, BS>(w.dz[1], wimg + D.img_wt[1], w.a[0], w.dz[0], B, s);
     // L0: weights only, from the boards
     wgrad<1>(Nn, ABoardDw{src, BS, D.C, B * NC, FastDiv(NC), FastDiv(BS)}, w.dz[0], B * NC, 9 * D.C + 1, 32, grad,
              D.off_w[0], s);
@@ -367,9 +373,8 @@ static int64_t backward_slab_floats(const DeepLayout &D, int64_t B) {
         if (p.z > 1) need = std::max(need, (int64_t)p.z * M * N);
     };
     add(D.K1 + 1, 64, 2, B);
-    need = std::max(need, (B + 1) / 2 * ((36 * 64 + 1) * 64));   // deep_conv3_dw_kernel's pair slabs
-    add(9 * 32 + 1, 64, 2, B * nc);
-    add(9 * 32 + 1, 32, 1, B * nc);
+    need = std::max(need, (B + 1) / 2 * ((36 * 64 + 1) * 64));   // deep_conv_dw_kernel's chunk slabs: L3 (pairs),
+    need = std::max(need, B * ((9 * 32 + 1) * 64));                 // L2 and L1 (one sample per chunk)
     add(9 * D.C + 1, 32, 1, B * nc);
     return std::max<int64_t>(need, 1);
 }

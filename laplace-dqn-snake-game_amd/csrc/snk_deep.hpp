@@ -52,7 +52,7 @@ struct DeepLayout {
     int64_t off_w[4], off_b[4], off_d1w, off_d1b, off_d2w, off_d2b, P;
     // bf16 weight image: conv L1..L3 [kk][co][ci], Dense1 [o][f]; L0 as
     // bf16-rounded fp32 [9C][32] (VALU)
-    int64_t img_w[4], img_d1, img_w3t, img_n;   // img_w3t: L3 weights in packed order [kk][ci][co] (data gradient)
+    int64_t img_w[4], img_d1, img_wt[4], img_n;   // img_wt[l]: L1..L3 weights in packed order [kk][ci][co] (data gradients)
     int64_t img0_n;                            // floats of the L0 image
 };
 DeepLayout deep_layout(int bs, int C);
@@ -72,8 +72,10 @@ __global__ void deep_image_kernel(const float *__restrict__ th, uint16_t *__rest
             img0[u] = u < nw ? bf2f(f2bf(th[D.off_w[0] + u])) : th[D.off_b[0] + (u - nw)];
             continue;
         }
-        if (t >= D.img_w3t) {   // L3 [kk][ci][co]: the packed order, for the data gradient's A operand
-            img[t] = f2bf(th[D.off_w[3] + (t - D.img_w3t)]);
+        if (t >= D.img_wt[1]) {   // L1..L3 [kk][ci][co]: the packed order, the data gradients' A operand
+            int l = 1;
+            while (l < 3 && t >= D.img_wt[l + 1]) ++l;
+            img[t] = f2bf(th[D.off_w[l] + (t - D.img_wt[l])]);
             continue;
         }
         if (t >= D.img_d1) {   // Dense1 [o][f] <- packed W[f][o]
