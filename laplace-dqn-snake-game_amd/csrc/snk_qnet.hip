@@ -706,6 +706,97 @@ __global__ __launch_bounds__(256) void head_pair_kernel(HeadNet tn, HeadNet qn, 
 }
 
 // backward of Dense2 + relu: dz1[s][o] = (h1 > 0) * sum_a dq[s][a] W2[a][o]
+// Dense1's backward at the update's batch (S <= 64) in one launch of small LDS-staged
+// GEMMs on the fp64 matrix cores (v_mfma_f64_16x16x4_f64: fp32 operands converted exactly,
+// products exact, sums in fp64, rounded once). The generic split-K pair (pair_kernel, f32
+// MFMA, operands gathered element by element through the implicit loaders) took 11 us for
+// 2 x 26 MFLOP. Blocks, each owning a block of D1B_F features f (K1 is a multiple of 64):
+//  * [0, nfb): dz3[s][f] = (a3[s][f] > 0) * sum_o dz1[s][o] W1[f][o]   (M = s, N = f, K = o)
+//  * [nfb, 2 nfb): dW1[f][o] = sum_s a3[s][f] dz1[s][o]                 (M = f, N = o, K = s)
+//  * 2 nfb: the bias row dW1[K1][o] = sum_s dz1[s][o]
+// The sums are more accurate than the fp32-accumulating forms (a VALU version with fp32 fma
+// chains drifted the free-running configs[0] trajectory to 2e-5 of the oracle's loss).
+// f64 16x16x4 operand map: lane l holds A[l & 15][k = l >> 4], B[k = l >> 4][l & 15]; D row
+// (l >> 4) + 4i, column l & 15.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int D1B_F = 32, D1B_P = 66, D1B_PA = 48;   // features per block, LDS row pitches (floats)
+__global__ __launch_bounds__(512) void d1_bwd_kernel(const float *__restrict__ a3, const float *__restrict__ dz1,
+                                                     const float *__restrict__ w1, float *__restrict__ dz3,
+                                                     float *__restrict__ dw, int S, int K1, int nfb) {
+    __shared__ float sdz[64 * D1B_P];             // dz1 [s][o]
+    __shared__ float sx[64 * D1B_P];              // dX: W1 rows [f][o]; dW: a3 [s][f] (pitch D1B_PA)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, kq = lane >> 4;
+    const int b = blockIdx.x;
+    const bool dx = b < nfb;
+    const int f0 = (dx ? b : b - nfb) * D1B_F;
+    {   // staging: every float4 load first (dz1: 2 per thread, the W1 or a3 block: 1), then the LDS stores
+        f32x4 vz[2], vx = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int q = tid + 512 * u, s = q >> 4;
+            vz[u] = s < S ? *reinterpret_cast<const f32x4 *>(dz1 + q * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        const int fx = tid >> 4, px = tid & 15;             // dX: W1 row f0 + fx, quad px
+        const int sa = tid >> 3, pa = tid & 7;              // dW: a3 row sa, quad pa of the block
+        if (b < 2 * nfb) {
+            if (dx) vx = *reinterpret_cast<const f32x4 *>(w1 + (int64_t)(f0 + fx) * 64 + 4 * px);
+            else if (sa < S) vx = *reinterpret_cast<const f32x4 *>(a3 + (int64_t)sa * K1 + f0 + 4 * pa);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int q = tid + 512 * u, s = q >> 4, o = (q & 15) * 4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sdz[s * D1B_P + o + e] = vz[u][e];
+        }
+        if (dx) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sx[fx * D1B_P + 4 * px + e] = vx[e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sx[sa * D1B_PA + 4 * pa + e] = vx[e];
+        }
+    }
+    __syncthreads();
+    if (b == 2 * nfb) {   // bias row
+        if (tid < 64) {
+            double v = 0.0;
+            for (int s = 0; s < S; ++s) v += (double)sdz[s * D1B_P + tid];
+            dw[(int64_t)K1 * 64 + tid] = (float)v;
+        }
+        return;
+    }
+    // 8 output tiles per block, one per wave
+    f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+    if (dx) {   // tile = wave: s tile wave >> 1 (of 4), f tile wave & 1 (of 2)
+        const int mt = wave >> 1, nt = wave & 1;
+#pragma unroll
+        for (int k = 0; k < 64; k += 4)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)sdz[(16 * mt + r) * D1B_P + k + kq],
+                                                       (double)sx[(16 * nt + r) * D1B_P + k + kq], acc, 0, 0, 0);
+        const int f = f0 + 16 * nt + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int s = 16 * mt + kq + 4 * i;
+            if (s < S) {
+                const int64_t o = (int64_t)s * K1 + f;
+                dz3[o] = a3[o] > 0.0f ? (float)acc[i] : 0.0f;
+            }
+        }
+    } else {    // tile = wave: f tile wave >> 2 (of 2), o tile wave & 3 (of 4)
+        const int mt = wave >> 2, nt = wave & 3;
+#pragma unroll
+        for (int k = 0; k < 64; k += 4)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)sx[(k + kq) * D1B_PA + 16 * mt + r],
+                                                       (double)sdz[(k + kq) * D1B_P + 16 * nt + r], acc, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = f0 + 16 * mt + kq + 4 * i;
+            dw[(int64_t)f * 64 + 16 * nt + r] = (float)acc[i];
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float *__restrict__ dq, const float *__restrict__ h1,
                                                        const float *__restrict__ theta, QLayout L, int64_t S,
                                                        float *__restrict__ dz1) {
@@ -1315,6 +1406,11 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         // Dense1: dW (+ bias row) | dX with the relu mask of a3
         const int64_t M1 = L.K1 + 1;
         float *d1d = dst(0, p.d1, L.off_d1w, M1 * 64, slab + sr.d1);
+        if (S <= 64 && p.d1.z == 1 && L.K1 % D1B_F == 0) {   // d1_bwd_kernel (fp64 MFMA, one launch)
+            const int nfb = L.K1 / D1B_F;
+            d1_bwd_kernel<<<2 * nfb + 1, 512, 0, s>>>(w.a3, w.dz1, th + L.off_d1w, w.dz3, d1d, (int)S, L.K1, nfb);
+            launch_check("d1_bwd_kernel");
+        } else
         pair_launch<128>(gemm_job<2, 2>(ADenseDw<>{w.a3, L.K1, S}, BRows{w.dz1, S, 64}, EpSlab{d1d, (int)M1, 64}, M1,
                                         64, S, p.d1),
                          gemm_job<2, 2>(ARowMajor{w.dz1, 64, 64}, BTrans{th + L.off_d1w, 64, L.K1, 64},
