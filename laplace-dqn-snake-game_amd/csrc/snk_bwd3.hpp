@@ -268,7 +268,7 @@ constexpr int C2_DS = 48, C2_BS = 36, C2_WS = 36;   // LDS row strides (floats),
 
 __host__ __device__ inline int c2_bwd_lds_floats(int bs) {
     const int bp2 = (bs + 2) * (bs + 2);
-    int dw = bp2 * 16 + bs * bs * C2_DS, dx = bp2 * C2_BS + 144 * C2_WS;
+    int dw = bp2 * 16 + bs * bs * C2_DS, dx = bp2 * C2_BS + 144 * C2_WS + 2 * bp2;   // + conv1's planes (C <= 2)
     if (dw < 4 * 4608) dw = 4 * 4608;   // the weight-gradient block's cross-wave sum
     return dw > dx ? dw : dx;
 }
@@ -393,6 +393,15 @@ __device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb
                 }
             }
         }
+        // conv1's input planes inside a zero border (the fused conv1 weight gradient reads them
+        // from LDS: a global load per MFMA operand left the MFMA chain waiting on each)
+        if (a.c1slab) {
+            float *Xb = Wl + 144 * C2_WS;
+            for (int e = tid; e < a.C * bp2; e += 256) {
+                const int c = e / bp2, pb = e - c * bp2, jj = pb / bp - 1, ii = pb - (jj + 1) * bp - 1;
+                Xb[e] = (ii >= 0 && ii < bs && jj >= 0 && jj < bs) ? a.x.load(s, c, ii + jj * bs) : 0.0f;
+            }
+        }
         const f32x4 *sw = reinterpret_cast<const f32x4 *>(a.w);
         f32x4 v[5];   // 144 rows x 8 float4 = 1152 = 4.5 per thread
 #pragma unroll
@@ -452,8 +461,8 @@ __device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb
                 if (pos < bs2) {
                     if (k1 < nrow) {
                         const int kk = k1 / a.C, c = k1 - kk * a.C;
-                        const int xi = pi + kk % 3 - 1, xj = pj + kk / 3 - 1;
-                        if (xi >= 0 && xi < bs && xj >= 0 && xj < bs) xv = a.x.load(s, c, xi + xj * bs);
+                        // bordered (pi + kk % 3, pj + kk / 3) = input (pi + kk % 3 - 1, pj + kk / 3 - 1)
+                        xv = Wl[144 * C2_WS + c * bp2 + (pi + kk % 3) + (pj + kk / 3) * bp];
                     } else if (k1 == nrow) {
                         xv = 1.0f;
                     }
