@@ -1206,6 +1206,66 @@ static bool upd_fwd_launch(const UpdFwdArgs &a, hipStream_t s) {
 #undef SNK_UPDF
 }
 
+// Dense1 of the update's two nets (S <= 64 samples each) into the head's K-split slabs, on
+// the fp64 matrix cores: block (output half, slab z, net) stages its slab's a3 columns
+// (S x F, F = the slab's features <= 256) and W1 rows (F x 32) by float4 loads into LDS, one
+// 16x16 output tile per wave over k = F (v_mfma_f64_16x16x4_f64: fp32 operands, fp64 sums,
+// rounded once per slab). The x6 conv kernel (MODE_DENSE) ran these 26 slab blocks of 128
+// rows (64 of them real) at 10.3 us.
+constexpr int D1U_FMAX = 256, D1U_AP = D1U_FMAX + 2, D1U_WP = 48;   // LDS pitches (floats): conflict-free reads
+struct D1UpdNet {
+    const float *a3, *w1;   // a3 [S][K1], W1 [K1][64] (packed: theta + off_d1w)
+    float *slab;            // [ks][S][64]
+};
+__global__ __launch_bounds__(512) void dense1_upd_kernel(D1UpdNet n0, D1UpdNet n1, int S, int K1, int F) {
+    extern __shared__ __attribute__((aligned(16))) float d1sm[];
+    float *As = d1sm, *Ws = d1sm + 64 * D1U_AP;
+    const D1UpdNet n = blockIdx.z ? n1 : n0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int half = blockIdx.x, z = blockIdx.y;
+    const int f0 = z * F, fn = min(F, K1 - f0);   // features of this slab (a multiple of 64)
+    {
+        constexpr int PA = 64 * D1U_FMAX / 4 / 512, PW = D1U_FMAX * 32 / 4 / 512;   // float4 per thread
+        f32x4 va[PA], vw[PW];
+#pragma unroll
+        for (int u = 0; u < PA; ++u) {   // a3 row s, quad c of the slab
+            const int e = tid + 512 * u, sr = e / (D1U_FMAX / 4), c = e - sr * (D1U_FMAX / 4);
+            va[u] = (sr < S && 4 * c < fn) ? *reinterpret_cast<const f32x4 *>(n.a3 + (int64_t)sr * K1 + f0 + 4 * c)
+                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < PW; ++u) {   // W1 row f, quad c of this output half
+            const int e = tid + 512 * u, f = e >> 3, c = e & 7;
+            vw[u] = f < fn ? *reinterpret_cast<const f32x4 *>(n.w1 + (int64_t)(f0 + f) * 64 + 32 * half + 4 * c)
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < PA; ++u) {
+            const int e = tid + 512 * u, sr = e / (D1U_FMAX / 4), c = e - sr * (D1U_FMAX / 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) As[sr * D1U_AP + 4 * c + q] = va[u][q];
+        }
+#pragma unroll
+        for (int u = 0; u < PW; ++u) {
+            const int e = tid + 512 * u, f = e >> 3, c = e & 7;
+            *reinterpret_cast<f32x4 *>(Ws + f * D1U_WP + 4 * c) = vw[u];
+        }
+    }
+    __syncthreads();
+    // wave: sample tile mt = wave >> 1, output tile nt = wave & 1 (of this half)
+    const int r = lane & 15, kq = lane >> 4, mt = wave >> 1, nt = wave & 1;
+    typedef double f64x4u __attribute__((ext_vector_type(4)));
+    f64x4u acc = {0.0, 0.0, 0.0, 0.0};
+    const float *pa = As + (16 * mt + r) * D1U_AP + kq, *pw = Ws + kq * D1U_WP + 16 * nt + r;
+    for (int k = 0; k < fn; k += 4)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)pa[k], (double)pw[k * D1U_WP], acc, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int sr = 16 * mt + kq + 4 * i;
+        if (sr < S) n.slab[((int64_t)z * S + sr) * 64 + 32 * half + 16 * nt + r] = (float)acc[i];
+    }
+}
+
 void qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s) {
     // the x6 weight planes of both nets are kept current by every theta change
     if (net[0].wtb && net[1].wtb && (L.C == 1 || L.C == 2) && S >= 1 && S <= 4096) {
@@ -1223,7 +1283,18 @@ void qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hi
                 net[g].w->x0_valid = net[g].w->has_train ? 1 : 0;
                 net[g].w->wmax_n = 0;   // no conv3 weight-max partials from this path
             }
-            forward_layers(L, net, 2, S, s, 3, 3);   // Dense1 slabs
+            int kc;
+            const int ks = d1_split(L, S, kc);
+            if (S <= 64 && kc * 64 <= D1U_FMAX) {   // Dense1 slabs on dense1_upd_kernel
+                const D1UpdNet d0{net[0].w->a3, net[0].th + L.off_d1w, net[0].w->slab};
+                const D1UpdNet d1{net[1].w->a3, net[1].th + L.off_d1w, net[1].w->slab};
+                const size_t lds = (size_t)(64 * D1U_AP + D1U_FMAX * D1U_WP) * 4;
+                set_lds_limit((const void *)dense1_upd_kernel, lds);
+                dense1_upd_kernel<<<dim3(2, (unsigned)ks, 2), 512, lds, s>>>(d0, d1, (int)S, L.K1, kc * 64);
+                launch_check("dense1_upd_kernel");
+            } else {
+                forward_layers(L, net, 2, S, s, 3, 3);   // Dense1 slabs
+            }
             return;
         }
     }
