@@ -193,7 +193,13 @@ static void conv_layers_bs(const DeepNet &N, const float *th, const uint16_t *im
     const DeepLayout &D = N.D;
     if (lo <= 1 && hi >= 1) conv_layer<32, 32, 3, 1, BS>(w.a[0], img + D.img_w[1], th + D.off_b[1], w.a[1], S, s);
     if (lo <= 2 && hi >= 2) conv_layer<32, 64, 3, 1, BS>(w.a[1], img + D.img_w[2], th + D.off_b[2], w.a[2], S, s);
-    if (lo <= 3 && hi >= 3) {   // two samples per step of a persistent workgroup (deep_conv3_kernel)
+    if (lo <= 3 && hi >= 3 && S <= 512) {   // small batches: tile rows x samples (deep_conv3_small_kernel)
+        using Sx = DeepDxShape<64, 64, 6, 5, BS - 5>;
+        set_lds_limit((const void *)deep_conv3_small_kernel<BS>, Sx::LDS);
+        deep_conv3_small_kernel<BS><<<dim3(Sx::NB, (unsigned)S), 512, Sx::LDS, s>>>(w.a[2], img + D.img_w[3],
+                                                                                   th + D.off_b[3], w.a[3], S);
+        launch_check("deep_conv3_small_kernel");
+    } else if (lo <= 3 && hi >= 3) {   // two samples per step of a persistent workgroup (deep_conv3_kernel)
         using Sh = DeepL3Shape<BS>;
         static_assert(Sh::LDS <= 160 * 1024, "deep L3 LDS");
         set_lds_limit((const void *)deep_conv3_kernel<BS>, Sh::LDS);

@@ -159,6 +159,96 @@ __global__ __launch_bounds__(512) void deep_conv_dx_kernel(const float *__restri
     }
 }
 
+// ---------------------------------------------------------------- L3 forward, small batches
+// deep_conv3_small_kernel: L3's forward (6x6, 64 -> 64, valid) at the update's batch, on the
+// data-gradient kernel's tiling (4x4 output tiles, a bordered LDS image of the tile row's input
+// rows, the weight fragments through a 4-offset register ring), so grid = NB tile rows x S
+// samples (256
+// workgroups at B = 64) instead of the persistent pair kernel's
+// B / 2 = 32 (41 us per net). Input a2 is bf16 (staged as is), the epilogue is bias + relu ->
+// bf16 a3, and the weights are the forward image [kk][co][ci] (rows co, k = ci).
+template <int H>
+__global__ __launch_bounds__(512) void deep_conv3_small_kernel(const uint16_t *__restrict__ x,
+                                                               const uint16_t *__restrict__ wimg,
+                                                               const float *__restrict__ bias,
+                                                               uint16_t *__restrict__ y, int64_t S) {
+    constexpr int WO = H - 5;
+    using Sh = DeepDxShape<64, 64, 6, 5, WO>;   // output grid WO x WO, input grid H x H
+    constexpr int NB = Sh::NB, PJ = Sh::PJ, PST = Sh::PST, ROWS = Sh::ROWS, RING = 4, NT = (NB + 1) / 2;
+    static_assert(Sh::HO == H, "input grid");
+    extern __shared__ __attribute__((aligned(16))) uint16_t c3ssm[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, g = lane >> 4, ct = wave & 3, th = wave >> 2;
+    const int tj = blockIdx.x;
+    const int64_t s = blockIdx.y;
+    if (s >= S) return;
+    // weight fragments of offset kk: rows co = 16 ct + r, k = ci 32 c + 8 g .. +7 (c = 0, 1)
+    const uint16_t *wl = wimg + (ct * 16 + r) * 64 + 8 * g;
+    u32x4 wf[RING][2];
+#pragma unroll
+    for (int o = 0; o < RING; ++o)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) wf[o][c] = *reinterpret_cast<const u32x4 *>(wl + o * 4096 + 32 * c);
+    // stage input rows 4tj .. 4tj + ROWS - 1 (image row y), columns 0 .. PJ - 1 (image column c)
+    {
+        constexpr int NP = ROWS * PJ * 8, PT = (NP + 511) / 512;   // 16-byte pieces (8 channels)
+        const uint16_t *src = x + s * (H * H * 64);
+        u32x4 v[PT];
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+            const int q = tid + u * 512, pos = q >> 3, pc = q & 7;
+            const int yy = pos / PJ, cc = pos - yy * PJ, jj = 4 * tj + yy;
+            const bool ok = q < NP && jj < H && cc < H;
+            v[u] = ok ? *reinterpret_cast<const u32x4 *>(src + (jj * H + cc) * 64 + pc * 8) : u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+            const int q = tid + u * 512, pos = q >> 3, pc = q & 7;
+            if (q < NP) *reinterpret_cast<u32x4 *>(c3ssm + pos * PST + pc * 8) = v[u];
+        }
+    }
+    __syncthreads();
+    // lane position (4 ti + (r & 3), 4 tj + (r >> 2)) reads input (i + du, j + dv): image row
+    // (r >> 2) + dv, column 4 ti + (r & 3) + du. Wave th takes row tiles th*NT .. th*NT + NT - 1
+    // (a tile past NB repeats NB - 1 and is dropped); per accumulator the MFMAs run offset by
+    // offset, channel half 0 then 1: deep_conv3_kernel's order, so a3 is bit-identical.
+    const int lbase = ((r >> 2) * PJ + (r & 3)) * PST + 8 * g;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int k4 = 0; k4 < 36; k4 += RING) {
+#pragma unroll
+        for (int o = 0; o < RING; ++o) {
+            const int kk = k4 + o, du = kk % 6, dv = kk / 6;
+            const uint16_t *Bk = c3ssm + lbase + (dv * PJ + du) * PST;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                bf16x8 xv[NT];
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+                    xv[i] = as_bf(*reinterpret_cast<const u32x4 *>(Bk + 4 * min(th * NT + i, NB - 1) * PST + 32 * c));
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wf[o][c]), xv[i], acc[i], 0, 0, 0);
+            }
+            if (kk + RING < 36) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) wf[o][c] = *reinterpret_cast<const u32x4 *>(wl + (kk + RING) * 4096 + 32 * c);
+            }
+        }
+    }
+    const f32x4 bb = *reinterpret_cast<const f32x4 *>(bias + ct * 16 + 4 * g);
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        const int ti = th * NT + i;
+        const int ii = 4 * ti + (r & 3), jj = 4 * tj + (r >> 2);
+        if (ti >= NB || ii >= WO || jj >= WO) continue;
+        *reinterpret_cast<u32x2 *>(y + (s * (WO * WO) + ii + jj * WO) * 64 + ct * 16 + 4 * g) = relu_bf16x4(acc[i], bb);
+    }
+}
+
 // ---------------------------------------------------------------- weight gradient
 // wave tile: COW co tiles x CIW ci tiles x DUW kernel columns; the first NWB of the 8
 // waves cover the KS columns x CO/16 x CI/16 tiles of one kernel row
