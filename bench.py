@@ -13,8 +13,10 @@ value = env-steps of all ranks / max-over-ranks wall time. Synthetic data:
 env dynamics are the real game from SnakeGame(); the net is glorot-initialised
 (no checkpoint of the 2-frame 12x12 net exists).
 
-python bench.py [--gpus N] [--steps K] [--warmup W]
-For N > 1 launch one process per GPU with torch.distributed.run.
+python bench.py [--gpus N] [--steps K] [--warmup W] [--workload configs1|configs3]
+For N > 1 launch one process per GPU with torch.distributed.run. --workload
+configs3 runs BASELINE configs[3]: 32,768 envs per GPU (262,144 at --gpus 8);
+the default N=1 line also carries that shard on one GPU (configs3_per_rank).
 """
 from __future__ import annotations
 
@@ -33,6 +35,14 @@ PEAK_BF16_TFLOPS = 2516.0  # MI355X_MICROARCH.md: BF16 MFMA dense peak (2.5 PF, 
 X6_PRODUCTS = 6            # bf16 MFMA products per fp32 product in the exact-split forward
 H3_PRODUCTS = 3            # fp16 MFMA products per fp32 product in the h3 conv3 (snk_conv_h3.hpp)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E spec peak
+CONFIGS3_ENVS_PER_GPU = 262144 // 8   # BASELINE configs[3]: 262,144 envs sharded over 8 GPUs
+
+
+def act_forward_flop(n: int, bs: int, C: int) -> float:
+    """FLOP of the fused act-forward kernel (conv_h3f_kernel: conv1 + conv2 + conv3)
+    over n states: 2 n (bs^2 16 9C + bs^2 32 144 + Wo^2 64 1152)."""
+    wo = bs - 5
+    return 2.0 * n * (bs * bs * 16 * 9 * C + bs * bs * 32 * 144 + wo * wo * 64 * 1152)
 
 
 def _latest_traffic(kern: str, pattern: str = "*_conv3_traffic.json"):
@@ -60,7 +70,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--repeats", type=int, default=5,
                    help="timed windows of --steps steps each; value and ms_per_step are the median window's")
-    p.add_argument("--n-envs", type=int, default=4096)
+    p.add_argument("--workload", choices=("configs1", "configs3"), default="configs1",
+                   help="configs1: 4096 envs per GPU (BASELINE configs[1], the metric's workload); configs3: "
+                        "32,768 envs per GPU, configs[3]'s 262,144 envs over 8 GPUs (--gpus 8)")
+    p.add_argument("--n-envs", type=int, default=0, help="envs per GPU (0: the workload's)")
     p.add_argument("--board-size", type=int, default=12)
     p.add_argument("--n-frames", type=int, default=2)
     p.add_argument("--updates-per-iter", type=int, default=1)
@@ -73,9 +86,13 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="skip per-kernel timing")
     p.add_argument("--no-dbuild", action="store_true", help="skip the Laplace D builds")
     p.add_argument("--no-configs2", action="store_true", help="skip the configs[2] deep bf16 net line")
+    p.add_argument("--no-configs3", action="store_true", help="skip the configs[3] per-rank shard line")
     p.add_argument("--d-samples", type=int, default=0, help="Jacobian Gram rows (0 = the whole replay buffer)")
     p.add_argument("--d-snapshots", type=int, default=1000, help="K of the snapshot D (compute_D.jl:51)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.n_envs <= 0:
+        a.n_envs = CONFIGS3_ENVS_PER_GPU if a.workload == "configs3" else 4096
+    return a
 
 
 def _cpu_model() -> str:
@@ -194,6 +211,48 @@ def configs2(args, snk, graph) -> dict:
                               "flop_per_launch": flop[d], "traffic": None},
                              **_deep_traffic(d, n, bs)),
             "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"]}}
+
+
+def configs3_per_rank(args, snk, graph) -> dict:
+    """BASELINE.json configs[3] is 262,144 lockstep envs over 8 GPUs: 32,768 per
+    GPU, each rank with its own 50k replay shard and B = 64 per update (the
+    ranks' mean gradient all-reduce adds one RCCL call per update at N > 1;
+    bench.py --workload configs3 --gpus 8 runs the whole config). This is one
+    rank's shard on this GPU: the same trainer graph as the headline at 32,768
+    12x12 envs, median of 3 windows of 16 steps, and the dominant kernel's
+    roofline (conv_h3f_kernel over 32,768 states, HIP events in the loop)."""
+    import numpy as np
+    from snake_amd import _lib
+    n, bs, C = CONFIGS3_ENVS_PER_GPU, args.board_size, args.n_frames
+    tr = snk.Trainer(n_envs=n, board_size=bs, n_frames=C, capacity=args.capacity, batch_size=64,
+                     epsilon=args.epsilon, epsilon_end=args.epsilon, decay=0.0, updates_per_iter=1, seed=3333)
+    snk.fill_buffer_(tr, graph=graph)
+    tr.run(16, learn=True, graph=graph)
+    steps, windows = 16, []
+    for _ in range(3):
+        _lib.call("snk_synchronize")
+        t0 = time.perf_counter()
+        tr.run(steps, learn=True, graph=graph)
+        _lib.call("snk_synchronize")
+        windows.append(time.perf_counter() - t0)
+    el = float(np.median(windows))
+    loop_ms = _lib.f64(0)
+    _lib.call("snk_trainer_time_act_kernel", tr.handle, 10, ctypes.byref(loop_ms))
+    fl = act_forward_flop(n, bs, C)
+    peak = PEAK_BF16_TFLOPS / H3_PRODUCTS
+    tf = fl / (loop_ms.value * 1e-3) / 1e12 if loop_ms.value > 0 else 0.0
+    st = tr.stats()
+    return {"workload": f"configs[3] per-rank shard: {n} lockstep {bs}x{bs} envs on this GPU ({C} frames, replay "
+                        f"{args.capacity}, 1 B=64 update per step) = 262,144 / 8 ranks",
+            "value": n * steps / el, "unit": "env-steps/s", "ms_per_step": 1000.0 * el / steps,
+            "windows_ms": [1000.0 * w for w in windows], "steps": steps,
+            "effective_global_batch_at_8": 8 * 64,
+            "roofline": {"bound": "mfma", "kernel": "conv_h3f_kernel (conv1 + conv2 + conv3 of the act forward)",
+                         "achieved": tf, "peak": peak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / peak,
+                         "avg_launch_ms": loop_ms.value, "flop_per_launch": fl,
+                         "avg_launch_ms_how": "HIP events around the launch in 10 eager training iterations"},
+            "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
+                            "food_faults": tr.game.check_faults()}}
 
 
 def step_kernel_point(snk, n, bs, C, store):
@@ -509,9 +568,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (real Snake dynamics from SnakeGame(); glorot-initialised Q-net)",
-        "config": {"workload": f"{n} lockstep {bs}x{bs} envs/GPU, {C}-frame 3-action DQN: "
+        "config": {"workload": (f"configs[3]: {world * n} envs over {world} GPU(s), " if args.workload == "configs3"
+                                else "configs[1]: ") +
+                               f"{n} lockstep {bs}x{bs} envs/GPU, {C}-frame 3-action DQN: "
                                f"eps-greedy Q forward + step!/virtual_step + store! + "
                                f"{args.updates_per_iter} B=64 update(s) per step",
+                   "effective_global_batch": 64 * world,
+                   "batch_semantics": "B = 64 per rank per update, gradients mean-all-reduced over the ranks "
+                                      "(RCCL): an effective batch of 64 x n_gpus per update"
+                                      if world > 1 else "B = 64 per update",
                    "n_envs_per_gpu": n, "board_size": bs, "n_frames": C, "replay_capacity": args.capacity,
                    "batch_size": 64, "epsilon": args.epsilon, "parallelism": f"dp{world}" if world > 1 else "none",
                    "hipgraph": graph,
@@ -533,7 +598,7 @@ def main():
         flop_conv1 = 2.0 * n * bs * bs * 16 * 9 * C
         flop_conv3 = 2.0 * n * wo * wo * (36 * 32) * 64
         flop_conv2 = 2.0 * n * bs * bs * 144 * 32
-        flop_total = 2.0 * n * (bs * bs * 16 * 9 * C + bs * bs * 32 * 144 + wo * wo * 64 * 1152 + wo * wo * 64 * 64 + 64 * 3)
+        flop_total = act_forward_flop(n, bs, C) + 2.0 * n * (wo * wo * 64 * 64 + 64 * 3)
         # ms[1] == 0: conv1 + conv2 run inside conv3's kernel (conv_h3f_kernel), ms[2] times all
         # three; ms[0] is then the conv3 weight-max scan (the h3 weight scale)
         fused = ms[1] == 0.0
@@ -605,6 +670,11 @@ def main():
         except Exception as e:   # report, do not fail the headline line
             out["reference_ratio"] = {"error": str(e)}
         out["updates_per_s"] = args.updates_per_iter * args.steps / elapsed
+    if rank == 0 and world == 1 and not args.no_configs3 and args.workload == "configs1":
+        try:
+            out["configs3_per_rank"] = configs3_per_rank(args, snk, graph)
+        except Exception as e:
+            out["configs3_per_rank"] = {"error": str(e)}
     if rank == 0 and world == 1 and not args.no_configs2:
         try:
             out["configs2"] = configs2(args, snk, graph)

@@ -150,9 +150,10 @@ int snk_dqn_create(snk_dqn *out, int32_t board_size, int32_t n_frames, float lr,
  * snk_dqn_last_q refuse it (SNK_ERR_INVALID). */
 int snk_dqn_create_deep(snk_dqn *out, int32_t board_size, int32_t n_frames, float lr, float rho, float eps,
                         uint64_t init_seed);
-/* measurement: average ms per launch of each layer of the deep net's
- * epsilon_greedy forward over env's batch, ms_out[6] = L0 (VALU conv), L1, L2,
- * L3 (bf16 MFMA convs), Dense1, head (HIP events on the library stream) */
+/* measurement: average ms per launch of each stage of the deep net's
+ * epsilon_greedy forward over env's batch (HIP events on the library stream),
+ * ms_out[6]: [0] L0 + L1 + L2 (one fused bf16 MFMA launch, deep_front_kernel),
+ * [1] = [2] = 0 (inside [0]), [3] L3 (deep_conv3_kernel), [4] Dense1, [5] head */
 int snk_dqn_time_deep_layers(snk_dqn m, snk_env env, int32_t reps, double *ms_out);
 int snk_dqn_destroy(snk_dqn m);
 int snk_dqn_nparams(snk_dqn m, int64_t *P_out);
@@ -244,11 +245,21 @@ int snk_trainer_run_partial(snk_trainer t, int32_t n_updates);
  * (utils.jl:431,469), compute_D at 1 (compute_D.jl:56,134). Default 0. */
 int snk_trainer_set_nb(snk_trainer t, int64_t nb);
 /* test/trace hook: after every update the finished gradient (P floats, packed layout
- * of snk_dqn_buffer_ptr) is also copied to grad_ring_dev + slot * P, where slot =
- * (index of the update within the call's launch sequence: iteration in the captured
- * graph x updates_per_iter + update) % slots. One device-to-device copy per update,
- * appended to the same graphs (which are re-captured). NULL turns it off. */
+ * of snk_dqn_buffer_ptr) is also copied to grad_ring_dev + slot * P, where
+ * slot = (i x updates_per_iter + u) % slots for update u of iteration i, and i counts
+ * the iterations of ONE launch sequence: within a captured graph (a graph replay
+ * restarts at i = 0: graphs of graph_unroll iterations, then single-iteration graphs
+ * for the remainder) or within an eager snk_trainer_run call (i = 0, 1, ... mod 2^20).
+ * A ring of graph_unroll x updates_per_iter slots therefore maps one graph replay
+ * slot for slot. One device-to-device copy per update, appended to the same graphs
+ * (which are re-captured). NULL turns it off. */
 int snk_trainer_set_trace(snk_trainer t, float *grad_ring_dev, int64_t slots);
+/* test/trace hook: after every iteration's act forward its actions (n_envs bytes,
+ * action indices) are copied to act_ring_dev + slot * n_envs and, if q_ring_dev is
+ * not NULL, its Q values (n_envs x 3 floats, [env][action]) to q_ring_dev +
+ * slot * 3 n_envs, slot = i % slots with i as in snk_trainer_set_trace. NULL turns
+ * it off. */
+int snk_trainer_set_act_trace(snk_trainer t, uint8_t *act_ring_dev, float *q_ring_dev, int64_t slots);
 int snk_trainer_stats(snk_trainer t, snk_trainer_stats_t *out);
 /* tr.losses: loss of update u at host[u % loss_log_capacity] */
 int snk_trainer_losses(snk_trainer t, double *host, int64_t n);

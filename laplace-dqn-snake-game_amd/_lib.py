@@ -112,6 +112,7 @@ _PROTOS = {
     "snk_trainer_run_partial": [vp, i32],
     "snk_trainer_set_nb": [vp, i64],
     "snk_trainer_set_trace": [vp, vp, i64],
+    "snk_trainer_set_act_trace": [vp, vp, vp, i64],
     "snk_trainer_stats": [vp, vp],
     "snk_trainer_time_act_kernel": [vp, i32, vp],
     "snk_trainer_losses": [vp, vp, i64],

@@ -371,6 +371,9 @@ static void deep_backward_bs(DeepNet &Nn, const float *th, const uint16_t *wimg,
              D.off_w[0], s);
 }
 
+// largest training batch of the deep backward (chunk slabs: 2.4 GB at L3)
+constexpr int DEEP_BWD_MAX_B = 8192;
+
 static int64_t backward_slab_floats(const DeepLayout &D, int64_t B) {
     const int64_t nc = (int64_t)D.bs * D.bs;
     int64_t need = 0;
@@ -473,6 +476,12 @@ void deep_prepare(snk_dqn_s *h, int64_t S_act, int64_t B) {
     DeepNet &N = *h->deep;
     if (S_act > 0) work_ensure(N, N.act, S_act, false);
     if (B > 0) {
+        // the backward kernels are sized for the reference's B = 64: their chunk slabs grow
+        // linearly with B ((B+1)/2 x 147,520 floats at L3) and conv_dx puts B on grid.y, so
+        // a batch past this bound is refused here instead of over-allocating or failing a launch
+        SNK_CHECK(B <= DEEP_BWD_MAX_B, SNK_ERR_INVALID,
+                  "deep net: training batch %lld > %d (the bf16 backward is built for B = 64 batches)",
+                  (long long)B, DEEP_BWD_MAX_B);
         work_ensure(N, N.tgt, B, false);
         work_ensure(N, N.trn, B, true);
         const int64_t need = backward_slab_floats(N.D, B);

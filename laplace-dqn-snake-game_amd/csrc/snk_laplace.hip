@@ -231,20 +231,33 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s, int r
     dim3 grid((unsigned)a.ntiles, (unsigned)z);
     if (a.xh) {   // pre-split rows (h3): fp16 parts, 3 products per fp32 product
         SNK_CHECK(out == SYRK_F32 && z == 1 && a.ldh % SY_KS == 0 && a.xe, SNK_ERR_INTERNAL, "syrk h3 arguments");
-        // production: syrk_h3q_kernel (v_mfma_f32_16x16x32_f16). Measurement builds:
-        // SNK_SYRK=h3 the round-2 32x32x16 kernel; SNK_SYRK_VAR = 1 / 2 without MFMAs /
-        // without stage DMAs (snk_syrk.hpp)
+        // production: syrk_h3q_kernel (v_mfma_f32_16x16x32_f16); SNK_SYRK=h3 selects the
+        // round-2 32x32x16 kernel (same results class, parity-tested)
         static const char *kind = getenv("SNK_SYRK");
+#ifdef SNK_SYRK_MEASURE
+        // measurement build only (make measure: libsnakehip_measure.so, never shipped):
+        // SNK_SYRK_VAR = 1 / 2 run the kernel without MFMAs / without stage DMAs, i.e.
+        // WRONG results by design (snk_syrk.hpp)
         static const int var = getenv("SNK_SYRK_VAR") ? atoi(getenv("SNK_SYRK_VAR")) : 0;
+#else
+        constexpr int var = 0;
+#endif
         if (!(kind && !strcmp(kind, "h3"))) {
+#ifdef SNK_SYRK_MEASURE
             if (var == 1) syrk_h3q_kernel<1><<<grid, 512, 0, s>>>(a);
             else if (var == 2) syrk_h3q_kernel<2><<<grid, 512, 0, s>>>(a);
-            else syrk_h3q_kernel<0><<<grid, 512, 0, s>>>(a);
+            else
+#endif
+                syrk_h3q_kernel<0><<<grid, 512, 0, s>>>(a);
         } else {
+#ifdef SNK_SYRK_MEASURE
             if (var == 1) syrk_h3_kernel<8, 1><<<grid, 512, 0, s>>>(a);
             else if (var == 2) syrk_h3_kernel<8, 2><<<grid, 512, 0, s>>>(a);
-            else syrk_h3_kernel<8><<<grid, 512, 0, s>>>(a);
+            else
+#endif
+                syrk_h3_kernel<8><<<grid, 512, 0, s>>>(a);
         }
+        (void)var;
     } else {      // D'D: fp32 rows, bf16 x6 split in the kernel, one fp64 slab per z
         SNK_CHECK(out == SYRK_SLAB64 && a.g64, SNK_ERR_INTERNAL, "syrk: fp32 rows only for the slab Gram");
         syrk_slab_kernel<<<grid, 256, 0, s>>>(a);

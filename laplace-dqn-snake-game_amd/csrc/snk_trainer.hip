@@ -67,6 +67,12 @@ struct snk_trainer_s {
     // trace + slot * P, slot = (position of the update in the launch sequence) % trace_slots
     float *trace = nullptr;
     int64_t trace_slots = 0;
+    // snk_trainer_set_act_trace: every iteration's actions (n bytes) and act-forward
+    // Q values (n x 3 floats, optional) are copied to act_trace / q_trace + slot * n (x 3),
+    // slot = (iteration within the launch sequence) % act_trace_slots
+    uint8_t *act_trace = nullptr;
+    float *q_trace = nullptr;
+    int64_t act_trace_slots = 0;
     void drop_graphs() {
         for (int i = 0; i < 4; ++i) {
             if (exec[i]) (void)hipGraphExecDestroy(exec[i]);
@@ -110,14 +116,22 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     ha.seed = h->cfg.seed;
     ha.tptr = &E.ctl->t;
     ha.eps_dev = &h->stats->epsilon;
+    const float *qact = q->act.q;
     if (q->deep)
-        deep_forward(q, SNK_NET_Q, src_env(E), E.n, HEAD_ACT, ha, s);
+        qact = deep_forward(q, SNK_NET_Q, src_env(E), E.n, HEAD_ACT, ha, s);
     else
         qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q,
                      ride ? &rider : nullptr);
     // step! + virtual_step + store! + the episode statistics, one launch
     const EpisodeAcc acc{&h->stats->episodes, &h->stats->score_sum, &h->stats->env_steps, &h->stats->reward_sum,
                          &h->stats->reward_max, &h->stats->score_max};
+    if (h->act_trace) {
+        const int64_t slot = (int64_t)it % h->act_trace_slots;
+        SNK_HIP(hipMemcpyAsync(h->act_trace + slot * E.n, h->act, (size_t)E.n, hipMemcpyDeviceToDevice, s));
+        if (h->q_trace)
+            SNK_HIP(hipMemcpyAsync(h->q_trace + slot * E.n * 3, qact, (size_t)E.n * 3 * sizeof(float),
+                                   hipMemcpyDeviceToDevice, s));
+    }
     env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s, &acc);
     if (!upd) return;
     for (int u = 0; u < n_upd; ++u) {
@@ -333,6 +347,18 @@ extern "C" int snk_trainer_set_trace(snk_trainer h, float *grad_ring_dev, int64_
         SNK_HIP(hipStreamSynchronize(stream()));
         h->trace = grad_ring_dev;
         h->trace_slots = grad_ring_dev ? slots : 0;
+        h->drop_graphs();   // re-captured with (or without) the copies
+    });
+}
+
+extern "C" int snk_trainer_set_act_trace(snk_trainer h, uint8_t *act_ring_dev, float *q_ring_dev, int64_t slots) {
+    return guard([&] {
+        SNK_CHECK(h && (act_ring_dev == nullptr || slots > 0) && (q_ring_dev == nullptr || act_ring_dev),
+                  SNK_ERR_INVALID, "bad set_act_trace arguments");
+        SNK_HIP(hipStreamSynchronize(stream()));
+        h->act_trace = act_ring_dev;
+        h->q_trace = act_ring_dev ? q_ring_dev : nullptr;
+        h->act_trace_slots = act_ring_dev ? slots : 0;
         h->drop_graphs();   // re-captured with (or without) the copies
     });
 }

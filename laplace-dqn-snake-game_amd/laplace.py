@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import warnings
 
 import numpy as np
 
@@ -125,7 +126,7 @@ class LaplaceD:
 
 def compute_D(tr, K: int = 1000, thin: int = 10, burn_in: int = 50_000, graph: bool = True,
               reset_optimizer: bool = True, schedule: str = "episode", n_batches: int | None = None,
-              on_update=None) -> LaplaceD | None:
+              on_update=None, strict: bool = False) -> LaplaceD | None:
     """compute_D.jl:33-86 on a Trainer: fill_buffer!, a fresh RMSProp state
     (`Flux.setup`, :47), then the training loop `while nb <= n_batches`
     (:56-58, nb from 1, n_batches = tr.n_batches unless given): from
@@ -137,7 +138,8 @@ def compute_D(tr, K: int = 1000, thin: int = 10, burn_in: int = 50_000, graph: b
 
     If the loop ends (nb > n_batches) before the K-th column, the reference
     returns `nothing` without building D; so does this: the updates still run,
-    and None is returned.
+    a RuntimeWarning names the nb the K-th column needs, and None is returned
+    (strict=True raises ValueError instead).
 
     schedule="episode": the reference's loop body, one full epsilon-greedy
     episode stored and one B-sample update per nb (:89-138, EpisodeLoop).
@@ -185,6 +187,12 @@ def compute_D(tr, K: int = 1000, thin: int = 10, burn_in: int = 50_000, graph: b
     for pos, at in enumerate(snaps):
         if at > n_batches:                                  # `while nb <= n_batches` ends first
             updates(nb, n_batches)
+            msg = (f"compute_D: the loop ended at nb = {n_batches} (n_batches) before the K-th snapshot "
+                   f"(column {pos + 1} of {K} falls at nb = {at}); returning None as compute_D.jl:58 "
+                   f"returns nothing. Raise n_batches to >= {snaps[-1]} to build D.")
+            if strict:
+                raise ValueError(msg)
+            warnings.warn(msg, RuntimeWarning, stacklevel=2)
             return None
         updates(nb, at - 1)
         nb = at

@@ -96,6 +96,20 @@ class Trainer:
             call("snk_trainer_set_trace", self._h, ring.ptr, int(ring.shape[0]))
         self._trace = ring
 
+    def set_act_trace(self, acts: DeviceArray | None, q: DeviceArray | None = None) -> None:
+        """Copy every iteration's actions into acts[slot] (device [slots, n_envs]
+        uint8) and, if given, its act-forward Q values into q[slot] (device
+        [slots, n_envs, 3] float32); slot = iteration within the run's launch
+        sequence % slots. Test infrastructure, as set_trace."""
+        if acts is None:
+            call("snk_trainer_set_act_trace", self._h, None, None, 0)
+        else:
+            if q is not None and q.shape[0] != acts.shape[0]:
+                raise ValueError("act and Q trace rings need the same slot count")
+            call("snk_trainer_set_act_trace", self._h, acts.ptr, q.ptr if q is not None else None,
+                 int(acts.shape[0]))
+        self._act_trace = (acts, q)
+
     def stats(self) -> dict:
         st = _lib.TrainerStats()
         call("snk_trainer_stats", self._h, C.byref(st))

@@ -58,3 +58,34 @@ def floyd(seed: int, draw: int, n_len: int, batch: int) -> list[int]:
 
 
 TRAINER_SAMPLE_SALT = 0x5A4D504C45   # snk_trainer.hip: replay draws use cfg.seed ^ this
+
+
+def _splitmix64_np(x):
+    z = x + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def rng_hash_np(seed: int, a: np.ndarray, b: int) -> np.ndarray:
+    """rng_hash over an array of first counters (uint64 wrap-around arithmetic)."""
+    with np.errstate(over="ignore"):
+        a = np.asarray(a, np.uint64)
+        return _splitmix64_np(_splitmix64_np(np.uint64(seed) ^ (a * np.uint64(0xD1B54A32D192ED03))) ^ np.uint64(b))
+
+
+def explore_np(seed: int, n_envs: int, t: int, epsilon) -> np.ndarray:
+    """explore() for envs 0..n_envs-1 at step t: the random action index, or -1
+    where epsilon_greedy takes the greedy action."""
+    e = np.arange(n_envs, dtype=np.uint64)
+    u = (rng_hash_np(seed, e, t) >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    r = ((rng_hash_np(seed ^ 0xA5A5A5A5A5A5A5A5, e, t) >> np.uint64(32)) % np.uint64(3)).astype(np.int64)
+    return np.where(u < np.float32(epsilon), r, -1)
+
+
+def first_argmax_np(q: np.ndarray) -> np.ndarray:
+    """first_argmax over rows of q [n, 3]."""
+    a = np.zeros(len(q), np.int64)
+    a = np.where(q[:, 1] > q[np.arange(len(q)), a], 1, a)
+    a = np.where(q[:, 2] > q[np.arange(len(q)), a], 2, a)
+    return a

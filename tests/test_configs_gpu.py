@@ -291,5 +291,9 @@ def test_compute_D_stops_at_n_batches(snk):
     after n_batches, the loop runs updates 1..n_batches and returns nothing."""
     tr = snk.Trainer(n_envs=1, board_size=10, n_frames=2, capacity=200, seed=3, n_batches=9)
     losses = []
-    out = snk.compute_D(tr, K=3, thin=2, burn_in=6, on_update=lambda nb, loss: losses.append(nb))
+    with pytest.warns(RuntimeWarning, match="before the K-th snapshot"):
+        out = snk.compute_D(tr, K=3, thin=2, burn_in=6, on_update=lambda nb, loss: losses.append(nb))
     assert out is None and losses == list(range(1, 10))
+    tr = snk.Trainer(n_envs=1, board_size=10, n_frames=2, capacity=200, seed=3, n_batches=9)
+    with pytest.raises(ValueError, match="n_batches to >= 10"):
+        snk.compute_D(tr, K=3, thin=2, burn_in=6, strict=True)

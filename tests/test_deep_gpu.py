@@ -79,7 +79,7 @@ def _replay(snk, bs, C, n=64, T=10, seed=3):
     return rb
 
 
-@pytest.mark.parametrize("bs,C", [(10, 2), (20, 2)])
+@pytest.mark.parametrize("bs,C", [(10, 2), (12, 2), (20, 2)])
 def test_deep_loss_grad_and_update_vs_oracle(snk, bs, C):
     """One DQN update of the deep net on a replay batch: Huber loss and the
     bf16-MFMA gradient vs the oracle (same rounding points), RMSProp on the
@@ -128,6 +128,18 @@ def test_deep_loss_grad_and_update_vs_oracle(snk, bs, C):
     snk.update_target_net_(m)
     assert np.array_equal(m.get_params(snk.SNK_NET_TARGET), th1)
     assert np.array_equal(m.forward(x, snk.SNK_NET_TARGET), m.forward(x))
+
+
+def test_deep_training_batch_bound(snk):
+    """The bf16 backward is built for B = 64 batches (its chunk slabs grow with B,
+    conv_dx puts B on grid.y): a training batch past the library's bound fails
+    cleanly with SNK_ERR_INVALID before any allocation or launch."""
+    rb = _replay(snk, 10, 2, n=64, T=130)
+    m = snk.DQNModel(10, 3, n_frames=2, seed=2, deep=True)
+    ids = snk.DeviceArray(8193, np.int64)
+    ids.upload(np.arange(8193, dtype=np.int64))
+    with pytest.raises(snk.SnakeHipError, match="training batch"):
+        m.loss_grad(rb, ids, 8193)
 
 
 def test_deep_trainer_graph_vs_eager_and_counts(snk):

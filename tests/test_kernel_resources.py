@@ -113,3 +113,13 @@ def test_syrk_h3q_register_budget(meta):
     for n in k:
         f = meta[n]
         assert f["vgpr_count"] + f.get("agpr_count", 0) <= 256, (n, f)
+
+
+def test_no_wrong_result_measurement_variants(meta):
+    """The Gram kernel's measurement variants (VAR 1: no MFMA, VAR 2: no stage
+    DMAs; wrong results by design) exist only in the measurement build
+    (make measure, -DSNK_SYRK_MEASURE): the shipping library holds VAR 0 only,
+    so no environment variable can select them."""
+    bad = [n for n in meta if re.search(r"syrk_h3q_kernelILi[1-9]E|syrk_h3_kernelILi\d+ELi[1-9]E", n)]
+    assert not bad, bad
+    assert any(re.search(r"syrk_h3q_kernelILi0E", n) for n in meta)
