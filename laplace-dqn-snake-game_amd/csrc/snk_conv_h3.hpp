@@ -43,6 +43,10 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ f16x8 as_h(const u32x4 &v) { return __builtin_bit_cast(f16x8, v); }
 
+// s_waitcnt immediate: vmcnt(n) (LDS-DMA, loads and stores count together, in issue order),
+// lgkmcnt and expcnt left at their maxima
+__device__ __forceinline__ constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+
 // e such that max * 2^e < 2^15 (>= 2^14 for a normal max); 0 for a zero or non-finite max
 __device__ __forceinline__ int h3_exp(float m) {
     const uint32_t b = __float_as_uint(m) & 0x7fffffffu;

@@ -38,7 +38,36 @@ struct H3FArgs {
     const float *b3;     // conv3 bias [64]
     float *out;          // a3 [S][ho^2][64]
     SampleRider rider;   // rider.out: one extra workgroup runs this replay draw (the trainer's update sample)
+    // NBUF = 8: w3 pre-split (w3_split_kernel) into the B buffers' byte order, copied by LDS-DMA
+    const uint16_t *w3h;
+    const int *w3e;      // its exponent (ew)
 };
+
+// conv3's weight image [36 kk][64 co][32 ci] (fp32) -> fp16 h / l parts of w * 2^ew, ew from the
+// partial maxima, laid out exactly as conv_h3f_kernel's register path stores one offset into a B
+// buffer (512 16-byte chunks per offset: h chunk x6s_bswz(c), l chunk x6s_bswz(256 + c) for the
+// chunk c = (co, ci / 8); each of its two 8-byte halves one float4 of the image): a lane-linear
+// copy of an offset's 8 KB is then a B buffer. One thread per float4 of the image.
+static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__restrict__ img, const float *__restrict__ wmax,
+                                                       int nwmax, uint16_t *__restrict__ out, int *__restrict__ eout) {
+    __shared__ float red4[4];
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < nwmax; i += 256) m = fmaxf(m, wmax[i]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+    __syncthreads();
+    const int ew = h3_exp(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
+    if (blockIdx.x == 0 && threadIdx.x == 0) *eout = ew;
+    const int t = blockIdx.x * 256 + threadIdx.x;   // < 36 * 512
+    const int kk = t >> 9, tt = t & 511;
+    const f32x4 v = reinterpret_cast<const f32x4 *>(img)[t];
+    const int bch = (tt >> 3) * 4 + ((tt & 7) >> 1), bhalf = tt & 1;
+    u32x2 h, l;
+    h3_split4(v, ew, h, l);
+    u32x2 *o = reinterpret_cast<u32x2 *>(out) + (int64_t)kk * 512 * 2;
+    o[x6s_bswz(bch) * 2 + bhalf] = h;
+    o[x6s_bswz(256 + bch) * 2 + bhalf] = l;
+}
 
 // Profiling builds only (make clocks): per-workgroup phase timestamps, read back by
 // snk_h3f_debug_clocks (slots: start, conv1, scales + splits, conv2, conv3 image + B
@@ -68,7 +97,10 @@ constexpr int h3f_lds_bytes() {
 // runs); 4 = one barrier per offset PAIR (B(kk+3) staged, read two offsets later)
 template <int HIN, int NBUF = 4, int CF = 2>
 __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
-    static_assert(NBUF == 2 || NBUF == 4, "B buffers");
+    static_assert(NBUF == 2 || NBUF == 4 || NBUF == 8, "B buffers");
+    // NBUF 8: the B buffers are filled by LDS-DMA from the pre-split image a.w3h (no
+    // register staging, no split): offset kk + 4 is issued while kk runs
+    constexpr bool DMA = NBUF == 8;
     constexpr int KS = 6, CN = 64, CK = 32, NSG = 4, NB = 2 * CN * CK / 8;
     constexpr int NKK = KS * KS;
     constexpr int hin = HIN, ho = HIN - KS + 1, ho2 = ho * ho, hin2 = hin * hin;
@@ -103,21 +135,43 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     // conv3 B register sets (as conv_h3s_kernel)
     const f32x4 *__restrict__ wsrc = reinterpret_cast<const f32x4 *>(a.w3);
     f32x4 bst[2];
-    auto b_load = [&](int kk, int set) { bst[set] = wsrc[(int64_t)min(kk, NKK - 1) * NB + tid]; };
+    auto b_load = [&](int kk, int set) {
+        if constexpr (!DMA) bst[set] = wsrc[(int64_t)min(kk, NKK - 1) * NB + tid];
+    };
     const int bch = (tid >> 3) * 4 + ((tid & 7) >> 1);
     const int bhalf = tid & 1;
     int ew = 0;
     auto b_store = [&](int buf, int set) {
-        u32x2 h, l;
-        h3_split4(bst[set], ew, h, l);
-        Bs2[(buf * NB + x6s_bswz(bch)) * 2 + bhalf] = h;
-        Bs2[(buf * NB + x6s_bswz(256 + bch)) * 2 + bhalf] = l;
+        if constexpr (!DMA) {
+            u32x2 h, l;
+            h3_split4(bst[set], ew, h, l);
+            Bs2[(buf * NB + x6s_bswz(bch)) * 2 + bhalf] = h;
+            Bs2[(buf * NB + x6s_bswz(256 + bch)) * 2 + bhalf] = l;
+        }
     };
-    b_load(0, 0);
-    b_load(1, 1);
+    // DMA: offset kk's pre-split 8 KB into buffer kk & 7, chunk tid by lane tid (past the
+    // last offset: harmless reloads of it)
+    auto dma = [&](int kk) __attribute__((always_inline)) {
+        if constexpr (DMA) {
+            const int k = min(kk, NKK - 1);
+            __builtin_amdgcn_global_load_lds((const void *)(a.w3h + ((int64_t)k * NB + tid) * 8),
+                                             (__attribute__((address_space(3))) void *)(Bs + (kk & (NBUF - 1)) * NB + wave * 64),
+                                             16, 0, 0);
+        }
+    };
+    if constexpr (DMA) {   // offsets 0..3 now (conv1 stages its boards in buffer 7)
+        dma(0);
+        dma(1);
+        dma(2);
+        dma(3);
+    } else {
+        b_load(0, 0);
+        b_load(1, 1);
+    }
     // conv3 weight-max partials: loaded here, reduced after conv1 (their latency hides
     // behind the board loads instead of following conv1)
-    const float wmx = tid < a.nwmax ? a.wmax[tid] : 0.0f;
+    const float wmx = !DMA && tid < a.nwmax ? a.wmax[tid] : 0.0f;
+    const int ew_dma = DMA ? *a.w3e : 0;
 
     // conv2 bias of this lane's output channels (16 ct + 4 g + e), early
     float b2v[2][4];
@@ -152,8 +206,9 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         // computes the same four output channels (4 (tid & 3) .. +3), so its 9 CF weight
         // quads live in registers and a tap costs one LDS float
         constexpr int C = CF;
-        float *xin = reinterpret_cast<float *>(Bs);    // [NSG][C][NPB]
-        static_assert(NSG * C * NPB <= NBUF * NB * 4, "conv1 staging fits the B buffers");
+        // [NSG][C][NPB]; DMA: in buffer 7 (buffers 0..3 are filling already)
+        float *xin = reinterpret_cast<float *>(Bs + (DMA ? 7 * NB : 0));
+        static_assert(NSG * C * NPB <= (DMA ? NB : NBUF * NB) * 4, "conv1 staging fits the B buffers");
         __shared__ const int8_t *pbase[NSG * C];
         if (tid < NSG * C) pbase[tid] = tid / C < ns ? a.src.plane(s0 + tid / C, tid % C) : nullptr;
         const int cq = tid & 3;
@@ -221,7 +276,8 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     }
     H3F_CLK(1);
     float wm3 = wmx;
-    for (int i = tid + 512; i < a.nwmax; i += 512) wm3 = fmaxf(wm3, a.wmax[i]);
+    if (!DMA)
+        for (int i = tid + 512; i < a.nwmax; i += 512) wm3 = fmaxf(wm3, a.wmax[i]);
     float mw2 = 0.0f, ms[NSG] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int u = 0; u < LW; ++u) {
@@ -261,7 +317,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
 #pragma unroll
         for (int q = 0; q < NSG; ++q) ea1[q] = h3_exp(m[q]);
         ew2 = h3_exp(m[4]);
-        ew = h3_exp(m[5]);
+        ew = DMA ? ew_dma : h3_exp(m[5]);
     }
 #pragma unroll
     for (int u = 0; u < LW; ++u) {   // image [kk][co][ci]: k = 16 * (kk - 2p) + ci in offset pair p
@@ -411,6 +467,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     }
     b_store(0, 0);
     b_store(1, 1);
+    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // offsets 0..3 landed (published below)
 
     constexpr int T = (NSG * ho2 + 15) / 16;
     const int rg = wave >> 1, cg = wave & 1;
@@ -473,7 +530,19 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         // buffer (kk+3) & 3, barrier after odd offsets: a buffer written at offset kk is
         // read at kk+2 and last read at kk-2, so a barrier always separates the two
         auto step = [&](int kk, const Frag &cur, Frag &nxt, int set) {
-            if (NBUF == 2) {
+            if constexpr (DMA) {
+                // offset kk + 4 into buffer (kk + 4) & 7, last read at step kk - 5 (a barrier
+                // since); after odd offsets: everything but the newest DMA landed (offsets
+                // <= kk + 3, read at steps <= kk + 2), the barrier publishes it
+                dma(kk + 4);
+                frag_read(kk + 1, nxt);
+                mfma_block(cur);
+                if (kk & 1) {
+                    __builtin_amdgcn_s_waitcnt(waitcnt_vm(1));
+                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                    __builtin_amdgcn_s_barrier();
+                }
+            } else if (NBUF == 2) {
                 b_load(kk + 3, set ^ 1);
                 frag_read(kk + 1, nxt);
                 mfma_block(cur);
@@ -502,6 +571,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             step(kk + 1, f1, f0, 1);
         }
         H3F_CLK(5);
+        if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // the tail reloads landed
         // output through LDS as conv_h3s_kernel
         constexpr int CS = 80;
         static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN, NBUF>() - NBUF * NB * 16, "output staging fits");

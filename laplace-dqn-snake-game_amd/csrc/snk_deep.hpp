@@ -347,6 +347,19 @@ struct DeepFrontShape {
 };
 // 16-byte chunk c of a 64-byte weight row
 __device__ __forceinline__ int dfr_slot(int row, int c) { return row * 32 + 8 * (c ^ ((row >> 1) & 3)); }
+// The L0 / L1 epilogue stores into X: an MFMA accumulator lane (r, g) holds channel quad g of
+// tile position (r & 3, r >> 2), so a 16-lane store group (one g) would write four tile rows
+// whose X addresses differ by multiples of 128 bytes: 4-way bank conflicts on ds_write_b64
+// (bank = dword mod 32; 25 % of the kernel's LDS cycles in profiles/r03_pmc_deep_fwd.json).
+// The fragment READS (9x as many) are conflict-free on this layout and no X layout or chunk
+// swizzle serves both (tools/), so the store transposes instead: lane
+// 16a + 4b + c takes lane 16b + 4a + c's data (ds_bpermute), i.e. channel quad r >> 2 of
+// position (r & 3, row g): one tile row per group, 16 distinct bank pairs.
+__device__ __forceinline__ u32x2 dfr_tr44(const u32x2 &v, int lane) {
+    const int src = (((lane >> 2) & 3) * 16 + ((lane >> 4) & 3) * 4 + (lane & 3)) * 4;
+    return u32x2{(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v[0]),
+                 (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v[1])};
+}
 
 template <int C, int H, bool KEEP>
 __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const float *__restrict__ img0,
@@ -444,11 +457,13 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                 }
                 const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, as_bf(u32x4{w[0], w[1], w[2], w[3]}),
                                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                if (i < H && j < H) {
-                    const u32x2 o = relu_bf16x4(acc, b0);
-                    *reinterpret_cast<u32x2 *>(X + ((i + 1) + (j + 1) * PJ) * XST + half * 16 + 4 * g) = o;
-                    if (KEEP) *reinterpret_cast<u32x2 *>(a0 + (s * M + i + j * H) * 32 + half * 16 + 4 * g) = o;
-                }
+                const u32x2 o = relu_bf16x4(acc, b0);
+                if (KEEP && i < H && j < H)
+                    *reinterpret_cast<u32x2 *>(a0 + (s * M + i + j * H) * 32 + half * 16 + 4 * g) = o;
+                const u32x2 ot = dfr_tr44(o, lane);   // quad r >> 2 of position (r & 3, row g)
+                const int ti = 4 * (t % NB) + (r & 3), tj = 4 * (t / NB) + g;
+                if (ti < H && tj < H)
+                    *reinterpret_cast<u32x2 *>(X + ((ti + 1) + (tj + 1) * PJ) * XST + half * 16 + 4 * (r >> 2)) = ot;
             }
         }
         __syncthreads();
@@ -482,12 +497,15 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                 if (i2 >= TPS || (i2 == TPS - 1 && !last_ok)) continue;
                 int i, j;
                 tpos(t, i, j);
-                if (i >= H || j >= H) continue;
+                const int ti = 4 * (t % NB) + (r & 3), tj = 4 * (t / NB) + g;   // the transposed store's position
 #pragma unroll
                 for (int c2 = 0; c2 < 2; ++c2) {
                     const u32x2 o = relu_bf16x4(acc[ii][c2], b1[c2]);
-                    *reinterpret_cast<u32x2 *>(X + ((i + 1) + (j + 1) * PJ) * XST + c2 * 16 + 4 * g) = o;
-                    if (KEEP) *reinterpret_cast<u32x2 *>(a1 + (s * M + i + j * H) * 32 + c2 * 16 + 4 * g) = o;
+                    if (KEEP && i < H && j < H)
+                        *reinterpret_cast<u32x2 *>(a1 + (s * M + i + j * H) * 32 + c2 * 16 + 4 * g) = o;
+                    const u32x2 ot = dfr_tr44(o, lane);
+                    if (ti < H && tj < H)
+                        *reinterpret_cast<u32x2 *>(X + ((ti + 1) + (tj + 1) * PJ) * XST + c2 * 16 + 4 * (r >> 2)) = ot;
                 }
             }
         }

@@ -271,7 +271,10 @@ __global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_
             epr_out = epr;
             score_out = score;
             if (fault) atomicAdd(E.fault_count, 1u);
-            if (store) {
+            // store! in env order (utils.jl:267-277): with more envs than capacity, only the
+            // last cap transitions of the step survive it, so only they are written (the
+            // overwritten ones would otherwise race on their slots)
+            if (store && E.n - e <= R.cap) {
                 const int64_t slot = (rc + e) % R.cap;
                 R.reward[slot] = reward;
                 R.act[slot] = (uint8_t)(act_mode == SNK_ACT_INDEX ? a % 3 : avail_index(prev, dir));
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_
                 const uint8_t f = s_flag[el];
                 const i32x4 vc = vcur[k0 + k];
                 const i32x4 vnew = (f & 1) ? patch16(vc, c * 16, s_pc + el * 4) : vc;
-                if (store && (f & 1)) {
+                if (store && (f & 1) && E.n - ge <= R.cap) {
                     const int64_t slot = (rc + ge) % R.cap;
                     int8_t *rf = R.frames + slot * (int64_t)(R.C + 1) * PITCH + c * 16;
                     if (rd_prv) {

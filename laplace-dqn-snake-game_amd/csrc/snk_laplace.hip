@@ -721,18 +721,30 @@ __global__ __launch_bounds__(256) void lap_sample_kernel(const double *__restric
     }
 }
 
-// dynamic LDS floats of lap_act_kernel
-static inline int64_t lap_act_lds_floats(const QLayout &L) {
+// lap_act_kernel's LDS (floats): [xin | a1 | w2s] (overlaid by the conv3 weight ring
+// once conv2 is done) | a2 | a3 | Dense1 partials | h1
+constexpr int LAP_RING = 5;          // conv3 weight chunks (one kernel offset, 32 x 64 floats) in flight
+constexpr int LAP_CH = 32 * 64;
+static inline int64_t lap_act_front_floats(const QLayout &L) {
     const int bp = L.bs + 2, r4 = (L.C * bp * bp + 3) & ~3, a4 = (16 * bp * bp + 3) & ~3;
-    return (int64_t)r4 + a4 + 9 * 16 * 32 + (int64_t)L.ncell * 32 + L.K1 + 16 * 64 + 64 + 8;
+    return std::max<int64_t>((int64_t)r4 + a4 + 9 * 16 * 32, (int64_t)LAP_RING * LAP_CH);
+}
+static inline int64_t lap_act_lds_floats(const QLayout &L) {
+    return lap_act_front_floats(L) + (int64_t)L.ncell * 32 + L.K1 + 16 * 64 + 64 + 8;
 }
 
-// one workgroup (256 threads) per env g: the greedy action of model g on the env's state
+// one workgroup (256 threads) per env g: the greedy action of model g on the env's state.
+// Latency matters as much as bandwidth here (the episode tail runs a few live models per
+// launch): conv3's weights arrive by LDS-DMA through a ring of LAP_RING kernel offsets
+// (each weight fetched once, read from LDS by the 16 position groups that share it), and
+// Dense1's stream into a register ring three k-steps deep. The FMAs run on v_pk_fma_f32
+// (two accumulators per instruction) in the scalar form's per-accumulator order, so every
+// output is bit-identical to an fmaf chain over (kk, ci) / k ascending.
 __global__ __launch_bounds__(256) void lap_act_kernel(QLayout L, const float *__restrict__ W, int64_t ldw, BoardSrc src,
                                                       const uint8_t *__restrict__ fin, uint8_t *__restrict__ act,
-                                                      float *__restrict__ qout) {
+                                                      float *__restrict__ qout, int front) {
     const int64_t g = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (fin && fin[g]) {
         if (tid == 0) act[g] = 0;
         return;
@@ -742,10 +754,11 @@ __global__ __launch_bounds__(256) void lap_act_kernel(QLayout L, const float *__
     float *xin = lsm;                       // [C][bp*bp] bordered input planes
     float *a1 = xin + ((C * bp * bp + 3) & ~3);   // [16][bp*bp] bordered conv1 output (16-B aligned sections)
     float *w2s = a1 + ((16 * bp * bp + 3) & ~3);  // conv2 weights [(kk*16+ci)*32+co]
-    float *a2 = w2s + 9 * 16 * 32;          // [ncell][32]
+    float *ring = lsm;                      // conv3 weight chunks [LAP_RING][32 ci][64 co] (after conv2)
+    float *a2 = lsm + front;                // [ncell][32]
     float *a3 = a2 + nc * 32;               // [Wo*Wo][64]
     float *red = a3 + L.K1;                 // [16][64] Dense1 partial sums
-    float *h1 = red + 4 * 64;               // [64]
+    float *h1 = red + 16 * 64;              // [64]
     const float *th = W + g * ldw;
     for (int q = tid; q < (int)(w2s - xin); q += 256) xin[q] = 0.0f;
     for (int q = tid; q < 9 * 16 * 32; q += 256) w2s[q] = th[L.off_w2 + q];
@@ -773,87 +786,135 @@ __global__ __launch_bounds__(256) void lap_act_kernel(QLayout L, const float *__
         }
     }
     __syncthreads();
-    // conv2 (3x3, 16 -> 32, pad 1): co = tid & 31, positions (tid >> 5) + 8 r
+    // conv2 (3x3, 16 -> 32, pad 1): co = tid & 31, positions p and p + 8 h (h = ceil(rows / 2)
+    // rows of 8 apart) as one packed accumulator pair
     {
-        const int co = tid & 31;
+        const int co = tid & 31, p0 = tid >> 5;
         const float b = th[L.off_b2 + co];
-        for (int p = tid >> 5; p < nc; p += 8) {
-            const int j = p / bs, i = p - j * bs;
-            float acc = b;
+        const int nr = (nc - p0 + 7) / 8, hr = (nr + 1) / 2;   // this thread's positions p0 + 8 r, r < nr
+        for (int r = 0; r < hr; ++r) {
+            const int pa = p0 + 8 * r, rb = r + hr;
+            const int pb = rb < nr ? p0 + 8 * rb : pa;
+            const int ja = pa / bs, ia = pa - ja * bs, jb = pb / bs, ib = pb - jb * bs;
+            f32x2 acc{b, b};
             for (int kk = 0; kk < 9; ++kk) {
                 const int du = kk % 3, dv = kk / 3;
-                const float *ap = a1 + (i + du) + (j + dv) * bp;
+                const float *apa = a1 + (ia + du) + (ja + dv) * bp, *apb = a1 + (ib + du) + (jb + dv) * bp;
 #pragma unroll 4
-                for (int ci = 0; ci < 16; ++ci) acc = __builtin_fmaf(ap[ci * bp * bp], w2s[(kk * 16 + ci) * 32 + co], acc);
+                for (int ci = 0; ci < 16; ++ci) {
+                    const float w = w2s[(kk * 16 + ci) * 32 + co];
+                    acc = __builtin_elementwise_fma(f32x2{apa[ci * bp * bp], apb[ci * bp * bp]}, f32x2{w, w}, acc);
+                }
             }
-            a2[p * 32 + co] = fmaxf(acc, 0.0f);
+            a2[pa * 32 + co] = fmaxf(acc[0], 0.0f);
+            if (rb < nr) a2[pb * 32 + co] = fmaxf(acc[1], 0.0f);
         }
     }
-    __syncthreads();
-    // conv3 (6x6, 32 -> 64, pad 0), weights streamed from HBM: thread -> 4 output
-    // channels 4*(tid & 15) .. +3 at positions (tid >> 4) + 16 r, r < 4 (Wo^2 <= 64);
-    // per 4 input channels: 4 ds_read_b128 of a2, 4 float4 weight loads, 64 FMAs
+    __syncthreads();   // conv1/conv2 staging free: the conv3 weight ring overlays it
+    // conv3 (6x6, 32 -> 64, pad 0): thread -> 4 output channels 4*(tid & 15) .. +3 at
+    // positions (tid >> 4) + 16 r, r < 4 (Wo^2 <= 64); chunk kk of the weights (rows
+    // (kk, ci), 64 co) lands in ring slot kk % LAP_RING by LDS-DMA (wave w moves rows
+    // 8w .. 8w+7: two 1 KB pieces of 16 B per lane)
     {
+        const float *w3g = th + L.off_w3;
+        auto dma = [&](int kk) __attribute__((always_inline)) {
+            const int k = kk < 36 ? kk : 35;   // past the end: harmless reloads (never read)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int piece = wave * 2 + q;   // 256 floats each
+                __builtin_amdgcn_global_load_lds((const void *)(w3g + (int64_t)k * LAP_CH + piece * 256 + lane * 4),
+                                                 (__attribute__((address_space(3))) void *)(ring + (kk % LAP_RING) * LAP_CH +
+                                                                                           piece * 256),
+                                                 16, 0, 0);
+            }
+        };
+#pragma unroll
+        for (int q = 0; q < LAP_RING - 1; ++q) dma(q);
         const int cq = tid & 15, pg = tid >> 4;
         const int np = Wo * Wo;
-        float acc[4][4];
+        f32x2 acc[4][2];
         int base[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int p = pg + 16 * r;
             const int pj = p < np ? p / Wo : 0, pi = p < np ? p - pj * Wo : 0;
             base[r] = (pi + pj * bs) * 32;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[r][j] = th[L.off_b3 + 4 * cq + j];
+            acc[r][0] = f32x2{th[L.off_b3 + 4 * cq], th[L.off_b3 + 4 * cq + 1]};
+            acc[r][1] = f32x2{th[L.off_b3 + 4 * cq + 2], th[L.off_b3 + 4 * cq + 3]};
         }
-        const f32x4 *w3 = reinterpret_cast<const f32x4 *>(th + L.off_w3) + cq;   // [(kk*32+ci)*16 + cq]
         for (int kk = 0; kk < 36; ++kk) {
+            // chunk kk landed (this wave's pieces: the LAP_RING - 2 younger chunks stay in
+            // flight), every wave's pieces visible after the barrier; the slot of chunk
+            // kk - 1, refilled below, was last read before it
+            __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * (LAP_RING - 2)));
+            __syncthreads();
+            dma(kk + LAP_RING - 1);
             const int du = kk % 6, dv = kk / 6;
             const int off = (du + dv * bs) * 32;
+            const float *wk = ring + (kk % LAP_RING) * LAP_CH + 4 * cq;
 #pragma unroll 2
             for (int ci = 0; ci < 32; ci += 4) {
                 f32x4 w[4], av[4];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) w[c] = w3[(kk * 32 + ci + c) * 16];
+                for (int c = 0; c < 4; ++c) w[c] = *reinterpret_cast<const f32x4 *>(wk + (ci + c) * 64);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) av[r] = *reinterpret_cast<const f32x4 *>(a2 + base[r] + off + ci);
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
-                    for (int c = 0; c < 4; ++c)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[r][j] = __builtin_fmaf(av[r][c], w[c][j], acc[r][j]);
+                    for (int c = 0; c < 4; ++c) {
+                        const f32x2 x{av[r][c], av[r][c]};
+                        acc[r][0] = __builtin_elementwise_fma(x, f32x2{w[c][0], w[c][1]}, acc[r][0]);
+                        acc[r][1] = __builtin_elementwise_fma(x, f32x2{w[c][2], w[c][3]}, acc[r][1]);
+                    }
             }
         }
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // the clamped tail reloads
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int p = pg + 16 * r;
             if (p < np)
                 *reinterpret_cast<f32x4 *>(a3 + p * 64 + 4 * cq) =
-                    f32x4{fmaxf(acc[r][0], 0.f), fmaxf(acc[r][1], 0.f), fmaxf(acc[r][2], 0.f), fmaxf(acc[r][3], 0.f)};
+                    f32x4{fmaxf(acc[r][0][0], 0.f), fmaxf(acc[r][0][1], 0.f), fmaxf(acc[r][1][0], 0.f),
+                          fmaxf(acc[r][1][1], 0.f)};
         }
     }
     __syncthreads();
     // Dense1: thread -> 4 outputs 4*(tid & 15) .. +3 over the 16th (tid >> 4) of the
-    // K1 inputs (4 at a time: one ds_read_b128, 4 float4 weight loads, 16 FMAs), then
-    // a 16-way reduction in LDS
+    // K1 inputs (4 at a time: one ds_read_b128, 4 float4 weight loads, 16 FMAs), the
+    // weight loads three k-steps ahead in a register ring; then a 16-way reduction in LDS
     {
         const int oq = tid & 15, part = tid >> 4;
         const int kq = (L.K1 / 4 + 15) / 16 * 4, k0 = part * kq, k1 = min(L.K1, k0 + kq);
         const f32x4 *wd = reinterpret_cast<const f32x4 *>(th + L.off_d1w) + oq;   // [k*16 + oq]
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-        for (int k = k0; k < k1; k += 4) {
-            const f32x4 a = *reinterpret_cast<const f32x4 *>(a3 + k);
-            f32x4 w[4];
+        const int n = k1 > k0 ? (k1 - k0) / 4 : 0;
+        constexpr int RD = 4;
+        f32x4 wr[RD][4];
+        auto ld = [&](int i, int slot) __attribute__((always_inline)) {
+            const int k = n > 0 ? k0 + 4 * (i < n ? i : n - 1) : 0;   // past the end: reloads (unused)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) w[c] = wd[(int64_t)(k + c) * 16];
+            for (int c = 0; c < 4; ++c) wr[slot][c] = wd[(int64_t)(k + c) * 16];
+        };
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
+        for (int q = 0; q < RD - 1; ++q) ld(q, q);
+        f32x2 acc[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+        for (int i0 = 0; i0 < n; i0 += RD) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] = __builtin_fmaf(a[c], w[c][j], acc[j]);
+            for (int q = 0; q < RD; ++q) {
+                const int i = i0 + q;
+                ld(i + RD - 1, (q + RD - 1) % RD);
+                if (i < n) {
+                    const f32x4 a = *reinterpret_cast<const f32x4 *>(a3 + k0 + 4 * i);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const f32x2 x{a[c], a[c]};
+                        acc[0] = __builtin_elementwise_fma(x, f32x2{wr[q][c][0], wr[q][c][1]}, acc[0]);
+                        acc[1] = __builtin_elementwise_fma(x, f32x2{wr[q][c][2], wr[q][c][3]}, acc[1]);
+                    }
+                }
+            }
         }
-        *reinterpret_cast<f32x4 *>(red + part * 64 + 4 * oq) = acc;
+        *reinterpret_cast<f32x4 *>(red + part * 64 + 4 * oq) = f32x4{acc[0][0], acc[0][1], acc[1][0], acc[1][1]};
     }
     __syncthreads();
     if (tid < 64) {
@@ -949,13 +1010,13 @@ static void lap_rollout(snk_dqn m, const float *W, int64_t ldw, int64_t G, float
     SNK_HIP(hipMemsetAsync(len_dev, 0, G * sizeof(int32_t), s));
     const size_t lds = (size_t)lap_act_lds_floats(L) * sizeof(float);
     SNK_CHECK(lds <= 160 * 1024 && L.Wo * L.Wo <= 64 && L.K1 % 4 == 0 && L.off_w3 % 4 == 0 && L.off_d1w % 4 == 0 &&
-                  (G == 1 || ldw % 4 == 0),
+                  (G == 1 || ldw % 4 == 0) && lap_act_front_floats(L) % 4 == 0,
               SNK_ERR_INVALID,
               "Laplace sampling: board side %d too large", L.bs);
     set_lds_limit((const void *)lap_act_kernel, lds);
     const BoardSrc src = src_env(E);
     for (int t = 0; t < T; ++t) {
-        lap_act_kernel<<<(unsigned)G, 256, lds, s>>>(L, W, ldw, src, fin, act, nullptr);
+        lap_act_kernel<<<(unsigned)G, 256, lds, s>>>(L, W, ldw, src, fin, act, nullptr, (int)lap_act_front_floats(L));
         launch_check("lap_act_kernel");
         env_launch_step(E, act, SNK_ACT_INDEX, &R, s);
         lap_track_kernel<<<(unsigned)ceil_div(G, 256), 256, 0, s>>>(E.out_done, E.out_ep_reward, G, t, fin, len_dev,

@@ -880,7 +880,7 @@ void qwork_free(QWork &w) {
     for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a2b, (void *)w.a1b, (void *)w.a3, (void *)w.slab, (void *)w.cslab,
                     (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.x0, (void *)w.target,
-                    (void *)w.loss, (void *)w.wmax_part})
+                    (void *)w.loss, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e})
         dfree(p);
     w = QWork{};
 }
@@ -938,6 +938,8 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     w.h1 = dalloc<float>((size_t)cap * 64);
     w.q = dalloc<float>((size_t)cap * 3);
     w.wmax_part = dalloc<float>((size_t)std::max<int64_t>(cap, 256));
+    w.w3h = dalloc<uint16_t>((size_t)36 * 512 * 8);
+    w.w3e = dalloc<int>(1);
     if (tr) {
         w.has_train = 1;
         w.dq = dalloc<float>((size_t)cap * 3);
@@ -972,15 +974,26 @@ static void h3c2_launch_bs(const float *a1, const float *wimg, const float *b2, 
     launch_check("conv_h3c2_kernel");
 }
 
-// conv3 B staging: 4 LDS buffers, one barrier per offset pair
+// conv3 B staging: 8 LDS buffers filled by LDS-DMA from the pre-split image (fa.w3h,
+// w3_split_kernel) where they fit (board side <= 12); else 4 buffers split in registers.
+// One barrier per offset pair either way.
 template <int HIN, int CF>
 static void h3f_launch_t(const H3FArgs &fa, int64_t S, hipStream_t s) {
-    constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, 4>();
-    static_assert(lds <= 160 * 1024, "conv_h3f LDS");
-    set_lds_limit((const void *)conv_h3f_kernel<HIN, 4, CF>, lds);
-    conv_h3f_kernel<HIN, 4, CF><<<(unsigned)(ceil_div(S, 4) + (fa.rider.out ? 1 : 0)), 512, lds, s>>>(fa, (int)S);
+    const unsigned grid = (unsigned)(ceil_div(S, 4) + (fa.rider.out ? 1 : 0));
+    if constexpr (h3f_lds_bytes<HIN, 8>() <= 160 * 1024) {
+        constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, 8>();
+        SNK_CHECK(fa.w3h && fa.w3e, SNK_ERR_INTERNAL, "conv_h3f: no pre-split conv3 weights");
+        set_lds_limit((const void *)conv_h3f_kernel<HIN, 8, CF>, lds);
+        conv_h3f_kernel<HIN, 8, CF><<<grid, 512, lds, s>>>(fa, (int)S);
+    } else {
+        constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, 4>();
+        static_assert(lds <= 160 * 1024, "conv_h3f LDS");
+        set_lds_limit((const void *)conv_h3f_kernel<HIN, 4, CF>, lds);
+        conv_h3f_kernel<HIN, 4, CF><<<grid, 512, lds, s>>>(fa, (int)S);
+    }
     launch_check("conv_h3f_kernel");
 }
+static bool h3f_dma(int bs) { return bs <= 12; }
 template <int HIN>
 static void h3f_launch_bs(const H3FArgs &fa, int C, int64_t S, hipStream_t s) {
     if (C == 1)
@@ -1075,8 +1088,16 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
                 rd = SampleRider{};
             }
             SNK_CHECK(!rd.out || (lo <= 2 && hi >= 1), SNK_ERR_INTERNAL, "sample rider without a launch");
+            if (lo <= 2 && hi >= 1 && h3f_dma(L.bs)) {   // the conv3 weights pre-split once for every workgroup
+                w3_split_kernel<<<36 * 512 / 256, 256, 0, s>>>(img, w.wmax_part, w.wmax_n, w.w3h, w.w3e);
+                launch_check("w3_split_kernel");
+            }
             if (lo <= 2 && hi >= 1) {
                 H3FArgs fa{};
+                if (h3f_dma(L.bs)) {
+                    fa.w3h = w.w3h;
+                    fa.w3e = w.w3e;
+                }
                 fa.rider = rd;
                 fa.src = n.src; fa.w1 = n.th + L.off_w1; fa.b1 = n.th + L.off_b1;
                 fa.w2 = n.wt + L.off_t2; fa.b2 = n.th + L.off_b2; fa.w3 = img; fa.wmax = w.wmax_part;

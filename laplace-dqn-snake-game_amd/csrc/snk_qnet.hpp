@@ -72,6 +72,8 @@ struct QWork {
     const float *wmax_img = nullptr; //   of this image
     int wmax_fresh = 0;              //   set by the trainer: the partials were written by the grad_update that
                                      //   last changed the image (the next full forward skips its scan; reset there)
+    uint16_t *w3h = nullptr;         // h3 conv3 weights pre-split for conv_h3f_kernel's LDS-DMA staging:
+    int *w3e = nullptr;              //   [36 kk][512 16-byte chunks] in the B buffers' swizzled order, and their exponent
     double *target = nullptr, *loss = nullptr;
     int has_train = 0;
     int64_t gen = 0;          // bumped on every reallocation (captured graphs hold the old pointers)

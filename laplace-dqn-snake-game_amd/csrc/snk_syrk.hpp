@@ -314,7 +314,6 @@ static __global__ __launch_bounds__(256) void h3_seg_rows_kernel(H3Segs sg, int6
 // MFMAs. Rows past N read row N-1 (never stored); the zero tail of ldh
 // covers the k range.
 constexpr int SH_BUF = 4, SH_ROW = 32;   // halves per LDS row (one 32-k stage)
-__device__ __forceinline__ constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
 // NW waves: 8 (two per SIMD, 64 x 32 per wave) or 4 (one per SIMD, 64 x 64 per wave:
 // half the fragment reads per MFMA)

@@ -209,3 +209,143 @@ def test_deep_net_refused_by_jacobian_and_laplace_sampling(snk):
     tr = snk.Trainer(n_envs=64, board_size=12, n_frames=2, capacity=256, model=m, seed=3)
     with pytest.raises(snk.SnakeHipError, match="deep"):
         snk.laplace_sampling_(tr, lap, n_models=4)
+
+
+def _threaded(fn, parts, workers=16):
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(min(workers, len(parts))) as ex:
+        return list(ex.map(fn, parts))
+
+
+def _deep_q(bs, C, p, x):
+    parts = [ix for ix in np.array_split(np.arange(len(x)), min(16, len(x))) if len(ix)]
+    return np.concatenate(_threaded(lambda ix: oracle.deep_forward(bs, C, p, x[ix]), parts))
+
+
+def _deep_loss_grad(bs, C, qp, tp, f, ac, rw, dn, mk):
+    """oracle.deep_loss_grad over the batch in 16 threads: the Huber loss is a mean, so the
+    chunks' (loss, gradient) are weighted by their share of the batch (fp64 sums)."""
+    B = len(ac)
+    parts = [ix for ix in np.array_split(np.arange(B), 16) if len(ix)]
+    res = _threaded(lambda ix: oracle.deep_loss_grad(bs, C, qp, tp, f[ix, :C], ac[ix], rw[ix], f[ix, 1:], dn[ix],
+                                                     mk[ix]), parts)
+    loss = sum(r[0] * len(ix) for r, ix in zip(res, parts)) / B
+    g = sum(r[1] * len(ix) for r, ix in zip(res, parts)) / B
+    return loss, g
+
+
+def test_configs2_trainer_graph_trajectory_vs_oracle(snk):
+    """configs[2] as bench.py times it: 65,536 lockstep 20x20 games, 2 frames, the
+    deeper bf16 net, replay capacity 50,000 (each lockstep step overfills it: only the
+    step's last 50,000 transitions survive, as sequential store! leaves them), B = 64,
+    one captured graph of 4 iterations (deep_front_kernel / deep_conv3_kernel /
+    deep_dense1_kernel act forward over 65,536 states, the 20x20 step + store, the
+    deep update: deep_conv3_small_kernel forward, the LDS-image backward kernels,
+    RMSProp + images + target sync). epsilon 0.25, so most actions are greedy.
+    The act / Q trace and the gradient trace make every iteration of the graph
+    observable; the oracle replays it decision by decision:
+      explored actions, env outputs, boards, all 50,000 replay slots   bit-exact
+      greedy actions == first argmax of the device's own Q            exact
+      Q of 96 sampled states per iteration (every part of the grid)
+        vs the oracle's bf16 restatement at that iteration's params   2e-3 (as above)
+      greedy actions vs the oracle argmax (top-2 margin > 1e-3)       exact
+      every update, teacher-forced (the device's q_net, t_net, accumulator before it):
+        loss relative 2e-3, gradient normwise 1e-3
+      q_net, accumulator, t_net after the graph == Float32 RMSProp of the traced
+        gradients, t_net synced at nb % 3 == 0                        bit-exact"""
+    from devrng import TRAINER_SAMPLE_SALT, explore_np, first_argmax_np, floyd
+    bs, C, n, cap, B, rate, U, eps, seed = 20, 2, 65536, 50_000, 64, 3, 4, np.float32(0.25), 0xD2D2
+    tr = snk.Trainer(n_envs=n, board_size=bs, n_frames=C, capacity=cap, batch_size=B, n_batches=10_000,
+                     target_update_rate=rate, epsilon=float(eps), epsilon_end=float(eps), decay=0.0, seed=seed,
+                     graph_unroll=U, deep=True)
+    m = tr.model
+    P = m.P
+    perm = m.flux_index()
+    gring = snk.DeviceArray((U, P), np.float32)
+    aring = snk.DeviceArray((U, n), np.uint8)
+    qring = snk.DeviceArray((U, n, 3), np.float32)
+    tr.set_trace(gring)
+    tr.set_act_trace(aring, qring)
+    ob = oracle.OracleBatch(n, bs, C)
+    nc = bs * bs
+    frames = np.zeros((cap, C + 1, nc), np.int8)
+    o_act = np.zeros(cap, np.int32)
+    o_rew = np.zeros(cap, np.float32)
+    o_done = np.zeros(cap, np.uint8)
+    o_mask = np.zeros((cap, 3), np.uint8)
+    st = {"count": 0, "t": 0, "q": 0.0, "greedy": 0}
+
+    def check_acts(a, q, th, it):
+        states = ob.states()
+        ex = explore_np(seed, n, st["t"], eps)
+        rnd = ex >= 0
+        assert np.array_equal(a[rnd], ex[rnd]), st["t"]
+        assert np.array_equal(a[~rnd], first_argmax_np(q[~rnd])), st["t"]
+        sel = np.linspace(0, n - 8, 96).astype(np.int64) + it % 7
+        qref = _deep_q(bs, C, th, states[sel].astype(np.float32))
+        err = _err(q[sel], qref)
+        st["q"] = max(st["q"], err)
+        assert err <= 2e-3, (st["t"], err)
+        g = ~rnd[sel]
+        top = np.sort(qref[g], axis=1)
+        ok = top[:, 2] - top[:, 1] > 1e-3
+        assert np.array_equal(a[sel][g][ok], first_argmax_np(qref[g])[ok]), st["t"]
+        st["greedy"] += int(ok.sum())
+
+    def oracle_step(a):
+        out = ob.step(a)
+        keep = np.arange(max(0, n - cap), n)           # the step's surviving transitions
+        k = (st["count"] + keep) % cap
+        frames[k], o_act[k], o_rew[k] = out["frames"][keep], a[keep], out["reward"][keep]
+        o_done[k], o_mask[k] = out["done"][keep], out["mask"][keep]
+        st["count"] += n
+        st["t"] += 1
+        return out
+
+    def check_env(out):
+        o = tr.game.last("reward", "done", "mask")
+        assert np.array_equal(o["reward"], out["reward"]) and np.array_equal(o["done"], out["done"]), st["t"]
+        assert np.array_equal(o["mask"], out["mask"] @ np.array([1, 2, 4], np.uint8)), st["t"]
+        assert np.array_equal(tr.game.board_cells(), ob.boards()), st["t"]
+
+    th0 = m.get_params()
+    tr.run(1, learn=False, graph=True)                   # fill_buffer!: one step overfills the ring
+    check_acts(aring.numpy()[0], qring.numpy()[0], th0, 0)
+    out = oracle_step(aring.numpy()[0])
+    check_env(out)
+    assert len(tr.buffer) == cap
+
+    th, acc, tt = m.get_params(), m.get_params(snk.SNK_NET_OPT_STATE), m.get_params(snk.SNK_NET_TARGET)
+    tr.run(U, learn=True, graph=True)
+    acts, qs = aring.numpy(), qring.numpy()
+    gdev = np.empty((U, P), np.float32)
+    gdev[:, perm] = gring.numpy()
+    losses = tr.losses
+    sseed = seed ^ TRAINER_SAMPLE_SALT
+    worst_l = worst_g = 0.0
+    for i in range(U):
+        check_acts(acts[i], qs[i], th, 1 + i)
+        out = oracle_step(acts[i])
+        ids = floyd(sseed, i, min(st["count"], cap), B)
+        f = frames[ids]
+        lref, gref = _deep_loss_grad(bs, C, th, tt, f, o_act[ids], o_rew[ids], o_done[ids], o_mask[ids])
+        rl = abs(losses[i] - lref) / abs(lref)
+        rg = float(np.linalg.norm(gdev[i] - gref) / np.linalg.norm(gref))
+        worst_l, worst_g = max(worst_l, rl), max(worst_g, rg)
+        assert rl <= 2e-3 and rg <= 1e-3, (i, rl, rg)
+        th, acc = oracle.rmsprop(th, acc, gdev[i])
+        if i % rate == 0:
+            tt = th.copy()
+    check_env(out)
+    assert np.array_equal(m.get_params(), th) and np.array_equal(m.get_params(snk.SNK_NET_OPT_STATE), acc)
+    assert np.array_equal(m.get_params(snk.SNK_NET_TARGET), tt)
+    s = tr.stats()
+    assert s["updates"] == U and s["env_steps"] == st["t"] * n
+    got = snk.stack_exp(tr.buffer, np.arange(cap))
+    assert np.array_equal(got["states"], frames[:, :C].astype(np.float32))
+    assert np.array_equal(got["next_states"], frames[:, 1:].astype(np.float32))
+    assert np.array_equal(got["actions"], o_act + 1) and np.array_equal(got["rewards"], o_rew)
+    assert np.array_equal(got["dones"], o_done.astype(bool))
+    assert np.array_equal(got["suicidal_mask"], o_mask.astype(bool))
+    print(f"configs[2] graph: {st['t']} steps of {n} envs, Q max err {st['q']:.2e}, {st['greedy']} greedy actions "
+          f"vs the oracle; {U} updates: loss rel max {worst_l:.2e}, gradient max {worst_g:.2e}")

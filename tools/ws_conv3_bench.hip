@@ -35,33 +35,50 @@ __global__ __launch_bounds__(256) void ws(const u32x4 *w, const u32x4 *img, floa
         abase[k] = sr * XS + g * GG + j * XW + i;
     }
     for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
-        f32x4 acc[NT][2];
+        // two passes over the offsets, row tiles [0, 7) then [7, 13): 56 accumulator registers
 #pragma unroll
-        for (int k = 0; k < NT; ++k) acc[k][0] = acc[k][1] = f32x4{0, 0, 0, 0};
+        for (int pass = 0; pass < 2; ++pass) {
+            constexpr int TP = 7;
+            const int t0 = pass * TP, tn = pass ? NT - TP : TP;
+            f32x4 acc[TP][2];
 #pragma unroll
-        for (int kq = 0; kq < 18; ++kq) {
-            const int kk = oh * 18 + kq, dv = kk / 6, du = kk - dv * 6, off = dv * XW + du;
+            for (int k = 0; k < TP; ++k) acc[k][0] = acc[k][1] = f32x4{0, 0, 0, 0};
+            // A fragments two tiles ahead (named rotation: stage n holds tile n of the flattened (kq, k) walk)
+            constexpr int NST = 3;
+            f16x8 fh[NST], fl[NST];
+            auto rd = [&](int n, int slot) __attribute__((always_inline)) {
+                const int kq = n / TP, k = n % TP;
+                if (kq >= 18 || k >= tn) return;
+                const int kk = oh * 18 + kq, dv = kk / 6, du = kk - dv * 6, off = dv * XW + du;
+                fh[slot] = __builtin_bit_cast(f16x8, As[abase[t0 + k] + off]);
+                fl[slot] = __builtin_bit_cast(f16x8, As[abase[t0 + k] + off + PL]);
+            };
+            rd(0, 0);
+            rd(1, 1);
 #pragma unroll
-            for (int k = 0; k < NT; ++k) {
-                const f16x8 ah = __builtin_bit_cast(f16x8, As[abase[k] + off]);
-                const f16x8 al = __builtin_bit_cast(f16x8, As[abase[k] + off + PL]);
+            for (int n = 0; n < 18 * TP; ++n) {
+                const int kq = n / TP, k = n % TP;
+                rd(n + 2, (n + 2) % NST);
+                if (k < tn) {
+                    const f16x8 ah = fh[n % NST], al = fl[n % NST];
 #pragma unroll
-                for (int ct = 0; ct < 2; ++ct) {
-                    f32x4 c = acc[k][ct];
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wf[kq][ct][0], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wf[kq][ct][1], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wf[kq][ct][0], c, 0, 0, 0);
-                    acc[k][ct] = c;
+                    for (int ct = 0; ct < 2; ++ct) {
+                        f32x4 c = acc[k][ct];
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wf[kq][ct][0], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wf[kq][ct][1], c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wf[kq][ct][0], c, 0, 0, 0);
+                        acc[k][ct] = c;
+                    }
                 }
             }
+#pragma unroll
+            for (int k = 0; k < TP; ++k)
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (k < tn) out[(((int64_t)grp * NT * 2 + (t0 + k) * 2 + ct) * 4 + e) * 256 + tid] = acc[k][ct][e];
         }
-#pragma unroll
-        for (int k = 0; k < NT; ++k)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    out[(((int64_t)grp * NT * 2 + k * 2 + ct) * 4 + e) * 256 + tid] = acc[k][ct][e];
     }
 }
 
