@@ -38,19 +38,57 @@ struct H3FArgs {
     const float *b3;     // conv3 bias [64]
     float *out;          // a3 [S][ho^2][64]
     SampleRider rider;   // rider.out: one extra workgroup runs this replay draw (the trainer's update sample)
-    // NBUF = 8: w3 pre-split (w3_split_kernel) into the B buffers' byte order, copied by LDS-DMA
+    // NBUF = 8: w3 pre-split (w3_split_kernel) into the B buffers' byte order, copied by LDS-DMA;
+    // w2h the conv2 weights pre-split into the B2 image's bytes (H3F_B2_CHUNKS 16-byte chunks)
     const uint16_t *w3h;
-    const int *w3e;      // its exponent (ew)
+    const int *w3e;      // w3h's exponent (ew), then w2h's (ew2)
+    const uint16_t *w2h;
 };
+// conv2's split weight image in LDS: [5 offset pairs][h | l][32 co][48 halves] (k = 16 (kk & 1)
+// + ci in the first 32 halves of a row; kk = 9 is zero), 1,920 16-byte chunks, padded to 2,048
+constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 
 // conv3's weight image [36 kk][64 co][32 ci] (fp32) -> fp16 h / l parts of w * 2^ew, ew from the
 // partial maxima, laid out exactly as conv_h3f_kernel's register path stores one offset into a B
 // buffer (512 16-byte chunks per offset: h chunk x6s_bswz(c), l chunk x6s_bswz(256 + c) for the
 // chunk c = (co, ci / 8); each of its two 8-byte halves one float4 of the image): a lane-linear
 // copy of an offset's 8 KB is then a B buffer. One thread per float4 of the image.
+// Blocks 72..76: conv2's image [9 kk][32 co][16 ci] (fp32, 1,152 float4) split with its own
+// per-tensor exponent ew2 = h3_exp(max |w2|) into the B2 image (out2, zero-initialised: the
+// pad offset and the pad columns stay zero), eout[1] = ew2.
+constexpr int W3S_BLOCKS = 36 * 512 / 256, W2S_BLOCKS = (9 * 32 * 16 / 4 + 255) / 256;
 static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__restrict__ img, const float *__restrict__ wmax,
-                                                       int nwmax, uint16_t *__restrict__ out, int *__restrict__ eout) {
+                                                       int nwmax, uint16_t *__restrict__ out, int *__restrict__ eout,
+                                                       const float *__restrict__ img2, uint16_t *__restrict__ out2) {
     __shared__ float red4[4];
+    if (blockIdx.x >= W3S_BLOCKS) {   // conv2
+        constexpr int NW4 = 9 * 32 * 16 / 4;
+        const f32x4 *w4 = reinterpret_cast<const f32x4 *>(img2);
+        const int e = (blockIdx.x - W3S_BLOCKS) * 256 + threadIdx.x;
+        float m = 0.0f;
+        for (int i = threadIdx.x; i < NW4; i += 256) {
+            const f32x4 v = w4[i];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        }
+        m = wave_max(m);
+        if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+        __syncthreads();
+        const int ew2 = h3_exp(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
+        if (blockIdx.x == W3S_BLOCKS && threadIdx.x == 0) eout[1] = ew2;
+        if (e < NW4) {
+            const int kk = e >> 7, co = (e >> 2) & 31, ci0 = 4 * (e & 3);
+            const int p = kk >> 1, k0 = 16 * (kk & 1) + ci0;
+            u32x2 hh, ll;
+            h3_split4(w4[e], ew2, hh, ll);
+            u32x2 *o2 = reinterpret_cast<u32x2 *>(out2);
+            o2[(((p * 2 + 0) * 32 + co) * H3F_B2_BR + k0) / 4] = hh;
+            o2[(((p * 2 + 1) * 32 + co) * H3F_B2_BR + k0) / 4] = ll;
+        }
+        return;
+    }
+    const int t = blockIdx.x * 256 + threadIdx.x;   // < 36 * 512
+    const int kk = t >> 9, tt = t & 511;
+    const f32x4 v = reinterpret_cast<const f32x4 *>(img)[t];   // in flight beside the partial maxima
     float m = 0.0f;
     for (int i = threadIdx.x; i < nwmax; i += 256) m = fmaxf(m, wmax[i]);
     m = wave_max(m);
@@ -58,9 +96,6 @@ static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__res
     __syncthreads();
     const int ew = h3_exp(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
     if (blockIdx.x == 0 && threadIdx.x == 0) *eout = ew;
-    const int t = blockIdx.x * 256 + threadIdx.x;   // < 36 * 512
-    const int kk = t >> 9, tt = t & 511;
-    const f32x4 v = reinterpret_cast<const f32x4 *>(img)[t];
     const int bch = (tt >> 3) * 4 + ((tt & 7) >> 1), bhalf = tt & 1;
     u32x2 h, l;
     h3_split4(v, ew, h, l);
@@ -86,7 +121,7 @@ template <int HIN, int NBUF = 4>
 constexpr int h3f_lds_bytes() {
     constexpr int ho = HIN - 5, XW = ho + 8, PL = (HIN * XW + 3) & ~3, XS = 4 * 2 * PL + 4;
     constexpr int BP = HIN + 2;
-    constexpr int c2 = (4 * 2 * BP * BP * 16 + 5 * 2 * 32 * 48) * 2;   // conv2 staging (halves)
+    constexpr int c2 = (4 * 2 * BP * BP * 16 + 2048 * 8) * 2;   // conv2 staging: A1 image + the B2 image (2,048 chunks)
     constexpr int c3 = 4 * XS * 16;                                     // conv3 A image
     constexpr int cs = 4 * ho * ho * 80 * 4;                            // output staging
     constexpr int m = c2 > c3 ? (c2 > cs ? c2 : cs) : (c3 > cs ? c3 : cs);
@@ -159,11 +194,17 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
                                              16, 0, 0);
         }
     };
-    if constexpr (DMA) {   // offsets 0..3 now (conv1 stages its boards in buffer 7)
+    if constexpr (DMA) {   // offsets 0..3 now (conv1 stages its boards in buffer 7), and conv2's weights
         dma(0);
         dma(1);
         dma(2);
         dma(3);
+        static_assert(H3F_B2_CHUNKS == 4 * 512, "four B2 pieces per thread");
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            __builtin_amdgcn_global_load_lds((const void *)(a.w2h + ((int64_t)q * 512 + tid) * 8),
+                                             (__attribute__((address_space(3))) void *)(B2 + (q * 512 + wave * 64) * 8),
+                                             16, 0, 0);
     } else {
         b_load(0, 0);
         b_load(1, 1);
@@ -171,7 +212,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     // conv3 weight-max partials: loaded here, reduced after conv1 (their latency hides
     // behind the board loads instead of following conv1)
     const float wmx = !DMA && tid < a.nwmax ? a.wmax[tid] : 0.0f;
-    const int ew_dma = DMA ? *a.w3e : 0;
+    const int ew_dma = DMA ? a.w3e[0] : 0, ew2_dma = DMA ? a.w3e[1] : 0;
 
     // conv2 bias of this lane's output channels (16 ct + 4 g + e), early
     float b2v[2][4];
@@ -191,7 +232,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
                                                                                      : (BP - 1 - t) * BP;
             reinterpret_cast<u32x4 *>(A1)[((pc * NPB + pb) * XR) / 8 + piece] = u32x4{0u, 0u, 0u, 0u};
         }
-        if (tid < 2 * 32 * 2) {   // plane, co, two 16-byte pieces (k 16..31)
+        if (!DMA && tid < 2 * 32 * 2) {   // plane, co, two 16-byte pieces (k 16..31)
             const int pl = tid >> 6, co = (tid >> 1) & 31, piece = tid & 1;
             reinterpret_cast<u32x4 *>(B2)[(((4 * 2 + pl) * 32 + co) * BR + 16) / 8 + piece] = u32x4{0u, 0u, 0u, 0u};
         }
@@ -200,7 +241,8 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     const f32x4 *w4 = reinterpret_cast<const f32x4 *>(a.w2);
     const int na4 = ns * hin2 * 4;
 #pragma unroll
-    for (int u = 0; u < LW; ++u) wv[u] = w4[min(u * 512 + tid, NW4 - 1)];
+    for (int u = 0; u < LW; ++u)
+        if (!DMA) wv[u] = w4[min(u * 512 + tid, NW4 - 1)];
     {
         // ---- conv1: boards -> bordered float planes in the B buffers; each thread always
         // computes the same four output channels (4 (tid & 3) .. +3), so its 9 CF weight
@@ -282,7 +324,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
 #pragma unroll
     for (int u = 0; u < LW; ++u) {
         const f32x4 v = wv[u];
-        if (u * 512 + tid < NW4)
+        if (!DMA && u * 512 + tid < NW4)
             mw2 = fmaxf(mw2, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     }
 #pragma unroll
@@ -316,13 +358,13 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         }
 #pragma unroll
         for (int q = 0; q < NSG; ++q) ea1[q] = h3_exp(m[q]);
-        ew2 = h3_exp(m[4]);
+        ew2 = DMA ? ew2_dma : h3_exp(m[4]);
         ew = DMA ? ew_dma : h3_exp(m[5]);
     }
 #pragma unroll
     for (int u = 0; u < LW; ++u) {   // image [kk][co][ci]: k = 16 * (kk - 2p) + ci in offset pair p
         const int e = u * 512 + tid;
-        if (e < NW4) {
+        if (!DMA && e < NW4) {
             const int kk = e >> 7, co = (e >> 2) & 31, ci0 = 4 * (e & 3);
             const int p = kk >> 1, k0 = 16 * (kk & 1) + ci0;
             u32x2 hh, ll;

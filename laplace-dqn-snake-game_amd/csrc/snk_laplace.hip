@@ -687,8 +687,8 @@ __global__ void lap_normals_kernel(uint64_t seed, uint64_t model, uint32_t strea
 
 // W[g][j] (packed index j, Flux index fi = perm[j]) for models n0 .. n0+G-1:
 //   w = (mean[fi] + (c1 * sqrt|var[fi]|) * z1(fi)) + sum_k (c2 * D[k][fi]) * z2(k)   (k ascending)
-// 8 models per pass keep their gemv sums in registers; z2 of the G models in LDS
-constexpr int LAP_GM = 8;
+// LAP_GM models per pass keep their gemv sums in registers; z2 of the G models in LDS
+constexpr int LAP_GM = 32;   // models per pass: each pass re-reads D (P x K doubles) once
 __global__ __launch_bounds__(256) void lap_sample_kernel(const double *__restrict__ mean, const double *__restrict__ var,
                                                          const double *__restrict__ D, int K, int64_t P,
                                                          const int32_t *__restrict__ perm, uint64_t seed, int64_t n0,
@@ -721,16 +721,18 @@ __global__ __launch_bounds__(256) void lap_sample_kernel(const double *__restric
     }
 }
 
-// lap_act_kernel's LDS (floats): [xin | a1 | w2s] (overlaid by the conv3 weight ring
-// once conv2 is done) | a2 | a3 | Dense1 partials | h1
-constexpr int LAP_RING = 5;          // conv3 weight chunks (one kernel offset, 32 x 64 floats) in flight
+// lap_act_kernel's LDS (floats): a front region holding [xin | a1 | w2s] until conv2 is
+// done, then the conv3 weight ring, then [a3 | Dense1 partials | h1]; and a2. About 50 KB
+// at 12x12: three workgroups (models) per CU.
+constexpr int LAP_RING = 4;          // conv3 weight chunks (one kernel offset, 32 x 64 floats) in flight
 constexpr int LAP_CH = 32 * 64;
 static inline int64_t lap_act_front_floats(const QLayout &L) {
     const int bp = L.bs + 2, r4 = (L.C * bp * bp + 3) & ~3, a4 = (16 * bp * bp + 3) & ~3;
-    return std::max<int64_t>((int64_t)r4 + a4 + 9 * 16 * 32, (int64_t)LAP_RING * LAP_CH);
+    const int64_t tail = ((int64_t)L.K1 + 16 * 64 + 64 + 8 + 3) & ~int64_t(3);
+    return std::max<int64_t>(std::max<int64_t>((int64_t)r4 + a4 + 9 * 16 * 32, (int64_t)LAP_RING * LAP_CH), tail);
 }
 static inline int64_t lap_act_lds_floats(const QLayout &L) {
-    return lap_act_front_floats(L) + (int64_t)L.ncell * 32 + L.K1 + 16 * 64 + 64 + 8;
+    return lap_act_front_floats(L) + (int64_t)L.ncell * 32;
 }
 
 // one workgroup (256 threads) per env g: the greedy action of model g on the env's state.
@@ -756,7 +758,7 @@ __global__ __launch_bounds__(256) void lap_act_kernel(QLayout L, const float *__
     float *w2s = a1 + ((16 * bp * bp + 3) & ~3);  // conv2 weights [(kk*16+ci)*32+co]
     float *ring = lsm;                      // conv3 weight chunks [LAP_RING][32 ci][64 co] (after conv2)
     float *a2 = lsm + front;                // [ncell][32]
-    float *a3 = a2 + nc * 32;               // [Wo*Wo][64]
+    float *a3 = lsm;                        // [Wo*Wo][64] (after conv3: over the ring)
     float *red = a3 + L.K1;                 // [16][64] Dense1 partial sums
     float *h1 = red + 16 * 64;              // [64]
     const float *th = W + g * ldw;
@@ -786,28 +788,45 @@ __global__ __launch_bounds__(256) void lap_act_kernel(QLayout L, const float *__
         }
     }
     __syncthreads();
-    // conv2 (3x3, 16 -> 32, pad 1): co = tid & 31, positions p and p + 8 h (h = ceil(rows / 2)
-    // rows of 8 apart) as one packed accumulator pair
+    // conv2 (3x3, 16 -> 32, pad 1): thread -> output channels 4 (tid & 7) .. +3 at positions
+    // (tid >> 3) + 32 r, r < ceil(ncell / 32): per (kk, ci) one ds_read_b128 of four weights and
+    // one a1 read per position feed 4 FMAs per position (packed in pairs); every output's
+    // FMA chain runs kk, then ci, ascending, as the scalar form
     {
-        const int co = tid & 31, p0 = tid >> 5;
-        const float b = th[L.off_b2 + co];
-        const int nr = (nc - p0 + 7) / 8, hr = (nr + 1) / 2;   // this thread's positions p0 + 8 r, r < nr
-        for (int r = 0; r < hr; ++r) {
-            const int pa = p0 + 8 * r, rb = r + hr;
-            const int pb = rb < nr ? p0 + 8 * rb : pa;
-            const int ja = pa / bs, ia = pa - ja * bs, jb = pb / bs, ib = pb - jb * bs;
-            f32x2 acc{b, b};
-            for (int kk = 0; kk < 9; ++kk) {
-                const int du = kk % 3, dv = kk / 3;
-                const float *apa = a1 + (ia + du) + (ja + dv) * bp, *apb = a1 + (ib + du) + (jb + dv) * bp;
-#pragma unroll 4
-                for (int ci = 0; ci < 16; ++ci) {
-                    const float w = w2s[(kk * 16 + ci) * 32 + co];
-                    acc = __builtin_elementwise_fma(f32x2{apa[ci * bp * bp], apb[ci * bp * bp]}, f32x2{w, w}, acc);
+        constexpr int RP = 6;   // positions per thread: ncell <= 32 * RP (board side <= 13)
+        const int cq = tid & 7, pg = tid >> 3;
+        const f32x4 b4 = *reinterpret_cast<const f32x4 *>(th + L.off_b2 + 4 * cq);
+        f32x2 acc[RP][2];
+        int pb[RP];
+#pragma unroll
+        for (int r = 0; r < RP; ++r) {
+            const int p = min(pg + 32 * r, nc - 1);
+            const int j = p / bs, i = p - j * bs;
+            pb[r] = i + j * bp;
+            acc[r][0] = f32x2{b4[0], b4[1]};
+            acc[r][1] = f32x2{b4[2], b4[3]};
+        }
+        for (int kk = 0; kk < 9; ++kk) {
+            const int koff = kk % 3 + (kk / 3) * bp;
+#pragma unroll 2
+            for (int ci = 0; ci < 16; ++ci) {
+                const f32x4 w = *reinterpret_cast<const f32x4 *>(w2s + (kk * 16 + ci) * 32 + 4 * cq);
+                const float *ap = a1 + ci * bp * bp + koff;
+#pragma unroll
+                for (int r = 0; r < RP; ++r) {
+                    const float x = ap[pb[r]];
+                    acc[r][0] = __builtin_elementwise_fma(f32x2{x, x}, f32x2{w[0], w[1]}, acc[r][0]);
+                    acc[r][1] = __builtin_elementwise_fma(f32x2{x, x}, f32x2{w[2], w[3]}, acc[r][1]);
                 }
             }
-            a2[pa * 32 + co] = fmaxf(acc[0], 0.0f);
-            if (rb < nr) a2[pb * 32 + co] = fmaxf(acc[1], 0.0f);
+        }
+#pragma unroll
+        for (int r = 0; r < RP; ++r) {
+            const int p = pg + 32 * r;
+            if (p < nc)
+                *reinterpret_cast<f32x4 *>(a2 + p * 32 + 4 * cq) =
+                    f32x4{fmaxf(acc[r][0][0], 0.f), fmaxf(acc[r][0][1], 0.f), fmaxf(acc[r][1][0], 0.f),
+                          fmaxf(acc[r][1][1], 0.f)};
         }
     }
     __syncthreads();   // conv1/conv2 staging free: the conv3 weight ring overlays it
@@ -870,6 +889,7 @@ __global__ __launch_bounds__(256) void lap_act_kernel(QLayout L, const float *__
             }
         }
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // the clamped tail reloads
+        __syncthreads();                              // every wave's ring reads done: a3 overlays the ring
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int p = pg + 16 * r;
@@ -1010,7 +1030,7 @@ static void lap_rollout(snk_dqn m, const float *W, int64_t ldw, int64_t G, float
     SNK_HIP(hipMemsetAsync(len_dev, 0, G * sizeof(int32_t), s));
     const size_t lds = (size_t)lap_act_lds_floats(L) * sizeof(float);
     SNK_CHECK(lds <= 160 * 1024 && L.Wo * L.Wo <= 64 && L.K1 % 4 == 0 && L.off_w3 % 4 == 0 && L.off_d1w % 4 == 0 &&
-                  (G == 1 || ldw % 4 == 0) && lap_act_front_floats(L) % 4 == 0,
+                  (G == 1 || ldw % 4 == 0) && lap_act_front_floats(L) % 4 == 0 && L.ncell <= 32 * 6,
               SNK_ERR_INVALID,
               "Laplace sampling: board side %d too large", L.bs);
     set_lds_limit((const void *)lap_act_kernel, lds);
@@ -1089,32 +1109,36 @@ extern "C" int snk_laplace_sampling(snk_laplace h, snk_dqn m, snk_replay rb, int
         SNK_CHECK(D.bs == L.bs && D.C == L.C, SNK_ERR_INVALID, "replay geometry differs from the model");
         hipStream_t s = stream();
         const int64_t P = L.P;
-        const int64_t G0 = chunk > 0 ? chunk : std::max<int64_t>(1, std::min<int64_t>(n_models, 4096));
+        // every model in ONE lockstep rollout unless a chunk is asked for (16,384 models of
+        // 1.1 MB fit easily; each chunk pays a whole rollout's 501 steps); the current q_net's
+        // own greedy episode (play_episode(tr.model, 0f0), la_utils.jl:101) rides in the first
+        // chunk as one more env: row G of W holds its packed theta
+        const int64_t G0 = chunk > 0 ? chunk : std::max<int64_t>(1, std::min<int64_t>(n_models, 16384));
         const int64_t ldw = (P + 3) & ~int64_t(3);   // 16-byte aligned model rows (float4 weight loads)
-        DevBuf<float> W((size_t)std::max<int64_t>(G0, 1) * ldw);
-        DevBuf<float> rew(std::max<int64_t>(G0, 1));
-        DevBuf<int32_t> len(std::max<int64_t>(G0, 1));
-        // play_episode(tr.model, 0f0): the current q_net (packed theta) as a one-model batch
+        DevBuf<float> W((size_t)(std::max<int64_t>(G0, 1) + 1) * ldw);
+        DevBuf<float> rew(std::max<int64_t>(G0, 1) + 1);
+        DevBuf<int32_t> len(std::max<int64_t>(G0, 1) + 1);
         float tr_reward = 0.0f;
-        {
-            EnvHold e;
-            ReplayHold r;
-            lap_rollout(m, m->theta_q, P, 1, rew, len, e, r);
-            SNK_HIP(hipMemcpy(&tr_reward, rew, sizeof(float), hipMemcpyDeviceToHost));
-        }
         int64_t n_better = 0;
         std::vector<float> hr;
         std::vector<int32_t> hl;
-        for (int64_t n0 = 0; n0 < n_models; n0 += G0) {
-            const int64_t G = std::min(G0, n_models - n0);
-            lap_build(h, m, seed, n0, G, W, ldw);
+        for (int64_t n0 = 0; n0 < std::max<int64_t>(n_models, 1); n0 += G0) {
+            const int64_t G = std::min(G0, n_models - n0);   // 0 when n_models = 0: the reference episode alone
+            const int64_t GR = n0 == 0 ? G + 1 : G;          // + tr.model's env in the first chunk
+            if (G > 0) lap_build(h, m, seed, n0, G, W, ldw);
+            if (n0 == 0)
+                SNK_HIP(hipMemcpyAsync(W + G * ldw, m->theta_q, P * sizeof(float), hipMemcpyDeviceToDevice, s));
             EnvHold e;
             ReplayHold r;
-            lap_rollout(m, W, ldw, G, rew, len, e, r);
-            hr.resize(G);
-            hl.resize(G);
-            SNK_HIP(hipMemcpy(hr.data(), rew, G * sizeof(float), hipMemcpyDeviceToHost));
-            SNK_HIP(hipMemcpy(hl.data(), len, G * sizeof(int32_t), hipMemcpyDeviceToHost));
+            lap_rollout(m, W, ldw, GR, rew, len, e, r);
+            hr.resize(GR);
+            hl.resize(GR);
+            SNK_HIP(hipMemcpy(hr.data(), rew, GR * sizeof(float), hipMemcpyDeviceToHost));
+            SNK_HIP(hipMemcpy(hl.data(), len, GR * sizeof(int32_t), hipMemcpyDeviceToHost));
+            if (n0 == 0) {
+                SNK_CHECK(hl[G] > 0, SNK_ERR_INTERNAL, "tr.model: episode did not end");
+                tr_reward = hr[G];
+            }
             std::vector<int64_t> slots;
             for (int64_t g = 0; g < G; ++g) {
                 SNK_CHECK(hl[g] > 0, SNK_ERR_INTERNAL, "model %lld: episode did not end", (long long)(n0 + g));
@@ -1122,7 +1146,7 @@ extern "C" int snk_laplace_sampling(snk_laplace h, snk_dqn m, snk_replay rb, int
                 if (lengths_host) lengths_host[n0 + g] = hl[g];
                 if (hr[g] > tr_reward) {   // la_utils.jl:108
                     ++n_better;
-                    for (int t = 0; t < hl[g]; ++t) slots.push_back((int64_t)t * G + g);
+                    for (int t = 0; t < hl[g]; ++t) slots.push_back((int64_t)t * GR + g);
                 }
             }
             if (!slots.empty()) {

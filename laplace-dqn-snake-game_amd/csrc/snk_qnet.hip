@@ -880,7 +880,8 @@ void qwork_free(QWork &w) {
     for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a2b, (void *)w.a1b, (void *)w.a3, (void *)w.slab, (void *)w.cslab,
                     (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.x0, (void *)w.target,
-                    (void *)w.loss, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e})
+                    (void *)w.loss, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e,
+                    (void *)w.w2h})
         dfree(p);
     w = QWork{};
 }
@@ -939,7 +940,9 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     w.q = dalloc<float>((size_t)cap * 3);
     w.wmax_part = dalloc<float>((size_t)std::max<int64_t>(cap, 256));
     w.w3h = dalloc<uint16_t>((size_t)36 * 512 * 8);
-    w.w3e = dalloc<int>(1);
+    w.w3e = dalloc<int>(2);
+    w.w2h = dalloc<uint16_t>((size_t)H3F_B2_CHUNKS * 8);
+    SNK_HIP(hipMemsetAsync(w.w2h, 0, (size_t)H3F_B2_CHUNKS * 16, stream()));   // pads stay zero
     if (tr) {
         w.has_train = 1;
         w.dq = dalloc<float>((size_t)cap * 3);
@@ -1089,7 +1092,8 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             }
             SNK_CHECK(!rd.out || (lo <= 2 && hi >= 1), SNK_ERR_INTERNAL, "sample rider without a launch");
             if (lo <= 2 && hi >= 1 && h3f_dma(L.bs)) {   // the conv3 weights pre-split once for every workgroup
-                w3_split_kernel<<<36 * 512 / 256, 256, 0, s>>>(img, w.wmax_part, w.wmax_n, w.w3h, w.w3e);
+                w3_split_kernel<<<W3S_BLOCKS + W2S_BLOCKS, 256, 0, s>>>(img, w.wmax_part, w.wmax_n, w.w3h, w.w3e,
+                                                                        n.wt + L.off_t2, w.w2h);
                 launch_check("w3_split_kernel");
             }
             if (lo <= 2 && hi >= 1) {
@@ -1097,6 +1101,7 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
                 if (h3f_dma(L.bs)) {
                     fa.w3h = w.w3h;
                     fa.w3e = w.w3e;
+                    fa.w2h = w.w2h;
                 }
                 fa.rider = rd;
                 fa.src = n.src; fa.w1 = n.th + L.off_w1; fa.b1 = n.th + L.off_b1;

@@ -74,6 +74,7 @@ struct QWork {
                                      //   last changed the image (the next full forward skips its scan; reset there)
     uint16_t *w3h = nullptr;         // h3 conv3 weights pre-split for conv_h3f_kernel's LDS-DMA staging:
     int *w3e = nullptr;              //   [36 kk][512 16-byte chunks] in the B buffers' swizzled order, and their exponent
+    uint16_t *w2h = nullptr;         //   (w3e[1]: conv2's) and conv2's weights pre-split into the B2 image bytes
     double *target = nullptr, *loss = nullptr;
     int has_train = 0;
     int64_t gen = 0;          // bumped on every reallocation (captured graphs hold the old pointers)

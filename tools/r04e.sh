@@ -1,0 +1,15 @@
+# round 4: act-forward / laplace parity, conv_h3f phase clocks, lap_act per-dispatch trace, headline bench + stats
+set -o pipefail
+OUT=gpurun_out/r04e; mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_laplace_gpu.py tests/test_qnet_gpu.py tests/test_configs3_gpu.py tests/test_configs_gpu.py tests/test_train_parity_gpu.py -m gpu > $OUT/t.log 2>&1; rc=$?
+tail -n 2 $OUT/t.log; [ $rc -eq 0 ] || exit 1
+SNK_LIB=$GRAFT_REPO_ROOT/laplace-dqn-snake-game_amd/libsnakehip_clk.so timeout -k 10 200 python tools/h3f_clocks.py > $OUT/h3f_clocks.json 2>&1 || exit 2
+tail -1 $OUT/h3f_clocks.json
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/lstrace -o run -- python tools/lap_sampling.py > $OUT/ls.txt 2>&1 || exit 3
+tail -1 $OUT/ls.txt
+timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-dbuild --no-configs2 --no-cpu-baseline > $OUT/b.json 2> $OUT/b.err || exit 4
+python -c "import json; d=json.load(open('$OUT/b.json')); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['reference_ratio']['updates_per_s'], d['configs3_per_rank']['value'])"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-dbuild --no-extras --no-configs2 --no-configs3 > $OUT/pb.json 2> $OUT/prof.err || exit 5
+python tools/kstats.py $OUT/prof > $OUT/kstats.txt; head -14 $OUT/kstats.txt
+echo done
