@@ -63,6 +63,26 @@ def _latest_traffic(kern: str, pattern: str = "*_conv3_traffic.json"):
     return None
 
 
+def _latest_pmc(kern: str, pattern: str):
+    """Counter summary (tools/pmc_summary.py over the separate counter-only passes of
+    tools/pmc_any.sh / pmc_syrk.sh) of the newest committed profiles/<pattern> whose kernel
+    name starts with kern: MFMA busy at the clock the chip held (GRBM_GUI_ACTIVE), that
+    clock, LDS bank-conflict share, for the roofline objects."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", pattern)), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k, v in d.items():
+            if k.startswith(kern) and "mfma_busy" in v:
+                return {"pmc_kernel": k.split("(")[0], "pmc_mfma_busy_nominal_clock": v.get("mfma_busy"),
+                        "pmc_clock_ghz": v.get("clock_ghz"), "pmc_mfma_busy_at_clock": v.get("mfma_busy_at_clock"),
+                        "pmc_lds_bank_conflict_frac": v.get("lds_conflict_frac"),
+                        "pmc_source": os.path.relpath(f, REPO)}
+    return {}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -414,6 +434,8 @@ def d_build_gram(args, snk, model, dist, rank, world) -> dict:
                                     "traffic": None, "half_mfma_tflops_executed": tf * H3_PRODUCTS,
                                     "mfma_utilization": tf * H3_PRODUCTS / PEAK_BF16_TFLOPS,
                                     "fp32_mfma_peak": PEAK_FP32_TFLOPS}}}
+    if n == 50000 and world == 1:
+        res["d_build"]["roofline"].update(_latest_pmc("syrk_h3q_kernel<0, 4, false>", "*_pmc_syrk.json"))
     tr_file = _latest_traffic("syrk_h3q_kernel", "*_syrk_traffic.json") if n == 50000 and world == 1 else None
     if tr_file:
         rf = res["d_build"]["roofline"]
@@ -634,7 +656,9 @@ def main():
                                         "counted against the MFMA peak" if fused else None,
                            "half_mfma_tflops_executed": tf * nprod if x6 else None,
                            "fp32_mfma_peak": PEAK_FP32_TFLOPS}
-        tr_file = _latest_traffic("conv_h3f_kernel" if fused else "conv_h3s_kernel" if h3 else "conv_x6")
+        if fused and n == 4096 and bs == 12:
+            out["roofline"].update(_latest_pmc(f"conv_h3f_kernel<{bs}, 8, {C}>", "*_pmc_h3f.json"))
+        tr_file = _latest_traffic(f"conv_h3f_kernel<{bs}, 8, {C}>" if fused else "conv_h3s_kernel" if h3 else "conv_x6")
         if tr_file:
             out["roofline"]["traffic"] = tr_file["bytes_per_launch"]
             out["roofline"]["traffic_source"] = tr_file["source"]
