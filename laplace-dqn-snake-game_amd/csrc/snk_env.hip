@@ -36,7 +36,10 @@
 
 namespace snk {
 
-constexpr int ENV_NE = 64, ENV_NT = 128;
+// envs per workgroup: 64, or 32 for batches up to ENV_NE_SMALL_MAX envs (4096 envs in 64
+// workgroups left 3/4 of the CUs idle on a latency-bound step; 128 workgroups finish sooner)
+constexpr int ENV_NE = 64, ENV_NT = 128, ENV_NE_SMALL = 32;
+constexpr int64_t ENV_NE_SMALL_MAX = 16384;
 // Profiling builds only (make clocks): per-workgroup phase timestamps (100 MHz realtime
 // counter) into a debug buffer, read back by snk_env_debug_clocks.
 #ifdef SNK_ENV_CLOCKS
@@ -132,23 +135,23 @@ __device__ __forceinline__ uint32_t pack16(const i32x4 v) {
 template <int PITCH>
 constexpr int env_waves_per_simd() { return PITCH > 304 ? 4 : 5; }   // the register budget of NPT pieces
 
-template <int PITCH>
+template <int PITCH, int NE = ENV_NE>
 __global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_kernel(EnvDev E, const uint8_t *__restrict__ act,
                                                              int act_mode, ReplayDev R, int store, EpisodeAcc acc,
                                                              int with_acc) {
-    constexpr int NCH = PITCH / 16, NPT = (ENV_NE * NCH + ENV_NT - 1) / ENV_NT;
-    __shared__ uint32_t sbp[ENV_NE * NCH];                              // packed boards
-    __shared__ __attribute__((aligned(8))) int16_t s_pc[ENV_NE * 4];   // patch cells (tail, head, food), -1 = none
-    __shared__ uint8_t s_flag[ENV_NE];                                  // bit0 stepped, bit1 reset
+    constexpr int NCH = PITCH / 16, NPT = (NE * NCH + ENV_NT - 1) / ENV_NT;
+    __shared__ uint32_t sbp[NE * NCH];                              // packed boards
+    __shared__ __attribute__((aligned(8))) int16_t s_pc[NE * 4];   // patch cells (tail, head, food), -1 = none
+    __shared__ uint8_t s_flag[NE];                                  // bit0 stepped, bit1 reset
     __shared__ int16_t s_food[64];
-    __shared__ float s_epr[ENV_NE];   // finished episodes: reward (NaN = not finished), score
-    __shared__ uint8_t s_score[ENV_NE];
+    __shared__ float s_epr[NE];   // finished episodes: reward (NaN = not finished), score
+    __shared__ uint8_t s_score[NE];
     ENV_CLK(0);
     const int tid = threadIdx.x;
     const bool w0 = tid < 64;
     const int lane = tid & 63;
-    const int64_t e0 = (int64_t)blockIdx.x * ENV_NE;
-    const int ne = (int)min((int64_t)ENV_NE, E.n - e0);
+    const int64_t e0 = (int64_t)blockIdx.x * NE;
+    const int ne = (int)min((int64_t)NE, E.n - e0);
     const int64_t t = E.ctl->t;
     const int cur = (int)(t % 3), nxt = (int)((t + 1) % 3), prv = (int)((t + 2) % 3);
     const int64_t rc = store ? *R.count : 0;
@@ -517,10 +520,17 @@ void env_launch_step(const EnvDev &E, const uint8_t *act, int act_mode, const Re
     EpisodeAcc ea{};
     if (acc) ea = *acc;
     const int wa = acc ? 1 : 0;
-    const int grid = ceil_div(E.n, ENV_NE);
+    const bool small = E.n <= ENV_NE_SMALL_MAX && E.pitch <= 256;
+    const int grid = (int)ceil_div(E.n, small ? ENV_NE_SMALL : ENV_NE);
     const int store = R ? 1 : 0;
-#define SNK_ENV_CASE(P) \
-    case P: env_step_kernel<P><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, store, ea, wa); break;
+#define SNK_ENV_CASE(P)                                                                                      \
+    case P:                                                                                                  \
+        if (P <= 256 && small)                                                                               \
+            env_step_kernel<P, (P <= 256 ? ENV_NE_SMALL : ENV_NE)><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, \
+                                                                                      store, ea, wa);        \
+        else                                                                                                 \
+            env_step_kernel<P, ENV_NE><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, store, ea, wa);        \
+        break;
     switch (E.pitch) {
         SNK_ENV_CASE(48) SNK_ENV_CASE(64) SNK_ENV_CASE(96) SNK_ENV_CASE(112) SNK_ENV_CASE(128)
         SNK_ENV_CASE(144) SNK_ENV_CASE(176) SNK_ENV_CASE(208) SNK_ENV_CASE(240) SNK_ENV_CASE(256)
@@ -600,7 +610,7 @@ extern "C" int snk_env_create(snk_env *out, int64_t n, int32_t bs, int32_t C, ui
         d.fault_count = dalloc<uint32_t>(1);
         d.ctl = dalloc<Ctl>(1);
         d.ticket = dalloc<uint32_t>(9 * 32);
-        d.part = dalloc<uint64_t>((size_t)ceil_div(n, ENV_NE) * 4);
+        d.part = dalloc<uint64_t>((size_t)ceil_div(n, ENV_NE_SMALL) * 4);
         SNK_HIP(hipMemsetAsync(d.ticket, 0, 9 * 32 * sizeof(uint32_t), s));
         h->scratch = dalloc<uint8_t>(n);
         h->gather = dalloc<int8_t>((size_t)n * C * d.ring_cap);
