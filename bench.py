@@ -45,6 +45,16 @@ def act_forward_flop(n: int, bs: int, C: int) -> float:
     return 2.0 * n * (bs * bs * 16 * 9 * C + bs * bs * 32 * 144 + wo * wo * 64 * 1152)
 
 
+def update_flop(B: int, bs: int, C: int) -> float:
+    """Algorithmic FLOP of one B-sample DQN update (BASELINE.md's DQN-update row,
+    4 B F): forward of q_net and of t_net over the batch (2 F each sample) and
+    the backward of q_net (2 F: dX and dW). F = the fused conv stack + Dense
+    3136->256 + Dense 256->3 of one state."""
+    wo = bs - 5
+    f = act_forward_flop(1, bs, C) + 2.0 * (wo * wo * 64 * 256 + 256 * 3)
+    return 4.0 * B * f
+
+
 def _latest_traffic(kern: str, pattern: str = "*_conv3_traffic.json"):
     """HBM bytes per launch of a dominant kernel from the newest committed PMC pass
     (profiles/*_conv3_traffic.json for the act forward, *_syrk_traffic.json for the
@@ -689,8 +699,15 @@ def main():
         eps_rate = st["episodes"] / max(1, st["env_steps"])
         try:
             out["reference_ratio"] = reference_ratio(args, snk, graph, eps_rate)
-            out["reference_ratio"]["ms_per_update_marginal"] = (
-                (out["reference_ratio"]["ms_per_step"] - out["ms_per_step"]) / (out["reference_ratio"]["updates_per_step"] - 1))
+            rr = out["reference_ratio"]
+            rr["ms_per_update_marginal"] = (rr["ms_per_step"] - out["ms_per_step"]) / (rr["updates_per_step"] - 1)
+            ufl = update_flop(64, bs, C)
+            utf = ufl / (rr["ms_per_update_marginal"] * 1e-3) / 1e12 if rr["ms_per_update_marginal"] > 0 else 0.0
+            rr["update_roofline"] = {"bound": "mfma", "flop_per_update": ufl, "achieved": utf,
+                                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s (fp32)",
+                                     "frac": utf / PEAK_FP32_TFLOPS,
+                                     "note": "4 B F (B = 64) over the marginal update time; the update is a "
+                                             "chain of 7 dependent launches, latency-bound at B = 64"}
         except Exception as e:   # report, do not fail the headline line
             out["reference_ratio"] = {"error": str(e)}
         out["updates_per_s"] = args.updates_per_iter * args.steps / elapsed

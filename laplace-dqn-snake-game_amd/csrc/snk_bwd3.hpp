@@ -28,6 +28,19 @@
 
 namespace snk {
 
+// Profiling builds only (make clocks): per-workgroup phase stamps of conv3_bwd_kernel,
+// read back by snk_c3b_debug_clocks (slots: start, operands staged, MFMA done,
+// epilogue done, end; slot 6 = 1 + XCC_ID, slot 7 = 1 + the HW_ID word)
+#ifdef SNK_ENV_CLOCKS
+__device__ uint64_t *g_c3b_clk;
+#define C3B_CLK(slot)                                                                                 \
+    do {                                                                                              \
+        if (threadIdx.x == 0 && g_c3b_clk) g_c3b_clk[(int64_t)blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define C3B_CLK(slot) do { } while (0)
+#endif
+
 struct Conv3BwdArgs {
     const float *a2;    // [S][bs*bs][32]  conv2 output (relu'd)
     const float *dz3;   // [S][wo*wo][64]  gradient at conv3's pre-activation
@@ -99,6 +112,7 @@ __device__ __forceinline__ void c3_dw_block(const Conv3BwdArgs &a, int z, int gr
     c3_copy<8>(reinterpret_cast<f32x4 *>(D), reinterpret_cast<const f32x4 *>(a.dz3 + (int64_t)s0 * wo2 * 64),
                ns * wo2 * 16);
     __syncthreads();
+    C3B_CLK(1);
     const int r = lane & 31, h = lane >> 5;
     const int kk = grp * 4 + wave;
     const int dv = kk / 6, du = kk - dv * 6;
@@ -120,6 +134,7 @@ __device__ __forceinline__ void c3_dw_block(const Conv3BwdArgs &a, int z, int gr
             acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv ? x : 0.0f, y1, acc[1], 0, 0, 0);
         }
     }
+    C3B_CLK(2);
     float *out = a.slab + (int64_t)z * 1153 * 64;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -164,6 +179,7 @@ __device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg
     c3_copy_rows<4>(Dz, a.dz3 + (int64_t)s * wo2 * 64, wo2, [](int row) { return row; });
     c3_copy_rows<9>(Wl, a.w, NN, [cg](int n) { return (n / C3_CG) * 32 + cg * C3_CG + n % C3_CG; });
     __syncthreads();
+    C3B_CLK(1);
     // T in 16x16 tiles (v_mfma_f32_16x16x4_f32: lane l holds A[l&15][k + (l>>4)],
     // B[k + (l>>4)][l&15]; C rows 4*(l>>4) + e, column l&15), round robin over the waves
     // (all tiles kept in registers, then written over the operands after a barrier)
@@ -184,6 +200,7 @@ __device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg
         }
     }
     __syncthreads();
+    C3B_CLK(2);
 #pragma unroll
     for (int u = 0; u < MT; ++u) {
         const int t = wave + 4 * u;
@@ -197,6 +214,7 @@ __device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg
         }
     }
     __syncthreads();
+    C3B_CLK(3);
     // col2im + relu mask, (pin, ci) per thread: the 36 terms load together (out-of-grid
     // terms read a valid slot and add 0), summed kk ascending
 #pragma unroll
@@ -225,6 +243,13 @@ __device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg
 __global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float c3sm[];
     const int b = blockIdx.x;
+    C3B_CLK(0);
+#ifdef SNK_ENV_CLOCKS
+    if (threadIdx.x == 0 && g_c3b_clk) {
+        g_c3b_clk[(int64_t)b * 8 + 7] = 1 + (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_c3b_clk[(int64_t)b * 8 + 6] = 1 + (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));
+    }
+#endif
     if (b < a.nW) {
         switch (a.wo) {
             case 3: c3_dw_block<3>(a, b / 9, b % 9, c3sm); break;
@@ -236,6 +261,7 @@ __global__ __launch_bounds__(256) void conv3_bwd_kernel(Conv3BwdArgs a) {
         }
     } else
         c3_dx_block(a, (b - a.nW) / (32 / C3_CG), (b - a.nW) % (32 / C3_CG), c3sm);
+    C3B_CLK(4);
 }
 
 // ---------------------------------------------------------------- conv2 (3x3, pad 1, 16 -> 32)

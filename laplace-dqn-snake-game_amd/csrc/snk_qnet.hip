@@ -1990,6 +1990,25 @@ extern "C" int snk_upd_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t ar
         SNK_HIP(hipMemcpy(out_host, buf, n_wg * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     });
 }
+// out[wg][8] = conv3_bwd_kernel phase stamps of the LAST launch
+extern "C" int snk_c3b_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t arm) {
+    return guard([&] {
+        static uint64_t *buf = nullptr;
+        static int64_t cap = 0;
+        if (arm) {
+            if (n_wg > cap) {
+                dfree(buf);
+                buf = dalloc<uint64_t>(n_wg * 8);
+                cap = n_wg;
+            }
+            SNK_HIP(hipMemset(buf, 0, n_wg * 8 * sizeof(uint64_t)));
+            SNK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_c3b_clk), &buf, sizeof(buf)));
+            return;
+        }
+        SNK_HIP(hipDeviceSynchronize());
+        SNK_HIP(hipMemcpy(out_host, buf, n_wg * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    });
+}
 // out[wg][8] = conv_h3f_kernel phase stamps of the LAST launch
 extern "C" int snk_h3f_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t arm) {
     return guard([&] {
