@@ -1399,8 +1399,8 @@ static bool c3bwd_ok(const QLayout &L, int64_t S) {
 }
 
 // conv2's backward on conv2_bwd_kernel (snk_bwd3.hpp); larger boards: the generic pair
-static bool c2bwd_ok(const QLayout &L, int64_t S) {
-    return S <= (1 << 20) && (size_t)c2_bwd_lds_floats(L.bs) * sizeof(float) <= 160 * 1024;
+static bool c2bwd_ok(const QLayout &L, int64_t S) {   // the dX image pitch C2X_PJ holds bs + 2 <= 20
+    return S <= (1 << 20) && L.bs + 2 <= C2X_PJ && (size_t)c2_bwd_lds_floats(L.bs) * sizeof(float) <= 160 * 1024;
 }
 
 static BwdPlan bwd_plan(const QLayout &L, int64_t S) {
@@ -1519,8 +1519,19 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
             float *c3d = dst(1, p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
             const Conv3BwdArgs ca{w.a2, w.dz3, th + L.off_w3, c3d, w.dz2, (int)S, bs, L.Wo, C3_NSC, p.c3.z, p.c3.z * 9};
             const size_t lds = (size_t)std::max(c3_dw_lds_floats(bs, L.Wo, C3_NSC), c3_dx_lds_floats(L.Wo)) * 4;
-            set_lds_limit((const void *)conv3_bwd_kernel, lds);
-            conv3_bwd_kernel<<<(unsigned)(ca.nW + S * (32 / C3_CG)), 256, lds, s>>>(ca);
+            const unsigned nb = (unsigned)(ca.nW + S * (32 / C3_CG));
+            auto go = [&](auto kern) {
+                set_lds_limit((const void *)kern, lds);
+                kern<<<nb, 256, lds, s>>>(ca);
+            };
+            switch (L.Wo) {
+                case 3: go(conv3_bwd_kernel<3>); break;
+                case 4: go(conv3_bwd_kernel<4>); break;
+                case 5: go(conv3_bwd_kernel<5>); break;
+                case 6: go(conv3_bwd_kernel<6>); break;
+                case 7: go(conv3_bwd_kernel<7>); break;
+                default: go(conv3_bwd_kernel<8>); break;
+            }
             launch_check("conv3_bwd_kernel");
             fin(p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
         } else {
@@ -2003,6 +2014,25 @@ extern "C" int snk_c3b_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t ar
             }
             SNK_HIP(hipMemset(buf, 0, n_wg * 8 * sizeof(uint64_t)));
             SNK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_c3b_clk), &buf, sizeof(buf)));
+            return;
+        }
+        SNK_HIP(hipDeviceSynchronize());
+        SNK_HIP(hipMemcpy(out_host, buf, n_wg * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    });
+}
+// out[wg][8] = conv2_bwd_kernel phase stamps of the LAST launch
+extern "C" int snk_c2b_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t arm) {
+    return guard([&] {
+        static uint64_t *buf = nullptr;
+        static int64_t cap = 0;
+        if (arm) {
+            if (n_wg > cap) {
+                dfree(buf);
+                buf = dalloc<uint64_t>(n_wg * 8);
+                cap = n_wg;
+            }
+            SNK_HIP(hipMemset(buf, 0, n_wg * 8 * sizeof(uint64_t)));
+            SNK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_c2b_clk), &buf, sizeof(buf)));
             return;
         }
         SNK_HIP(hipDeviceSynchronize());

@@ -1,4 +1,4 @@
-"""Phase clocks of conv3's backward (profiling build: make -C .../csrc clocks).
+"""Phase clocks of conv3's and conv2's backward (profiling build: make -C .../csrc clocks).
 usage: SNK_LIB=<repo>/laplace-dqn-snake-game_amd/libsnakehip_clk.so python tools/c3b_clocks.py
 Runs a 4096-env trainer (B = 64 updates), arms the clocks, runs one more
 iteration and prints per-phase medians (us) of the weight-gradient and the
@@ -22,11 +22,16 @@ tr.run(4, learn=True, graph=False)
 B, wo = 64, 7
 nW = (B + 1) // 2 * 9
 nwg = nW + B * 8
-lib.snk_c3b_debug_clocks.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32]
+nwg2 = B + 2 * B
+for f in (lib.snk_c3b_debug_clocks, lib.snk_c2b_debug_clocks):
+    f.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32]
 assert lib.snk_c3b_debug_clocks(nwg, None, 1) == 0
+assert lib.snk_c2b_debug_clocks(nwg2, None, 1) == 0
 tr.run(1, learn=True, graph=False)
 buf = np.zeros((nwg, 8), np.uint64)
 assert lib.snk_c3b_debug_clocks(nwg, buf.ctypes.data, 0) == 0
+buf2 = np.zeros((nwg2, 8), np.uint64)
+assert lib.snk_c2b_debug_clocks(nwg2, buf2.ctypes.data, 0) == 0
 c = buf[:, :5].astype(np.float64) / 100.0
 t0 = c[:, 0].min()
 out = {"grid_end_us": float(c[:, 4].max() - t0), "n_wg": nwg}
@@ -62,4 +67,13 @@ for _, dlt, k in ev:
     cur[k] += dlt
     peak = max(peak, cur[k])
 out["max_resident_per_cu"] = peak
+c2 = buf2[:, :5].astype(np.float64) / 100.0
+t2 = c2[:, 0].min()
+c2o = {"grid_end_us": float(c2[:, 4].max() - t2)}
+for name, sl in (("dW", slice(0, B)), ("dX", slice(B, nwg2))):
+    cc = c2[sl]
+    c2o[name] = {"start_offset": stats(cc[:, 0] - t2), "lifetime": stats(cc[:, 4] - cc[:, 0]),
+                 "stage": stats(cc[:, 1] - cc[:, 0]), "mfma": stats(cc[:, 2] - cc[:, 1]),
+                 "epilogue": stats(cc[:, 4] - cc[:, 2])}
+out["conv2_bwd"] = c2o
 print(json.dumps(out, indent=1))
