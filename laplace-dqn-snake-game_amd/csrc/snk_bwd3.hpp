@@ -6,7 +6,7 @@
 // HOUT^2 = bs^2 input positions, 4/5 of whose 36 kernel offsets fall outside
 // the Wo x Wo gradient (1.36 GFLOP of MFMA work for 0.34 useful, plus a
 // partial-slab reduce). Both are reorganised around LDS-staged samples, in
-// one launch (blocks [0, nW) weight gradient, the rest data gradient):
+// one launch (blocks [0, S * 8) data gradient, the rest weight gradient):
 //
 //  * dW (grid: Z chunks of 2 samples x 9 groups of four kernel offsets, exact-fp32
 //    v_mfma_f32_32x32x2_f32):
@@ -314,10 +314,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WO >= 8 ? 2
         g_c3b_clk[(int64_t)b * 8 + 6] = 1 + (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));
     }
 #endif
-    if (b < a.nW)
-        c3_dw_block<WO>(a, b / 9, b % 9, c3sm);
+    const int nX = a.S * (32 / C3_CG);   // data-gradient blocks first: they wait on more staging
+    if (b < nX)
+        c3_dx_block<WO>(a, b / (32 / C3_CG), b % (32 / C3_CG), c3sm);
     else
-        c3_dx_block<WO>(a, (b - a.nW) / (32 / C3_CG), (b - a.nW) % (32 / C3_CG), c3sm);
+        c3_dw_block<WO>(a, (b - nX) / 9, (b - nX) % 9, c3sm);
     C3B_CLK(4);
 }
 
@@ -369,42 +370,45 @@ __device__ __forceinline__ void c2_dw_block(const Conv2BwdArgs &a, int s, float 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int bs = a.bs, bp = bs + 2, bs2 = bs * bs, bp2 = bp * bp;
     float *A1 = sm, *D2 = sm + bp2 * 16;
-    for (int e = tid; e < bp2 * 4; e += 256) reinterpret_cast<f32x4 *>(A1)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-    __syncthreads();
-    {
-        constexpr int U = 8;   // loads in flight per thread
-        const f32x4 *src = reinterpret_cast<const f32x4 *>(a.a1 + (int64_t)s * bs2 * 16);
-        for (int b = 0; b < bs2 * 4; b += U * 256) {
-            f32x4 v[U];
+    // a1[s] (4 float4 per position) and dz2[s] (8 per position) into registers first (boards up
+    // to 13 x 13; larger ones load the rest after), then the zero border ring of A1 and the
+    // scatter: border and interior are disjoint, so one barrier orders everything
+    constexpr int NA = 3, ND = 6;
+    const f32x4 *src = reinterpret_cast<const f32x4 *>(a.a1 + (int64_t)s * bs2 * 16);
+    const f32x4 *srd = reinterpret_cast<const f32x4 *>(a.dz2 + (int64_t)s * bs2 * 32);
+    f32x4 av[NA], dv[ND];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = b + u * 256 + tid;
-                v[u] = src[e < bs2 * 4 ? e : 0];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = b + u * 256 + tid;
-                if (e < bs2 * 4) {
-                    const int p = e >> 2, j = p / bs, i = p - j * bs;
-                    reinterpret_cast<f32x4 *>(A1 + ((i + 1) + (j + 1) * bp) * 16)[e & 3] = v[u];
-                }
-            }
-        }
-        const f32x4 *srd = reinterpret_cast<const f32x4 *>(a.dz2 + (int64_t)s * bs2 * 32);
-        for (int b = 0; b < bs2 * 8; b += U * 256) {
-            f32x4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = b + u * 256 + tid;
-                v[u] = srd[e < bs2 * 8 ? e : 0];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = b + u * 256 + tid;
-                if (e < bs2 * 8) reinterpret_cast<f32x4 *>(D2 + (e >> 3) * C2_DS)[e & 7] = v[u];
-            }
-        }
+    for (int u = 0; u < NA; ++u) {
+        const int e = u * 256 + tid;
+        av[u] = src[e < bs2 * 4 ? e : 0];
     }
+#pragma unroll
+    for (int u = 0; u < ND; ++u) {
+        const int e = u * 256 + tid;
+        dv[u] = srd[e < bs2 * 8 ? e : 0];
+    }
+    for (int e = tid; e < 4 * (bs + 1) * 4; e += 256) {
+        const int c = e & 3, q = e >> 2, side = q / (bs + 1), k = q - side * (bs + 1);
+        const int pi = side == 0 ? k : side == 1 ? bs + 1 : side == 2 ? k + 1 : 0;
+        const int pj = side == 0 ? 0 : side == 1 ? k : side == 2 ? bs + 1 : k + 1;
+        reinterpret_cast<f32x4 *>(A1 + (pi + pj * bp) * 16)[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto put_a = [&](int e, const f32x4 &v) {
+        const int p = e >> 2, j = p / bs, i = p - j * bs;
+        reinterpret_cast<f32x4 *>(A1 + ((i + 1) + (j + 1) * bp) * 16)[e & 3] = v;
+    };
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+        const int e = u * 256 + tid;
+        if (e < bs2 * 4) put_a(e, av[u]);
+    }
+    for (int e = NA * 256 + tid; e < bs2 * 4; e += 256) put_a(e, src[e]);
+#pragma unroll
+    for (int u = 0; u < ND; ++u) {
+        const int e = u * 256 + tid;
+        if (e < bs2 * 8) reinterpret_cast<f32x4 *>(D2 + (e >> 3) * C2_DS)[e & 7] = dv[u];
+    }
+    for (int e = ND * 256 + tid; e < bs2 * 8; e += 256) reinterpret_cast<f32x4 *>(D2 + (e >> 3) * C2_DS)[e & 7] = srd[e];
     __syncthreads();
     C2B_CLK(1);
     // wave w: output positions [w*q, w*q + q) (q = bs^2/4 rounded up to 4) for all
@@ -514,6 +518,19 @@ __device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb
 #pragma unroll
     for (int u = 0; u < 5; ++u)
         mw = fmaxf(mw, fmaxf(fmaxf(fabsf(wv[u][0]), fabsf(wv[u][1])), fmaxf(fabsf(wv[u][2]), fabsf(wv[u][3]))));
+    // the relu mask a1 of this wave's first two tiles' outputs (tile t = xb + C2_NXB*wave + 8u:
+    // position (4 bi + e, 4 bj + g), channel r), loaded before the barriers
+    float mk1[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int nbm = (bs + 3) >> 2, t = xb + C2_NXB * wave + 4 * C2_NXB * u;
+        const int bi = t % nbm, bj = t / nbm, oj = min(4 * bj + (lane >> 4), bs - 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int oi = min(4 * bi + e, bs - 1);
+            mk1[u][e] = t < nbm * nbm ? a.a1[((int64_t)s * bs2 + oi + oj * bs) * 16 + (lane & 15)] : 0.0f;
+        }
+    }
     md = wave_max(md);
     mw = wave_max(mw);
     if (lane == 0) {
@@ -567,7 +584,7 @@ __device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb
     // (9C of them, then the bias row of ones, then zeros)
     f32x4m c1acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int nrow = 9 * a.C;
-    for (int t = xb + C2_NXB * wave; t < nt; t += 4 * C2_NXB) {
+    for (int t = xb + C2_NXB * wave, u = 0; t < nt; t += 4 * C2_NXB, ++u) {
         // tile t = 4x4 positions (i, j) = (4 bi + (r & 3), 4 bj + (r >> 2)); A rows = positions
         const int bi = t % nb, bj = t / nb;
         const int i = min(4 * bi + (r & 3), bs - 1), j = min(4 * bj + (r >> 2), bs - 1);
@@ -596,7 +613,8 @@ __device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb
             dzm[e] = 0.0f;
             if (oi < bs && oj < bs) {
                 const int64_t o = ((int64_t)s * bs2 + oi + oj * bs) * 16 + r;
-                dzm[e] = a.a1[o] > 0.0f ? acc[e] * sc : 0.0f;
+                const float m1 = u == 0 ? mk1[0][e] : u == 1 ? mk1[1][e] : a.a1[o];
+                dzm[e] = m1 > 0.0f ? acc[e] * sc : 0.0f;
                 a.dzc1[o] = dzm[e];
             }
         }

@@ -41,8 +41,9 @@ def stats(v):
     return {"median": float(np.median(v)), "max": float(v.max()), "min": float(v.min())}
 
 
-for name, sl, phases in (("dW", slice(0, nW), ("stage", "mfma", "store")),
-                         ("dX", slice(nW, nwg), ("stage", "mfma", "t_store", "col2im"))):
+nX = B * 8   # data-gradient blocks come first in the grid
+for name, sl, phases in (("dW", slice(nX, nwg), ("stage", "mfma", "store")),
+                         ("dX", slice(0, nX), ("stage", "mfma", "t_store", "col2im"))):
     cc = c[sl]
     d = {"start_offset": stats(cc[:, 0] - t0), "lifetime": stats(cc[:, 4] - cc[:, 0]),
          "end": stats(cc[:, 4] - t0)}
