@@ -1613,7 +1613,9 @@ struct UpdArgs {
 // the finished gradient of the four packed parameters i0 .. i0+3 (i0 % 4 == 0, all in one
 // section): the sum of their K-split slabs (z ascending, float4 slab loads, sixteen in
 // flight per batch) or the value already there
-__device__ __forceinline__ f32x4 finish4(const UpdArgs &a, int64_t i0) {
+// (part / nparts: only slabs [zc * part / nparts, zc * (part + 1) / nparts), for blocks that
+// split a parameter's slab run over several threads)
+__device__ __forceinline__ f32x4 finish4(const UpdArgs &a, int64_t i0, int part = 0, int nparts = 1) {
     f32x4 g = *reinterpret_cast<const f32x4 *>(a.grad + i0);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1621,9 +1623,9 @@ __device__ __forceinline__ f32x4 finish4(const UpdArgs &a, int64_t i0) {
         if (a.g.z[k] > 1 && j >= 0 && j < a.g.n[k]) {
             const float *sl = a.g.slab[k] + j;
             const int64_t n = a.g.n[k];
-            const int zc = a.g.z[k];
+            const int zc = a.g.z[k] * (part + 1) / nparts;
             f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-            int z = 0;
+            int z = a.g.z[k] * part / nparts;
             for (; z + 16 <= zc; z += 16) {
                 f32x4 x[16];
 #pragma unroll
@@ -1647,10 +1649,11 @@ __device__ __forceinline__ f32x4 finish4(const UpdArgs &a, int64_t i0) {
 }
 
 // RMSProp of one parameter (rmsprop_kernel order); returns the new theta
-__device__ __forceinline__ float rms_one(const UpdArgs &a, int64_t i, float g, bool due, float omr) {
-    const float qd = a.u.rho * a.u.acc[i] + omr * (g * g);
+__device__ __forceinline__ float rms_one(const UpdArgs &a, int64_t i, float g, bool due, float omr, float acc0,
+                                        float th0) {   // acc0 / th0: acc[i] and theta[i], loaded by the caller
+    const float qd = a.u.rho * acc0 + omr * (g * g);
     a.u.acc[i] = qd;
-    const float th = a.u.theta[i] - (g * a.u.lr) / (__builtin_sqrtf(qd) + a.u.eps);
+    const float th = th0 - (g * a.u.lr) / (__builtin_sqrtf(qd) + a.u.eps);
     a.u.theta[i] = th;
     if (due) a.u.theta_t[i] = th;
     return th;
@@ -1682,18 +1685,41 @@ __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb,
     const int CN = S.CN, n_el = GU_ROWS * CN;
     const int64_t p0 = S.off + ((int64_t)kk * S.CK + cb * GU_ROWS) * CN;   // a multiple of 4
     float m = 0.0f;
+    // sections of 128 float4 per block (conv2: 16 x 32) with the finish to do: two threads per
+    // float4, each over half of the slab run (conv2's 64 per-sample slabs: two batches of 16
+    // loads per thread instead of four), the halves added in order through LDS
+    const bool split = a.finish && n_el == 512;
+    f32x4 g2 = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (split) {
+        __shared__ f32x4 part[128];
+        const int grp = threadIdx.x & 127, hf = threadIdx.x >> 7;
+        const f32x4 pv = finish4(a, p0 + 4 * grp, hf, 2);
+        if (hf) part[grp] = pv;
+        __syncthreads();
+        if (!hf) {
+            g2 = pv + part[grp];
+            *reinterpret_cast<f32x4 *>(a.grad + p0 + 4 * grp) = g2;
+        }
+    }
     for (int e = 4 * threadIdx.x; e < n_el; e += 4 * 256) {
         const int64_t i = p0 + e;
+        // the optimizer state first: issued with (or before) the slab loads instead of after
+        // the gradient store, which the compiler must assume aliases them
+        f32x4 ac = {0.f, 0.f, 0.f, 0.f}, th = {0.f, 0.f, 0.f, 0.f};
+        if (a.apply) {
+            ac = *reinterpret_cast<const f32x4 *>(a.u.acc + i);
+            th = *reinterpret_cast<const f32x4 *>(a.u.theta + i);
+        }
         f32x4 g;
-        if (a.finish) {
+        if (split) {
+            g = g2;
+        } else if (a.finish) {
             g = finish4(a, i);
             *reinterpret_cast<f32x4 *>(a.grad + i) = g;
         } else {
             g = *reinterpret_cast<const f32x4 *>(a.grad + i);
         }
         if (!a.apply) continue;
-        const f32x4 ac = *reinterpret_cast<const f32x4 *>(a.u.acc + i);
-        const f32x4 th = *reinterpret_cast<const f32x4 *>(a.u.theta + i);
         f32x4 qd, tn;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {   // rms_one's arithmetic, component by component
@@ -1742,7 +1768,20 @@ __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb,
 // the LAST block owns Dense2 (195 params): it stages dq and h1 through LDS and reduces
 // over the batch (d2_grad_kernel's order)
 constexpr int GU_OTHER = 16;
+// Profiling builds only (make clocks): grad_update_kernel stamps per block (0 start, 1 work
+// done; the last block: 2 all arrived, 3 post-update done, 1 rewritten after the next draw),
+// read back by snk_gu_debug_clocks
+#ifdef SNK_ENV_CLOCKS
+__device__ uint64_t *g_gu_clk;
+#define GU_CLK(slot)                                                                                  \
+    do {                                                                                              \
+        if (threadIdx.x == 0 && g_gu_clk) g_gu_clk[(int64_t)blockIdx.x * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define GU_CLK(slot) do { } while (0)
+#endif
 __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
+    GU_CLK(0);
     const QLayout &L = a.L;
     const bool due = a.apply && a.u.counter && (*a.u.counter % a.u.rate) == 0;   // utils.jl:469-472
     const float omr = 1.0f - a.u.rho;
@@ -1771,7 +1810,8 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
         } else if (t < 195) {
             g = a.grad[i];
         }
-        if (a.apply && t < 195) rms_one(a, i, g, due, omr);
+        if (a.apply && t < 195) rms_one(a, i, g, due, omr, a.u.acc[i], a.u.theta[i]);
+        if (a.has_post) post_loss_block(a.post);   // off the tail: the loss mean needs no other block
     } else if (b < nimg) {
         const int sec = b < nb2 ? 0 : b < nb2 + nb3 ? 1 : 2;
         const int bl = b - (sec == 0 ? 0 : sec == 1 ? nb2 : nb2 + nb3);
@@ -1794,6 +1834,7 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
                             : e < r0 + r1 + r2 ? L.off_b3 + (e - r0 - r1)
                                                : L.off_d1b + (e - r0 - r1 - r2);
             float g = a.grad[i];
+            const float acc0 = a.apply && sub == 0 ? a.u.acc[i] : 0.0f, th0 = a.apply && sub == 0 ? a.u.theta[i] : 0.0f;
             if (a.finish) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -1818,9 +1859,10 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
                 }
                 if (sub == 0) a.grad[i] = g;
             }
-            if (a.apply && sub == 0) rms_one(a, i, g, due, omr);
+            if (a.apply && sub == 0) rms_one(a, i, g, due, omr, acc0, th0);
         }
     }
+    GU_CLK(1);
     // every block read *counter (nb) above; the last to arrive advances it. The bookkeeping
     // reads nothing another block of this launch wrote, so the ticket needs no fence.
     // Arrivals are counted in 8 shards (blockIdx % 8); the last of a shard adds to the top
@@ -1842,8 +1884,10 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
     }
     __syncthreads();
     if (!s_last) return;
-    post_update_block(a.post);
+    GU_CLK(2);
+    post_count_block(a.post);
     if (threadIdx.x == 0) __hip_atomic_store(a.post.ticket + 8 * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    GU_CLK(3);
     if (!a.post.next.out) return;
     __shared__ int64_t s_draw;
     if (threadIdx.x == 0) s_draw = *a.post.updates;   // this thread's own store above
@@ -1854,6 +1898,9 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
         r.draw = (uint64_t)s_draw;
         sample_wave(r);
     }
+#ifdef SNK_ENV_CLOCKS
+    if (threadIdx.x == 0 && g_gu_clk) g_gu_clk[(int64_t)blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
@@ -1999,6 +2046,25 @@ extern "C" int snk_upd_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t ar
         }
         SNK_HIP(hipDeviceSynchronize());
         SNK_HIP(hipMemcpy(out_host, buf, n_wg * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    });
+}
+// out[wg][4] = grad_update_kernel stamps of the LAST launch
+extern "C" int snk_gu_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t arm) {
+    return guard([&] {
+        static uint64_t *buf = nullptr;
+        static int64_t cap = 0;
+        if (arm) {
+            if (n_wg > cap) {
+                dfree(buf);
+                buf = dalloc<uint64_t>(n_wg * 4);
+                cap = n_wg;
+            }
+            SNK_HIP(hipMemset(buf, 0, n_wg * 4 * sizeof(uint64_t)));
+            SNK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_gu_clk), &buf, sizeof(buf)));
+            return;
+        }
+        SNK_HIP(hipDeviceSynchronize());
+        SNK_HIP(hipMemcpy(out_host, buf, n_wg * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     });
 }
 // out[wg][8] = conv3_bwd_kernel phase stamps of the LAST launch

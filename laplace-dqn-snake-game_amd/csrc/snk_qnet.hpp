@@ -187,10 +187,14 @@ struct PostUpdate {
     SampleRider next;      // out != nullptr: the last block also draws the NEXT update's batch
                            // (draw = the advanced update count; one launch fewer per update)
 };
-// tr.losses / epsilon decay / nb += 1 after an update (utils.jl:456-481), the Huber
-// mean over the batch in a fixed order (256-thread strided sums, then a tree)
-__device__ inline void post_update_block(const PostUpdate &p) {   // 256 threads
+// tr.losses (utils.jl:404-406, 456-466): the Huber mean over the batch in a fixed order
+// (256-thread strided sums, then a tree) -> loss_out, last_loss, log[updates % cap]. Reads
+// only what the update's earlier launches wrote and *updates, which nothing but the
+// bookkeeping below advances, so any block of the update pass may run it
+__device__ inline void post_loss_block(const PostUpdate &p) {   // 256 threads
     __shared__ double sh[256];
+    int64_t upd = 0;
+    if (threadIdx.x == 0 && p.log) upd = *p.updates;
     double v = 0.0;
     for (int64_t i = threadIdx.x; i < p.B; i += 256) v += p.loss[i];
     sh[threadIdx.x] = v;
@@ -203,10 +207,21 @@ __device__ inline void post_update_block(const PostUpdate &p) {   // 256 threads
     const double l = sh[0] / (double)p.B;
     *p.loss_out = l;
     *p.last_loss = l;
-    if (p.log) p.log[*p.updates % p.log_cap] = l;      // track_loss! (utils.jl:404-406)
-    *p.epsilon = fmaxf(*p.epsilon - p.decay, p.eps_end);  // utils.jl:480
-    *p.updates += 1;
-    *p.nb += 1;
+    if (p.log) p.log[upd % p.log_cap] = l;
+}
+// epsilon decay and the update counters (utils.jl:469-481), after every block of the update
+// pass has read *nb (the target-sync decision)
+__device__ inline void post_count_block(const PostUpdate &p) {
+    if (threadIdx.x != 0) return;
+    const int64_t upd = *p.updates, nb = *p.nb;
+    const float eps = *p.epsilon;
+    *p.epsilon = fmaxf(eps - p.decay, p.eps_end);   // utils.jl:480
+    *p.updates = upd + 1;
+    *p.nb = nb + 1;
+}
+__device__ inline void post_update_block(const PostUpdate &p) {   // 256 threads
+    post_loss_block(p);
+    post_count_block(p);
 }
 void grad_update_launch(const QLayout &L, const GradSlabs *pending, float *grad, const UpdateTarget *apply,
                         hipStream_t s, const PostUpdate *post = nullptr);

@@ -24,6 +24,7 @@
 // only half 0 writes a1, a2 and x0. Dense1 and the heads follow as before.
 #pragma once
 
+#include "snk_conv_h3.hpp"
 #include "snk_conv_x6.hpp"
 #include "snk_qnet.hpp"
 
@@ -71,9 +72,21 @@ constexpr int UPDF_NT = 512;   // 8 waves: two per SIMD, so one wave's LDS / MFM
 __host__ __device__ constexpr int updf_f32_words(int hin, int C) {
     return (C * (hin + 2) * (hin + 2) + 9 * C * 16 + 16 + 3) & ~3;
 }
-__host__ __device__ constexpr int updf_lds_bytes(int hin, int C) {
+__host__ __device__ constexpr int updf_base_bytes(int hin, int C) {
     return updf_f32_words(hin, C) * 4 + (hin + 2) * (hin + 2) * UPDF_A1S * 2 + 9 * 3 * 32 * 16 * 2 +
            3 * hin * updf_pj(hin) * 32 * 2;
+}
+// conv3's weight ring: slots of one kernel offset (the workgroup's 32 columns, 3 planes, 6 KB)
+// in the LDS beyond the images, filled by LDS-DMA NR - 1 offsets ahead; boards whose images
+// leave room for fewer than UPDF_RING_MIN slots keep the register-staged path
+constexpr int UPDF_SLOT = 3 * 32 * 32 * 2, UPDF_RING_MAX = 12, UPDF_RING_MIN = 6;
+__host__ __device__ constexpr int updf_ring(int hin, int C) {
+    return (160 * 1024 - updf_base_bytes(hin, C)) / UPDF_SLOT >= UPDF_RING_MAX
+               ? UPDF_RING_MAX
+               : (160 * 1024 - updf_base_bytes(hin, C)) / UPDF_SLOT;
+}
+__host__ __device__ constexpr int updf_lds_bytes(int hin, int C) {
+    return updf_base_bytes(hin, C) + (updf_ring(hin, C) >= UPDF_RING_MIN ? updf_ring(hin, C) * UPDF_SLOT : 0);
 }
 
 // the three bf16 parts h, m, l of x (split_part's values, in one pass)
@@ -114,7 +127,10 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     uint16_t *A1 = reinterpret_cast<uint16_t *>(xin + updf_f32_words(HIN, C));   // [NB][UPDF_A1S]
     uint16_t *B2 = A1 + NB * UPDF_A1S;                               // [9 kk][3][32 co][16 ci]
     uint16_t *A2 = B2 + 9 * 3 * 32 * 16;                             // [3][HIN][PJ][32] (swizzled chunks)
-    static_assert((NB * UPDF_A1S * 2) % 16 == 0, "16-B regions");
+    constexpr int NR = updf_ring(HIN, C);
+    constexpr bool RING = NR >= UPDF_RING_MIN;
+    uint16_t *R3 = A2 + 3 * A2P;                                     // [NR][3 pl][32 cols][32 ci] (swizzled pieces)
+    static_assert((NB * UPDF_A1S * 2) % 16 == 0 && updf_base_bytes(HIN, C) % 16 == 0, "16-B regions");
 
     UPD_CLK(0);
     const UpdFwdNet &n = args.net[blockIdx.y];
@@ -178,6 +194,23 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     }
     __syncthreads();
     UPD_CLK(1);
+    // conv3's weight ring (RING): offset k's 384 16-byte pieces (3 planes x 32 columns x 4)
+    // go to slot k % NR by waves 0..5, one global_load_lds_dwordx4 each: lane-linear LDS
+    // slots, the source piece chosen so that slot piece p of row c holds global piece
+    // p ^ ((c >> 2) & 3) (the swizzle the fragment reads expect). Offsets 0 .. NR-2 are issued
+    // at the start of conv2
+    const uint16_t *wsrc3 = n.wtb + 3 * L.off_t3 + (int64_t)half * 32 * 32;   // planes [kk][3][64 co][32 ci]
+    auto dma3 = [&](int k) __attribute__((always_inline)) {
+        if constexpr (RING) {
+            if (wave < 6) {
+                const int q = wave * 64 + lane, row = q >> 2, pl = row >> 5, c = row & 31;
+                const int piece = (q & 3) ^ ((row >> 2) & 3);
+                __builtin_amdgcn_global_load_lds(
+                    (const void *)(wsrc3 + ((int64_t)(k * 3 + pl) * 64 + c) * 32 + piece * 8),
+                    (__attribute__((address_space(3))) void *)(R3 + (k % NR) * (UPDF_SLOT / 2) + wave * 512), 16, 0, 0);
+            }
+        }
+    };
 
     // ---- phase 1: conv1 (VALU), a1 and its split ---------------------------------------
     for (int o = tid; o < NC * 16; o += UPDF_NT) {
@@ -202,6 +235,12 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     }
     __syncthreads();
     UPD_CLK(2);
+    // (issued here, not before conv1: every __syncthreads waits vmcnt(0), and conv2 is long
+    // enough to cover the weights' trip from L2 / MALL, conv1 is not)
+    if constexpr (RING) {
+#pragma unroll
+        for (int k = 0; k < NR - 1; ++k) dma3(k);
+    }
 
     // ---- phase 2: conv2 on x6 MFMA: rows = the HIN^2 positions, 32 columns -------------
     // wave w owns column tile w & 1 and row tiles (w >> 1) + 4u; offset pair p outermost so
@@ -336,6 +375,48 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
             }
         };
         static_assert(NSTG % 2 == 0, "stages come in pairs");
+        if constexpr (RING) {
+            // one barrier per offset: wait for this wave's DMA of offset kk (the newer ones,
+            // up to NR - 2, may stay in flight), publish with the barrier (every wave has also
+            // read slot (kk - 1) % NR into registers), refill that slot with offset kk + NR - 1.
+            // Chains as the staged path: offset kk into acc[.][(kk % 3) & 1]
+            // software-pipelined: step kk reads offset kk's fragments (B from slot kk % NR, A from
+            // the image) into registers right after the barrier, then issues offset kk - 1's MFMAs
+            // from the previous step's registers, so the LDS latency hides under the MFMAs
+            static_assert(NTW == 1, "ring path: one row tile per wave");
+            const bool live = rt0 < T3;   // wave-uniform
+            u32x4 fa[2][3], fb[2][3];
+            auto frag = [&](int kk, u32x4 (&xa)[3], u32x4 (&xb)[3]) __attribute__((always_inline)) {
+                const int du = kk % 6, dv = kk / 6;
+                const uint16_t *bb = R3 + (kk % NR) * (UPDF_SLOT / 2) + (ct * 16 + r) * LDB + 8 * (g ^ ((r >> 2) & 3));
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) xb[pl] = *reinterpret_cast<const u32x4 *>(bb + pl * 32 * LDB);
+                const int R = qb[0] + du + dv * PJ;
+                const uint16_t *pa = A2 + R * 32 + 8 * (g ^ ((R >> 1) & 3));
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) xa[pl] = *reinterpret_cast<const u32x4 *>(pa + pl * A2P);
+            };
+#pragma unroll
+            for (int kk = 0; kk <= 36; ++kk) {
+                if (kk < 36) {
+                    if (kk + NR - 2 <= 35)
+                        __builtin_amdgcn_s_waitcnt(waitcnt_vm(NR - 2));
+                    else
+                        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of slot (kk - 1) % NR done
+                    __builtin_amdgcn_s_barrier();
+                    if (kk + NR - 1 < 36) dma3(kk + NR - 1);
+                    if (live) frag(kk, fa[kk & 1], fb[kk & 1]);
+                }
+                if (kk > 0 && live) {
+                    const int k1 = kk - 1;
+                    if (((k1 % 3) & 1) == 0)
+                        acc[0][0] = mfma_x6(fa[k1 & 1], fb[k1 & 1], acc[0][0]);
+                    else
+                        acc[0][1] = mfma_x6(fa[k1 & 1], fb[k1 & 1], acc[0][1]);
+                }
+            }
+        } else {
         sload(0, sa);
         sload(1, sb);
         sstore(0, sa);
@@ -350,6 +431,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
             if (stg + 2 < NSTG) sstore(0, sa);     // stage stg + 2 (buffer 0 last read at stg)
             __syncthreads();
             if (stg + 4 < NSTG) sload(stg + 4, sa);
+        }
         }
         UPD_CLK(4);
         const float bv = b3[col];
