@@ -25,6 +25,7 @@
 // Backward: gemm_bf16_kernel, the snk_gemm.hpp engine on
 //   v_mfma_f32_32x32x16_bf16 with the snk_loaders.hpp implicit-im2col loaders.
 #pragma once
+#include "snk_conv_h3.hpp"
 #include "snk_conv_x6.hpp"
 #include "snk_loaders.hpp"
 
@@ -575,7 +576,8 @@ template <int H>
 struct DeepL3Shape {
     static constexpr int WO = H - 5, TILES = 2 * WO, TPS = (TILES + 3) / 4, PJ = (H + 1 + 7) / 8 * 8;
     static constexpr int XS = H * PJ * 64;
-    static constexpr int LDS = 2 * XS * 2;
+    static constexpr int WSLOTS = 4, WSLOT = 64 * 64 * 2;   // weight ring: one kernel offset (8 KB) per slot
+    static constexpr int LDS = 2 * XS * 2 + WSLOTS * WSLOT;
     static constexpr int APIECES = 2 * H * H * 8, APT = (APIECES + 511) / 512;
 };
 __device__ __forceinline__ int dl3_slot(int row, int c) { return row * 64 + 8 * (c ^ (row & 7)); }
@@ -608,15 +610,32 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         const int pos = rem >> 3;   // rows are numbered across the pair (the swizzle uses the pair-wide row)
         *reinterpret_cast<u32x4 *>(As + dl3_slot(smp * (H * PJ) + (pos % H) + (pos / H) * PJ, rem & 7)) = v;
     };
-    // the 4 weight fragments of kernel offset kk this wave uses: [c][c2], row (2h + c2)*16 + r,
-    // channels 32c + 8g .. +7 of the image [kk][co][ci]
-    const uint16_t *wl = wimg + ((2 * half) * 16 + r) * 64 + 8 * g;
-    auto wload = [&](int kk, u32x4 (&f)[4]) __attribute__((always_inline)) {
+    // weight ring (LDS-DMA): kernel offset k of the image [kk][co][ci] goes to slot k % WSLOTS
+    // as 64 rows (co) of 128 bytes, 16-byte chunk q of row co at q ^ (co & 7) (every fragment
+    // read below on distinct bank quads, tools/lds_banks.py model). Wave w moves rows 8w .. 8w+7:
+    // one global_load_lds_dwordx4 per wave and offset, lane-linear in LDS, the source chunk
+    // picked to match the swizzle. The loads never land in VGPRs, so no compiler-inserted
+    // vmcnt wait can pull them forward (register loads two offsets ahead were waited on right
+    // after issue at the loop head: an L2 round trip every other offset)
+    uint16_t *Wr = As + 2 * Sh::XS;
+    auto wdma = [&](int k) __attribute__((always_inline)) {
+        const int kk = k % 36, row = wave * 8 + (lane >> 3), q = (lane & 7) ^ (row & 7);
+        __builtin_amdgcn_global_load_lds((const void *)(wimg + (int64_t)kk * 64 * 64 + row * 64 + q * 8),
+                                         (__attribute__((address_space(3))) void *)(Wr + (k % Sh::WSLOTS) * (Sh::WSLOT / 2) +
+                                                                                     wave * 512),
+                                         16, 0, 0);
+    };
+    // the 4 weight fragments of offset k this wave uses: [c][c2], row (2h + c2)*16 + r, channels
+    // 32c + 8g .. +7
+    auto wread = [&](int k, u32x4 (&f)[4]) __attribute__((always_inline)) {
+        const uint16_t *ws = Wr + (k % Sh::WSLOTS) * (Sh::WSLOT / 2);
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
-            for (int c2 = 0; c2 < 2; ++c2)
-                f[2 * c + c2] = *reinterpret_cast<const u32x4 *>(wl + (int64_t)kk * 64 * 64 + c2 * 16 * 64 + 32 * c);
+            for (int c2 = 0; c2 < 2; ++c2) {
+                const int row = (2 * half + c2) * 16 + r;
+                f[2 * c + c2] = *reinterpret_cast<const u32x4 *>(ws + row * 64 + (((4 * c + g) ^ (row & 7)) << 3));
+            }
     };
     // wave-uniform first input row of row tile t (sample t / WO, output row t % WO)
     auto trow = [&](int t) __attribute__((always_inline)) { return (t / WO) * (H * PJ) + (t % WO) * PJ; };
@@ -628,9 +647,9 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         for (int u = 0; u < APT; ++u)
             if (tid + u * 512 < APIECES) apark(u, apiece(p, u));
     }
-    u32x4 wf[2][4];   // offsets kk, kk + 1
-    wload(0, wf[0]);
-    wload(1, wf[1]);
+    // offsets 0 .. WSLOTS-2 in flight before the first pair (k counts offsets across pairs)
+#pragma unroll
+    for (int k = 0; k < Sh::WSLOTS - 1; ++k) wdma(k);
     __syncthreads();
     for (; p < npairs; p += gridDim.x) {
         const bool more = p + gridDim.x < npairs;
@@ -638,30 +657,34 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         f32x4 acc[TPS][2];
 #pragma unroll
         for (int i = 0; i < TPS; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // one barrier per offset: wait for this wave's DMA of offset kk (the WSLOTS - 2 newer
+        // ones stay in flight), barrier (every wave's piece landed; every wave is past offset
+        // kk - 1, so its slot is free), refill that slot with offset kk + WSLOTS - 1, compute kk
 #pragma unroll 1
-        for (int k2 = 0; k2 < 36; k2 += 2) {
+        for (int kk = 0; kk < 36; ++kk) {
+            __builtin_amdgcn_s_waitcnt(waitcnt_vm(Sh::WSLOTS - 2));
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            wdma(kk + Sh::WSLOTS - 1);
+            u32x4 wf[4];
+            wread(kk, wf);
+            const int du = kk % 6, dv = kk / 6;
+            const int sw = (r + du) & 7;
+            const int xl0 = (r + du) * 64 + 8 * (g ^ sw), xl1 = (r + du) * 64 + 8 * ((4 + g) ^ sw);
+            const uint16_t *Ak = As + dv * PJ * 64;
 #pragma unroll
-            for (int o = 0; o < 2; ++o) {
-                const int kk = k2 + o, du = kk % 6, dv = kk / 6;
-                const int sw = (r + du) & 7;
-                const int xl0 = (r + du) * 64 + 8 * (g ^ sw), xl1 = (r + du) * 64 + 8 * ((4 + g) ^ sw);
-                const uint16_t *Ak = As + dv * PJ * 64;
+            for (int c = 0; c < 2; ++c) {
 #pragma unroll
-                for (int c = 0; c < 2; ++c) {
+                for (int i = 0; i < TPS; ++i) {
+                    const int t = simd + 4 * i;
+                    if (i == TPS - 1 && !last_ok) continue;   // only the last tile can be missing
+                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(Ak + trow(t) * 64 + (c ? xl1 : xl0)));
 #pragma unroll
-                    for (int i = 0; i < TPS; ++i) {
-                        const int t = simd + 4 * i;
-                        if (i == TPS - 1 && !last_ok) continue;   // only the last tile can be missing
-                        const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(Ak + trow(t) * 64 + (c ? xl1 : xl0)));
-#pragma unroll
-                        for (int c2 = 0; c2 < 2; ++c2)
-                            acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wf[o][2 * c + c2]), xv,
-                                                                                 acc[i][c2], 0, 0, 0);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);   // the next step's reads after these MFMAs (registers)
+                    for (int c2 = 0; c2 < 2; ++c2)
+                        acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wf[2 * c + c2]), xv, acc[i][c2], 0,
+                                                                             0, 0);
                 }
-                const int kn = kk + 2 < 36 ? kk + 2 : kk - 34;   // two offsets ahead (wrapping to the next pair)
-                wload(kn, wf[o]);
+                __builtin_amdgcn_sched_barrier(0);   // the next step's reads after these MFMAs (registers)
             }
         }
         // epilogue: bias + relu + bf16, 4 channels per lane
@@ -687,6 +710,7 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         }
         __syncthreads();
     }
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // the ring's last refills land before the workgroup ends
 }
 
 // ---------------------------------------------------------------- Dense1
