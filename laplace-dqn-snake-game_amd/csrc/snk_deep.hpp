@@ -657,35 +657,45 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         f32x4 acc[TPS][2];
 #pragma unroll
         for (int i = 0; i < TPS; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // one barrier per offset: wait for this wave's DMA of offset kk (the WSLOTS - 2 newer
-        // ones stay in flight), barrier (every wave's piece landed; every wave is past offset
-        // kk - 1, so its slot is free), refill that slot with offset kk + WSLOTS - 1, compute kk
+        // one barrier per offset: wait for this wave's DMAs of offsets kk and kk + 1 (kk + 2 stays
+        // in flight), barrier (every wave's pieces landed; every wave is past offset kk - 1, so
+        // its slot is free), refill that slot with offset kk + 3. The weight fragments of kk + 1
+        // and the activation fragments of the next step are read while kk's MFMAs issue (one
+        // activation register per tile, reloaded right after the tile's MFMAs): only the first
+        // offset of a pair waits on its reads
+        bf16x8 xv[TPS];
+        auto xread = [&](int kk, int c, int i) __attribute__((always_inline)) {
+            const int du = kk % 6, dv = kk / 6, sw = (r + du) & 7;
+            return as_bf(*reinterpret_cast<const u32x4 *>(As + dv * PJ * 64 + trow(simd + 4 * i) * 64 + (r + du) * 64 +
+                                                          8 * ((4 * c + g) ^ sw)));
+        };
+#pragma unroll
+        for (int i = 0; i < TPS; ++i)
+            if (!(i == TPS - 1 && !last_ok)) xv[i] = xread(0, 0, i);
+        u32x4 wcur[4], wnext[4];
 #pragma unroll 1
         for (int kk = 0; kk < 36; ++kk) {
-            __builtin_amdgcn_s_waitcnt(waitcnt_vm(Sh::WSLOTS - 2));
+            __builtin_amdgcn_s_waitcnt(waitcnt_vm(Sh::WSLOTS - 3));
             __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
             __builtin_amdgcn_s_barrier();
             wdma(kk + Sh::WSLOTS - 1);
-            u32x4 wf[4];
-            wread(kk, wf);
-            const int du = kk % 6, dv = kk / 6;
-            const int sw = (r + du) & 7;
-            const int xl0 = (r + du) * 64 + 8 * (g ^ sw), xl1 = (r + du) * 64 + 8 * ((4 + g) ^ sw);
-            const uint16_t *Ak = As + dv * PJ * 64;
+            if (kk == 0) wread(0, wcur);
+            wread(kk + 1, wnext);   // kk = 35: offset 0 of the next pair (slot 36 % 4), harmless
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
+                const int nk = c == 0 ? kk : (kk + 1 < 36 ? kk + 1 : 0), nc = c ^ 1;   // the next step
 #pragma unroll
                 for (int i = 0; i < TPS; ++i) {
-                    const int t = simd + 4 * i;
                     if (i == TPS - 1 && !last_ok) continue;   // only the last tile can be missing
-                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(Ak + trow(t) * 64 + (c ? xl1 : xl0)));
 #pragma unroll
                     for (int c2 = 0; c2 < 2; ++c2)
-                        acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wf[2 * c + c2]), xv, acc[i][c2], 0,
-                                                                             0, 0);
+                        acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wcur[2 * c + c2]), xv[i], acc[i][c2],
+                                                                             0, 0, 0);
+                    xv[i] = xread(nk, nc, i);
                 }
-                __builtin_amdgcn_sched_barrier(0);   // the next step's reads after these MFMAs (registers)
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) wcur[q] = wnext[q];
         }
         // epilogue: bias + relu + bf16, 4 channels per lane
 #pragma unroll

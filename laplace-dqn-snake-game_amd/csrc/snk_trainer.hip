@@ -56,11 +56,14 @@ struct snk_trainer_s {
     int64_t log_cap = 0;
     uint32_t *ticket = nullptr;   // grad_update_kernel's arrival counter (post-update fold)
     int32_t B = 64;
-    // [2 * learn + unrolled]: one iteration, or `unroll` iterations back to back in one
-    // graph (iterations only communicate through device counters, so a longer graph is
-    // the same launch sequence with the per-graph launch gap paid once per `unroll`)
-    hipGraph_t graph[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipGraphExec_t exec[4] = {nullptr, nullptr, nullptr, nullptr};
+    // [learn][n]: n iterations back to back in one graph (iterations only communicate
+    // through device counters, so a longer graph is the same launch sequence with the
+    // per-graph launch gap and the first iteration's weight-max scan paid once per graph):
+    // n = `unroll`, and n = the remainder of a run that is not a multiple of it (one graph
+    // for the tail instead of one single-iteration graph per leftover iteration)
+    static constexpr int MAXG = 64;
+    hipGraph_t graph[2][MAXG + 1] = {};
+    hipGraphExec_t exec[2][MAXG + 1] = {};
     int unroll = 8;
     int64_t ws_gen = 0;   // dqn workspace generation the graphs were captured against
     // snk_trainer_set_trace: every update's finished gradient is also copied to
@@ -74,12 +77,13 @@ struct snk_trainer_s {
     float *q_trace = nullptr;
     int64_t act_trace_slots = 0;
     void drop_graphs() {
-        for (int i = 0; i < 4; ++i) {
-            if (exec[i]) (void)hipGraphExecDestroy(exec[i]);
-            if (graph[i]) (void)hipGraphDestroy(graph[i]);
-            exec[i] = nullptr;
-            graph[i] = nullptr;
-        }
+        for (int g = 0; g < 2; ++g)
+            for (int i = 0; i <= MAXG; ++i) {
+                if (exec[g][i]) (void)hipGraphExecDestroy(exec[g][i]);
+                if (graph[g][i]) (void)hipGraphDestroy(graph[g][i]);
+                exec[g][i] = nullptr;
+                graph[g][i] = nullptr;
+            }
     }
 };
 
@@ -302,8 +306,8 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
         if (learn && upi > 0) trainer_check_replay(h);
         trainer_refresh(h);
         const int g = learn ? 1 : 0;
-        auto capture = [&](int slot, int n) {
-            if (h->exec[slot]) return;
+        auto capture = [&](int n) {   // the n-iteration graph, captured once
+            if (h->exec[g][n]) return h->exec[g][n];
             SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             try {
                 for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s, i, i > 0, i + 1 < n);
@@ -312,22 +316,27 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
                 (void)hipStreamEndCapture(s, &dummy);
                 throw;
             }
-            SNK_HIP(hipStreamEndCapture(s, &h->graph[slot]));
-            SNK_HIP(hipGraphInstantiate(&h->exec[slot], h->graph[slot], nullptr, nullptr, 0));
+            SNK_HIP(hipStreamEndCapture(s, &h->graph[g][n]));
+            SNK_HIP(hipGraphInstantiate(&h->exec[g][n], h->graph[g][n], nullptr, nullptr, 0));
+            return h->exec[g][n];
         };
         if (!use_graph) {
             for (int64_t i = 0; i < iters; ++i)
                 trainer_iteration(h, learn != 0, upi, s, (int)(i % (1 << 20)), i > 0, i + 1 < iters);
             return;
         }
-        const int U = h->unroll;
-        int64_t i = 0;
-        if (U > 1 && iters >= U) {
-            capture(2 * g + 1, U);
-            for (; i + U <= iters; i += U) SNK_HIP(hipGraphLaunch(h->exec[2 * g + 1], s));
+        const int U = std::min(h->unroll, (int)snk_trainer_s::MAXG);
+        if (U <= 1) {
+            hipGraphExec_t e = capture(1);
+            for (int64_t i = 0; i < iters; ++i) SNK_HIP(hipGraphLaunch(e, s));
+            return;
         }
-        if (i < iters) capture(2 * g, 1);
-        for (; i < iters; ++i) SNK_HIP(hipGraphLaunch(h->exec[2 * g], s));
+        int64_t i = 0;
+        if (iters >= U) {
+            hipGraphExec_t e = capture(U);
+            for (; i + U <= iters; i += U) SNK_HIP(hipGraphLaunch(e, s));
+        }
+        if (i < iters) SNK_HIP(hipGraphLaunch(capture((int)(iters - i)), s));   // the tail: one graph (< U iterations)
     });
 }
 
