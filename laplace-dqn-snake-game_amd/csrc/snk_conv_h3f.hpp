@@ -43,6 +43,7 @@ struct H3FArgs {
     const uint16_t *w3h;
     const int *w3e;      // w3h's exponent (ew), then w2h's (ew2)
     const uint16_t *w2h;
+    float *a3max;        // optional: max of each sample's a3 (>= 0: post-relu), for Dense1's h3 scale
 };
 // conv2's split weight image in LDS: [5 offset pairs][h | l][32 co][48 halves] (k = 16 (kk & 1)
 // + ci in the first 32 halves of a row; kk = 9 is zero), 1,920 16-byte chunks, padded to 2,048
@@ -56,11 +57,39 @@ constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 // Blocks 72..76: conv2's image [9 kk][32 co][16 ci] (fp32, 1,152 float4) split with its own
 // per-tensor exponent ew2 = h3_exp(max |w2|) into the B2 image (out2, zero-initialised: the
 // pad offset and the pad columns stay zero), eout[1] = ew2.
+// Blocks 77.. (when out1): Dense1's image [nkk positions][64 out][64 in] split row by row
+// (one row = 64 inputs of one output at one position = 16 lanes, one float4 each) with the
+// row's own exponent e1[kk * 64 + out] = h3_exp(max |row|) into planes
+// out1[kk][h | l][64 out][64 in], 16-byte chunk q of a row at q ^ (out & 7) (dense_h3_kernel's
+// fragment reads: distinct bank quads). A per-(position, output) scale factors out of the
+// position's partial sum, so each is scaled back on its own.
 constexpr int W3S_BLOCKS = 36 * 512 / 256, W2S_BLOCKS = (9 * 32 * 16 / 4 + 255) / 256;
+__host__ __device__ constexpr int w1s_blocks(int nkk) { return nkk * 64 * 16 / 256; }
 static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__restrict__ img, const float *__restrict__ wmax,
                                                        int nwmax, uint16_t *__restrict__ out, int *__restrict__ eout,
-                                                       const float *__restrict__ img2, uint16_t *__restrict__ out2) {
+                                                       const float *__restrict__ img2, uint16_t *__restrict__ out2,
+                                                       const float *__restrict__ img1 = nullptr,
+                                                       uint16_t *__restrict__ out1 = nullptr, int *__restrict__ e1 = nullptr) {
     __shared__ float red4[4];
+    if (blockIdx.x >= W3S_BLOCKS + W2S_BLOCKS) {   // Dense1
+        const int t = (blockIdx.x - W3S_BLOCKS - W2S_BLOCKS) * 256 + threadIdx.x;
+        const int row = t >> 4, q4 = t & 15, kk = row >> 6, o = row & 63;
+        const f32x4 v = reinterpret_cast<const f32x4 *>(img1)[t];
+        float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+        m = dpp_max<0xB1>(m);    // the 16-lane row's max (wave_max's first four steps)
+        m = dpp_max<0x4E>(m);
+        m = dpp_max<0x141>(m);
+        m = dpp_max<0x140>(m);
+        const int ex = h3_exp(m);
+        if (q4 == 0) e1[row] = ex;
+        u32x2 hh, ll;
+        h3_split4(v, ex, hh, ll);
+        const int off = (o * 64 + (((q4 >> 1) ^ (o & 7)) << 3) + ((q4 & 1) << 2)) / 4;   // in u32x2 units
+        u32x2 *o1 = reinterpret_cast<u32x2 *>(out1 + (int64_t)kk * 2 * 4096);
+        o1[off] = hh;
+        o1[1024 + off] = ll;
+        return;
+    }
     if (blockIdx.x >= W3S_BLOCKS) {   // conv2
         constexpr int NW4 = 9 * 32 * 16 / 4;
         const f32x4 *w4 = reinterpret_cast<const f32x4 *>(img2);
@@ -194,18 +223,34 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
                                              16, 0, 0);
         }
     };
-    if constexpr (DMA) {   // offsets 0..3 now (conv1 stages its boards in buffer 7), and conv2's weights
-        dma(0);
-        dma(1);
-        dma(2);
-        dma(3);
-        static_assert(H3F_B2_CHUNKS == 4 * 512, "four B2 pieces per thread");
+    // DMA: conv2's weights and conv3's offsets 0..3 are issued once the boards are staged
+    // (below): vmcnt retires in order, so a load issued after them and used during conv1
+    // would wait for them (they sat in front of the boards, and every __syncthreads drained
+    // them)
+    auto dma_prologue = [&]() __attribute__((always_inline)) {
+        if constexpr (DMA) {
+            static_assert(H3F_B2_CHUNKS == 4 * 512, "four B2 pieces per thread");
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            __builtin_amdgcn_global_load_lds((const void *)(a.w2h + ((int64_t)q * 512 + tid) * 8),
-                                             (__attribute__((address_space(3))) void *)(B2 + (q * 512 + wave * 64) * 8),
-                                             16, 0, 0);
-    } else {
+            for (int q = 0; q < 4; ++q)
+                __builtin_amdgcn_global_load_lds((const void *)(a.w2h + ((int64_t)q * 512 + tid) * 8),
+                                                 (__attribute__((address_space(3))) void *)(B2 + (q * 512 + wave * 64) * 8),
+                                                 16, 0, 0);
+            dma(0);   // conv1 stages its boards in buffer 7
+            dma(1);
+            dma(2);
+            dma(3);
+        }
+    };
+    // LDS-only barrier (no vmcnt drain) while the prologue DMAs are in flight
+    auto lds_barrier = [&]() __attribute__((always_inline)) {
+        if constexpr (DMA) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+        } else {
+            __syncthreads();
+        }
+    };
+    if constexpr (!DMA) {
         b_load(0, 0);
         b_load(1, 1);
     }
@@ -292,7 +337,12 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             const int q = u * 512 + tid;
             if (q < NX) xin[q] = fl ? __int_as_float(bv[u]) : (float)bv[u];
         }
-        __syncthreads();
+        // after the boards are consumed: the compiler does not count LDS-DMAs in its vmcnt
+        // waits, so a wait for a load issued before them comes out as vmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+        dma_prologue();
+        __builtin_amdgcn_sched_barrier(0);
+        lds_barrier();
 #pragma unroll
         for (int u = 0; u < LA; ++u) {   // output (sample, position, channels 4 cq..): a1's layout
             const int e = min(u * 512 + tid, na4 - 1);
@@ -346,7 +396,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         red[wave][4] = mw2;
         red[wave][5] = wm3;
     }
-    __syncthreads();   // also: the border fill is complete
+    lds_barrier();   // also: the border fill is complete
     int ea1[NSG], ew2;
     {
         float m[6];
@@ -388,7 +438,8 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             A1v[(((sr * 2 + 1) * NPB + pb) * XR + c0) / 4] = ll;
         }
     }
-    __syncthreads();
+    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(4));   // conv2's weights landed (offsets 0..3 may not)
+    lds_barrier();
     H3F_CLK(2);
 
     // ---- conv2, transposed: C^T[co][row] = sum_k W[co][k] * A[row][k] with the weight
@@ -478,7 +529,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
 #pragma unroll
         for (int q = 0; q < NSG; ++q) red[wave][q] = m2[q];
     }
-    __syncthreads();   // also: every conv2 fragment read is done (the A image overlays them)
+    lds_barrier();   // also: every conv2 fragment read is done (the A image overlays them)
     H3F_CLK(3);
     int ea[NSG];
 #pragma unroll
@@ -533,6 +584,9 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         for (int k = 0; k < NT; ++k)
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) acc[k][ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        // the epilogue's two bias values, loaded before the offsets (inside the epilogue the
+        // compiler re-loaded and waited on them per row tile: three serial round trips)
+        const float bv2[2] = {a.b3[cg * 32 + r], a.b3[cg * 32 + 16 + r]};
         struct Frag {
             u32x4 a[NT][2], b[2][2];
         };
@@ -618,6 +672,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         constexpr int CS = 80;
         static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN, NBUF>() - NBUF * NB * 16, "output staging fits");
         float *Cs = reinterpret_cast<float *>(As);
+        float vm[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // this lane's max per sample (post-relu: >= 0)
 #pragma unroll
         for (int k = 0; k < NT; ++k) {
             const int p = 4 * (rg + 4 * k) + g;
@@ -625,15 +680,30 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) {
                 const int col = cg * 32 + ct * 16 + r;
-                const float bv = a.b3[col];
+                const float bv = bv2[ct];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float v = __builtin_ldexpf(acc[k][ct][e], -(ea[e] + ew)) + bv;
-                    Cs[(e * ho2 + p) * CS + col] = v > 0.0f ? v : 0.0f;
+                    const float rv = v > 0.0f ? v : 0.0f;
+                    Cs[(e * ho2 + p) * CS + col] = rv;
+                    vm[e] = fmaxf(vm[e], rv);
                 }
             }
         }
+        if (a.a3max) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                vm[e] = wave_max(vm[e]);
+                if (lane == 0) red[wave][e] = vm[e];
+            }
+        }
         __syncthreads();
+        if (a.a3max && tid < ns) {
+            float m = red[0][tid];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w][tid]);
+            a.a3max[s0 + tid] = m;
+        }
         const int n4o = ns * ho2 * 16;
         f32x4 *o4 = reinterpret_cast<f32x4 *>(a.out + (int64_t)s0 * ho2 * CN);
         const f32x4 *c4 = reinterpret_cast<const f32x4 *>(Cs);

@@ -1,0 +1,163 @@
+// snk_dense_h3.hpp — Dense1 of the act forward (3136 -> 64 at 12x12) on the fp16 h3 split.
+//
+// The x6 form (conv_x6_kernel MODE_DENSE) split every fp32 a3 element into three bf16
+// parts in registers and ran six part products per fp32 product; here A and B move as
+// fp16 h / l planes and a product takes three MFMAs (snk_conv_h3.hpp):
+//  * A = a3 rows (samples), fp32 from global, scaled by 2^ea[row] with
+//    ea = h3_exp(max of the sample's a3), which conv_h3f_kernel's epilogue writes
+//    (H3FArgs::a3max), split in registers;
+//  * B = the Dense1 image pre-split by w3_split_kernel with one exponent per (position,
+//    output) (its own row max), planes [kk][h | l][64 out][64 in], chunk-swizzled;
+//  * each position's six MFMAs (two 32-channel k-steps x hl + lh + hh) start from zero and
+//    are added into the tile's accumulator scaled by 2^-ew[kk][out] (exact: a power of two),
+//    the row scale 2^-ea comes back once at the end.
+// Grid: (S / 128 row blocks) x (slabs of KPZ positions), 4 waves of 32 rows (two 16-row tiles,
+// four 16-column tiles each); slab[z][s][o] as the x6 kernel's EPI_SLAB, summed by the head.
+// B of each position (16 KB) goes through an LDS ring of 4 slots filled by LDS-DMA three
+// positions ahead; A of the next position is loaded while the current one computes. KPZ is a
+// template constant and the position loop unrolled: straight-line code keeps the compiler's
+// vmcnt waits on the A registers exact (a loop back edge merged them to waits on the newest
+// loads, which also count the DMAs).
+#pragma once
+#include "snk_conv_h3.hpp"
+
+namespace snk {
+
+struct DenseH3Args {
+    const float *a3;       // [S][nkk * 64]
+    const float *a3max;    // [S] max of each row (>= 0)
+    const uint16_t *w1h;   // [nkk][2][64][64] (w3_split_kernel)
+    const int *w1e;        // [nkk][64]
+    float *slab;           // [nkk / KPZ][S][64]
+    int S, nkk;
+};
+constexpr int DH3_RING = 4, DH3_SLOT = 2 * 64 * 64 * 2;   // bytes per slot: both planes of one position
+
+template <int KPZ>   // positions per slab; the launch guarantees nkk % KPZ == 0
+__global__ __launch_bounds__(256) void dense_h3_kernel(DenseH3Args a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t dh3_lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int z = blockIdx.y, kk0 = z * KPZ;
+    const int K1 = a.nkk * 64;
+    const int row0 = blockIdx.x * 128 + wave * 32;
+    // B ring: position j of the slab in slot j % DH3_RING; 1024 16-byte pieces, 4 per lane
+    auto dma = [&](int j) __attribute__((always_inline)) {
+        const uint16_t *src = a.w1h + (int64_t)(kk0 + j) * 2 * 4096;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            __builtin_amdgcn_global_load_lds((const void *)(src + (u * 256 + tid) * 8),
+                                             (__attribute__((address_space(3))) void *)(dh3_lds + (j % DH3_RING) * (DH3_SLOT / 2) +
+                                                                                         (u * 256 + wave * 64) * 8),
+                                             16, 0, 0);
+    };
+    // A: rows row0 + 16t + r (clamped), channels 32ks + 8g .. +7 of position kk0 + j
+    int ar[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) ar[t] = min(row0 + 16 * t + r, a.S - 1);
+    auto aload = [&](int j, f32x4 (&x)[2][2][2]) __attribute__((always_inline)) {
+        const int kk = kk0 + j;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const float *p = a.a3 + (int64_t)ar[t] * K1 + kk * 64 + 32 * ks + 8 * g;
+                x[t][ks][0] = *reinterpret_cast<const f32x4 *>(p);
+                x[t][ks][1] = *reinterpret_cast<const f32x4 *>(p + 4);
+            }
+    };
+    int ea[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) ea[t] = h3_exp(a.a3max[ar[t]]);
+    // and the maxima of the C rows this lane writes (sample row0 + 16t + 4g + e), up front too
+    float cm[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cm[t][e] = a.a3max[min(row0 + 16 * t + 4 * g + e, a.S - 1)];
+    // the slab's B exponents of this lane's four columns, up front (a load inside the loop
+    // would be the newest VMEM op at its use, and its wait would drain the A / B prefetches)
+    int ewc[KPZ][4];
+#pragma unroll
+    for (int j = 0; j < KPZ; ++j)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) ewc[j][ct] = a.w1e[(kk0 + j) * 64 + ct * 16 + r];
+    f32x4v acc[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[t][ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    // issue order (vmcnt counts loads and DMAs together, in order): B(0), B(1), A(0), B(2),
+    // then per position j: A(j+1), B(j+3). At j, A(j) and everything older (B(<= j+1)) must
+    // have landed; only B(j+2), issued after A(j), may stay in flight (4 DMAs)
+    f32x4 xa[2][2][2][2];   // [set][tile][k-step][half]
+    dma(0);
+    if (KPZ > 1) dma(1);
+    aload(0, xa[0]);
+    if (KPZ > 2) dma(2);
+#pragma unroll
+    for (int j = 0; j < KPZ; ++j) {
+        if (j + 2 < KPZ) __builtin_amdgcn_s_waitcnt(waitcnt_vm(4));
+        else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of slot (j - 1) % 4 done
+        __builtin_amdgcn_s_barrier();         // every wave's pieces of B(j) landed; slot (j + 3) % 4 free
+        // pinned here: left to itself the scheduler sank the A loads behind this position's
+        // MFMAs, and the next position then waited on them at its first MFMA
+        __builtin_amdgcn_sched_barrier(0);
+        if (j + 1 < KPZ) aload(j + 1, xa[(j + 1) & 1]);
+        if (j + 3 < KPZ) dma(j + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        // A fragments: the position's 16 values per lane and tile, scaled and split
+        f16x8 ah[2][2], al[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                u32x2 h0, l0, h1, l1;
+                h3_split4(xa[j & 1][t][ks][0], ea[t], h0, l0);
+                h3_split4(xa[j & 1][t][ks][1], ea[t], h1, l1);
+                ah[t][ks] = as_h(u32x4{h0[0], h0[1], h1[0], h1[1]});
+                al[t][ks] = as_h(u32x4{l0[0], l0[1], l1[0], l1[1]});
+            }
+        const uint16_t *slot = dh3_lds + (j % DH3_RING) * (DH3_SLOT / 2);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+            const int o = ct * 16 + r;
+            const float sc = __builtin_ldexpf(1.0f, -ewc[j][ct]);
+            f16x8 bh[2], bl[2];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int off = o * 64 + (((4 * ks + g) ^ (o & 7)) << 3);
+                bh[ks] = as_h(*reinterpret_cast<const u32x4 *>(slot + off));
+                bl[ks] = as_h(*reinterpret_cast<const u32x4 *>(slot + 4096 + off));
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                f32x4v c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[t][ks], bl[ks], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[t][ks], bh[ks], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[t][ks], bh[ks], c, 0, 0, 0);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[t][ct][e] = __builtin_fmaf(c[e], sc, acc[t][ct][e]);
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    // C row 4g + e of tile t = sample row0 + 16t + 4g + e, column ct*16 + r; the row scale back
+    float *out = a.slab + (int64_t)z * a.S * 64;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int row = row0 + 16 * t + 4 * g + e;
+            if (row >= a.S) continue;
+            const int ex = h3_exp(cm[t][e]);
+#pragma unroll
+            for (int ct = 0; ct < 4; ++ct) out[(int64_t)row * 64 + ct * 16 + r] = __builtin_ldexpf(acc[t][ct][e], -ex);
+        }
+}
+
+}  // namespace snk

@@ -15,6 +15,7 @@
 
 #include "snk_conv_h3.hpp"
 #include "snk_conv_h3f.hpp"
+#include "snk_dense_h3.hpp"
 #include "snk_bwd3.hpp"
 #include "snk_conv_x6.hpp"
 #include "snk_loaders.hpp"
@@ -881,7 +882,7 @@ void qwork_free(QWork &w) {
                     (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.x0, (void *)w.target,
                     (void *)w.loss, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e,
-                    (void *)w.w2h})
+                    (void *)w.w2h, (void *)w.w1h, (void *)w.w1e, (void *)w.a3max})
         dfree(p);
     w = QWork{};
 }
@@ -942,6 +943,9 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     w.w3h = dalloc<uint16_t>((size_t)36 * 512 * 8);
     w.w3e = dalloc<int>(2);
     w.w2h = dalloc<uint16_t>((size_t)H3F_B2_CHUNKS * 8);
+    w.w1h = dalloc<uint16_t>((size_t)L.Wo * L.Wo * 2 * 4096);
+    w.w1e = dalloc<int>((size_t)L.Wo * L.Wo * 64);
+    w.a3max = dalloc<float>((size_t)cap);
     SNK_HIP(hipMemsetAsync(w.w2h, 0, (size_t)H3F_B2_CHUNKS * 16, stream()));   // pads stay zero
     if (tr) {
         w.has_train = 1;
@@ -997,6 +1001,19 @@ static void h3f_launch_t(const H3FArgs &fa, int64_t S, hipStream_t s) {
     launch_check("conv_h3f_kernel");
 }
 static bool h3f_dma(int bs) { return bs <= 12; }
+
+// dense_h3_kernel instantiations: KPZ positions per slab (d1_split's kk_per), all slabs full
+static bool dh3_ok(const QLayout &L, int ks, int kpz) {
+    static const bool on = !getenv("SNK_DH3") || atoi(getenv("SNK_DH3")) != 0;   // tests: x6 comparisons
+    return on && kpz == 7 && ks * kpz == L.Wo * L.Wo;
+}
+static void dh3_launch(const DenseH3Args &a, int ks, int kpz, hipStream_t s) {
+    SNK_CHECK(kpz == 7 && ks * kpz == a.nkk && a.S > 0, SNK_ERR_INTERNAL, "dense_h3: slab split");
+    constexpr size_t lds = (size_t)DH3_RING * DH3_SLOT;
+    set_lds_limit((const void *)dense_h3_kernel<7>, lds);
+    dense_h3_kernel<7><<<dim3((unsigned)ceil_div(a.S, 128), (unsigned)ks), 256, lds, s>>>(a);
+    launch_check("dense_h3_kernel");
+}
 template <int HIN>
 static void h3f_launch_bs(const H3FArgs &fa, int C, int64_t S, hipStream_t s) {
     if (C == 1)
@@ -1073,6 +1090,15 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
     // the sample rider.
     bool f123 = h3c2;
     for (int g = 0; g < ng; ++g) f123 = f123 && !net[g].w->has_train;
+    // Dense1 on dense_h3_kernel: this call runs conv_h3f (which writes the per-sample a3
+    // maxima) with the DMA'd weights (w3_split_kernel also splits Dense1) and then Dense1, at a
+    // slab split the kernel is instantiated for
+    bool dh3 = false;
+    if (f123 && hi >= 3 && lo <= 2 && h3f_dma(L.bs)) {
+        int kc;
+        const int ks = d1_split(L, S, kc);
+        dh3 = dh3_ok(L, ks, kc);
+    }
     if (f123 && hi >= 0 && lo <= 2) {
         for (int g = 0; g < ng; ++g) {
             const FwdNet &n = net[g];
@@ -1092,8 +1118,10 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             }
             SNK_CHECK(!rd.out || (lo <= 2 && hi >= 1), SNK_ERR_INTERNAL, "sample rider without a launch");
             if (lo <= 2 && hi >= 1 && h3f_dma(L.bs)) {   // the conv3 weights pre-split once for every workgroup
-                w3_split_kernel<<<W3S_BLOCKS + W2S_BLOCKS, 256, 0, s>>>(img, w.wmax_part, w.wmax_n, w.w3h, w.w3e,
-                                                                        n.wt + L.off_t2, w.w2h);
+                const int nkk = L.Wo * L.Wo;
+                w3_split_kernel<<<W3S_BLOCKS + W2S_BLOCKS + (dh3 ? w1s_blocks(nkk) : 0), 256, 0, s>>>(
+                    img, w.wmax_part, w.wmax_n, w.w3h, w.w3e, n.wt + L.off_t2, w.w2h, dh3 ? n.wt + L.off_td : nullptr,
+                    w.w1h, w.w1e);
                 launch_check("w3_split_kernel");
             }
             if (lo <= 2 && hi >= 1) {
@@ -1107,6 +1135,7 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
                 fa.src = n.src; fa.w1 = n.th + L.off_w1; fa.b1 = n.th + L.off_b1;
                 fa.w2 = n.wt + L.off_t2; fa.b2 = n.th + L.off_b2; fa.w3 = img; fa.wmax = w.wmax_part;
                 fa.nwmax = w.wmax_n; fa.b3 = n.th + L.off_b3; fa.out = w.a3;
+                fa.a3max = dh3 ? w.a3max : nullptr;
                 conv_h3f_launch(L.bs, L.C, fa, S, s);
             }
         }
@@ -1173,6 +1202,16 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             }
         }
         conv_fwd<32, 64, 6, 0>(io, ng, S * L.Wo * L.Wo, bs, L.Wo, s);
+    }
+    if (lo <= 3 && hi >= 3 && dh3) {   // Dense1 on the h3 split, the same slab layout
+        int kc;
+        const int ks = d1_split(L, S, kc);
+        for (int g = 0; g < ng; ++g) {
+            const FwdNet &n = net[g];
+            const DenseH3Args da{n.w->a3, n.w->a3max, n.w->w1h, n.w->w1e, n.w->slab, (int)S, L.Wo * L.Wo};
+            dh3_launch(da, ks, kc, s);
+        }
+        return;
     }
     if (lo <= 3 && hi >= 3) {   // Dense1 (split over the Wo^2 positions into partial slabs; bias + relu in the head)
         int kc;
@@ -1782,6 +1821,15 @@ __device__ uint64_t *g_gu_clk;
 #endif
 __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
     GU_CLK(0);
+    // the post-update words, read now by every block's thread 0 (only the last block to
+    // arrive uses them; no block of this pass writes them before that)
+    int64_t pre_upd = 0, pre_nb = 0;
+    float pre_eps = 0.0f;
+    if (a.has_post && threadIdx.x == 0) {
+        pre_upd = *a.post.updates;
+        pre_nb = *a.post.nb;
+        pre_eps = *a.post.epsilon;
+    }
     const QLayout &L = a.L;
     const bool due = a.apply && a.u.counter && (*a.u.counter % a.u.rate) == 0;   // utils.jl:469-472
     const float omr = 1.0f - a.u.rho;
@@ -1885,7 +1933,7 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
     __syncthreads();
     if (!s_last) return;
     GU_CLK(2);
-    post_count_block(a.post);
+    post_count_block(a.post, pre_upd, pre_nb, pre_eps);
     if (threadIdx.x == 0) __hip_atomic_store(a.post.ticket + 8 * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     GU_CLK(3);
     if (!a.post.next.out) return;

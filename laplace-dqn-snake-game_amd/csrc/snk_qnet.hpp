@@ -75,6 +75,9 @@ struct QWork {
     uint16_t *w3h = nullptr;         // h3 conv3 weights pre-split for conv_h3f_kernel's LDS-DMA staging:
     int *w3e = nullptr;              //   [36 kk][512 16-byte chunks] in the B buffers' swizzled order, and their exponent
     uint16_t *w2h = nullptr;         //   (w3e[1]: conv2's) and conv2's weights pre-split into the B2 image bytes
+    uint16_t *w1h = nullptr;         // Dense1's image pre-split for dense_h3_kernel ([Wo^2][2][64][64] halves),
+    int *w1e = nullptr;              //   one exponent per (position, output)
+    float *a3max = nullptr;          // per-sample max of a3 (conv_h3f_kernel's epilogue), Dense1's h3 row scale
     double *target = nullptr, *loss = nullptr;
     int has_train = 0;
     int64_t gen = 0;          // bumped on every reallocation (captured graphs hold the old pointers)
@@ -211,13 +214,18 @@ __device__ inline void post_loss_block(const PostUpdate &p) {   // 256 threads
 }
 // epsilon decay and the update counters (utils.jl:469-481), after every block of the update
 // pass has read *nb (the target-sync decision)
-__device__ inline void post_count_block(const PostUpdate &p) {
+// (upd, nb, eps: the three words as read before the pass, by the caller's thread 0: nothing
+// else writes them during the pass, and loading them after the last arrival was one more
+// round trip on the update's tail)
+__device__ inline void post_count_block(const PostUpdate &p, int64_t upd, int64_t nb, float eps) {
     if (threadIdx.x != 0) return;
-    const int64_t upd = *p.updates, nb = *p.nb;
-    const float eps = *p.epsilon;
     *p.epsilon = fmaxf(eps - p.decay, p.eps_end);   // utils.jl:480
     *p.updates = upd + 1;
     *p.nb = nb + 1;
+}
+__device__ inline void post_count_block(const PostUpdate &p) {
+    if (threadIdx.x != 0) return;
+    post_count_block(p, *p.updates, *p.nb, *p.epsilon);
 }
 __device__ inline void post_update_block(const PostUpdate &p) {   // 256 threads
     post_loss_block(p);

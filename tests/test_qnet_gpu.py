@@ -367,3 +367,46 @@ def test_trainer_episode_stats_fold(snk, n_envs):
     assert abs(st["reward_sum"] - rs) <= 1e-12 * max(1.0, abs(rs))
     assert tr.game.t == t0 + 60
     assert len(tr.buffer) == min(60 * n_envs, 4 * n_envs)
+
+
+_DH3_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import snake_amd as snk
+snk.load()
+rng = np.random.default_rng(6)
+m = snk.DQNModel(12, 3, n_frames=2, seed=23)
+x = rng.integers(-1, 3, size=(4096, 2, 144)).astype(np.float32)
+np.save(sys.argv[2], m(x))
+np.save(sys.argv[3], m.get_params())
+"""
+
+
+def test_dense_h3_act_forward(tmp_path):
+    """Dense1 of the 4096-state act forward on dense_h3_kernel (fp16 h3 split, per-sample
+    a3 scale from conv_h3f's epilogue, per-(position, output) weight scales from
+    w3_split_kernel) against the same forward with Dense1 on the x6 kernel (SNK_DH3=0)
+    and against the fp64 oracle: 1e-5 * max(1, |q|) both ways."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    out = {}
+    for flag in ("1", "0"):
+        env = dict(os.environ, SNK_DH3=flag)
+        q, p = tmp_path / f"q{flag}.npy", tmp_path / f"p{flag}.npy"
+        subprocess.run([sys.executable, "-c", _DH3_SCRIPT, repo, str(q), str(p)], env=env, check=True, timeout=240)
+        out[flag] = (np.load(q), np.load(p))
+    qh, p = out["1"]
+    qx, _ = out["0"]
+    assert np.array_equal(p, out["0"][1])
+    assert not np.array_equal(qh, qx), "SNK_DH3 did not switch the Dense1 kernel"
+    tol = 1e-5 * np.maximum(1.0, np.abs(qx))
+    assert (np.abs(qh - qx) <= tol).all(), float((np.abs(qh - qx) / np.maximum(1.0, np.abs(qx))).max())
+    rng = np.random.default_rng(6)
+    x = rng.integers(-1, 3, size=(4096, 2, 144)).astype(np.float32)
+    sel = np.arange(0, 4096, 16)
+    qref = oracle.qnet_forward(12, 2, p, x[sel])
+    for q in (qh, qx):
+        err = np.abs(q[sel] - qref) / np.maximum(1.0, np.abs(qref))
+        assert err.max() <= 1e-5, float(err.max())
