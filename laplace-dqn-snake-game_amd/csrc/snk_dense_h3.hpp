@@ -11,10 +11,11 @@
 //  * each position's six MFMAs (two 32-channel k-steps x hl + lh + hh) start from zero and
 //    are added into the tile's accumulator scaled by 2^-ew[kk][out] (exact: a power of two),
 //    the row scale 2^-ea comes back once at the end.
-// Grid: (S / 128 row blocks) x (slabs of KPZ positions), 4 waves of 32 rows (two 16-row tiles,
+// Grid: (S / 128 row blocks) x (slabs of KPZ positions), 8 waves of 16 rows (one 16-row tile,
 // four 16-column tiles each); slab[z][s][o] as the x6 kernel's EPI_SLAB, summed by the head.
 // B of each position (16 KB) goes through an LDS ring of 4 slots filled by LDS-DMA three
-// positions ahead; A of the next position is loaded while the current one computes. KPZ is a
+// positions ahead; A is loaded two positions ahead (the kernel is bound by the a3 stream:
+// 4 waves with one position in flight moved ~3 TB/s). KPZ is a
 // template constant and the position loop unrolled: straight-line code keeps the compiler's
 // vmcnt waits on the A registers exact (a loop back edge merged them to waits on the newest
 // loads, which also count the DMAs).
@@ -32,93 +33,86 @@ struct DenseH3Args {
     int S, nkk;
 };
 constexpr int DH3_RING = 4, DH3_SLOT = 2 * 64 * 64 * 2;   // bytes per slot: both planes of one position
+constexpr int DH3_NT = 512;                                  // 8 waves x 16 rows
 
 template <int KPZ>   // positions per slab; the launch guarantees nkk % KPZ == 0
-__global__ __launch_bounds__(256) void dense_h3_kernel(DenseH3Args a) {
+__global__ __launch_bounds__(DH3_NT) void dense_h3_kernel(DenseH3Args a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t dh3_lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
     const int z = blockIdx.y, kk0 = z * KPZ;
     const int K1 = a.nkk * 64;
-    const int row0 = blockIdx.x * 128 + wave * 32;
-    // B ring: position j of the slab in slot j % DH3_RING; 1024 16-byte pieces, 4 per lane
+    const int row0 = blockIdx.x * 128 + wave * 16;
+    // B ring: position j of the slab in slot j % DH3_RING; 1024 16-byte pieces, 2 per lane
     auto dma = [&](int j) __attribute__((always_inline)) {
         const uint16_t *src = a.w1h + (int64_t)(kk0 + j) * 2 * 4096;
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            __builtin_amdgcn_global_load_lds((const void *)(src + (u * 256 + tid) * 8),
+        for (int u = 0; u < 2; ++u)
+            __builtin_amdgcn_global_load_lds((const void *)(src + (u * 512 + tid) * 8),
                                              (__attribute__((address_space(3))) void *)(dh3_lds + (j % DH3_RING) * (DH3_SLOT / 2) +
-                                                                                         (u * 256 + wave * 64) * 8),
+                                                                                         (u * 512 + wave * 64) * 8),
                                              16, 0, 0);
     };
-    // A: rows row0 + 16t + r (clamped), channels 32ks + 8g .. +7 of position kk0 + j
-    int ar[2];
+    // A: row row0 + r (clamped), channels 32ks + 8g .. +7 of position kk0 + j
+    const int ar = min(row0 + r, a.S - 1);
+    auto aload = [&](int j, f32x4 (&x)[2][2]) __attribute__((always_inline)) {
+        const float *p = a.a3 + (int64_t)ar * K1 + (kk0 + j) * 64 + 8 * g;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) ar[t] = min(row0 + 16 * t + r, a.S - 1);
-    auto aload = [&](int j, f32x4 (&x)[2][2][2]) __attribute__((always_inline)) {
-        const int kk = kk0 + j;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                const float *p = a.a3 + (int64_t)ar[t] * K1 + kk * 64 + 32 * ks + 8 * g;
-                x[t][ks][0] = *reinterpret_cast<const f32x4 *>(p);
-                x[t][ks][1] = *reinterpret_cast<const f32x4 *>(p + 4);
-            }
+        for (int ks = 0; ks < 2; ++ks) {
+            x[ks][0] = *reinterpret_cast<const f32x4 *>(p + 32 * ks);
+            x[ks][1] = *reinterpret_cast<const f32x4 *>(p + 32 * ks + 4);
+        }
     };
-    int ea[2];
+    const int ea = h3_exp(a.a3max[ar]);
+    // the maxima of the C rows this lane writes (sample row0 + 4g + e), and the slab's B
+    // exponents of its four columns, up front (a load inside the loop would be the newest
+    // VMEM op at its use, and its wait would drain the A / B prefetches)
+    float cm[4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) ea[t] = h3_exp(a.a3max[ar[t]]);
-    // and the maxima of the C rows this lane writes (sample row0 + 16t + 4g + e), up front too
-    float cm[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cm[t][e] = a.a3max[min(row0 + 16 * t + 4 * g + e, a.S - 1)];
-    // the slab's B exponents of this lane's four columns, up front (a load inside the loop
-    // would be the newest VMEM op at its use, and its wait would drain the A / B prefetches)
+    for (int e = 0; e < 4; ++e) cm[e] = a.a3max[min(row0 + 4 * g + e, a.S - 1)];
     int ewc[KPZ][4];
 #pragma unroll
     for (int j = 0; j < KPZ; ++j)
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) ewc[j][ct] = a.w1e[(kk0 + j) * 64 + ct * 16 + r];
-    f32x4v acc[2][4];
+    f32x4v acc[4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[t][ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    // issue order (vmcnt counts loads and DMAs together, in order): B(0), B(1), A(0), B(2),
-    // then per position j: A(j+1), B(j+3). At j, A(j) and everything older (B(<= j+1)) must
-    // have landed; only B(j+2), issued after A(j), may stay in flight (4 DMAs)
-    f32x4 xa[2][2][2][2];   // [set][tile][k-step][half]
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    // issue order (vmcnt retires loads and DMAs together, in order): B(0) A(0) B(1) A(1) B(2),
+    // then per position j: A(j+2) B(j+3). At j, A(j) and everything older (B(<= j)) must have
+    // landed; B(j+1), A(j+1) and B(j+2), issued after A(j), may stay in flight
+    f32x4 xa[3][2][2];   // [set][k-step][half]
     dma(0);
-    if (KPZ > 1) dma(1);
     aload(0, xa[0]);
+    if (KPZ > 1) {
+        dma(1);
+        aload(1, xa[1]);
+    }
     if (KPZ > 2) dma(2);
 #pragma unroll
     for (int j = 0; j < KPZ; ++j) {
-        if (j + 2 < KPZ) __builtin_amdgcn_s_waitcnt(waitcnt_vm(4));
+        const int newer = (j + 1 < KPZ ? 6 : 0) + (j + 2 < KPZ ? 2 : 0);
+        if (newer == 8) __builtin_amdgcn_s_waitcnt(waitcnt_vm(8));
+        else if (newer == 6) __builtin_amdgcn_s_waitcnt(waitcnt_vm(6));
         else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of slot (j - 1) % 4 done
         __builtin_amdgcn_s_barrier();         // every wave's pieces of B(j) landed; slot (j + 3) % 4 free
-        // pinned here: left to itself the scheduler sank the A loads behind this position's
-        // MFMAs, and the next position then waited on them at its first MFMA
+        // pinned here: left to itself the scheduler sank the prefetches behind this
+        // position's MFMAs
         __builtin_amdgcn_sched_barrier(0);
-        if (j + 1 < KPZ) aload(j + 1, xa[(j + 1) & 1]);
+        if (j + 2 < KPZ) aload(j + 2, xa[(j + 2) % 3]);
         if (j + 3 < KPZ) dma(j + 3);
         __builtin_amdgcn_sched_barrier(0);
-        // A fragments: the position's 16 values per lane and tile, scaled and split
-        f16x8 ah[2][2], al[2][2];
+        // A fragments: the position's 16 values per lane, scaled and split
+        f16x8 ah[2], al[2];
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                u32x2 h0, l0, h1, l1;
-                h3_split4(xa[j & 1][t][ks][0], ea[t], h0, l0);
-                h3_split4(xa[j & 1][t][ks][1], ea[t], h1, l1);
-                ah[t][ks] = as_h(u32x4{h0[0], h0[1], h1[0], h1[1]});
-                al[t][ks] = as_h(u32x4{l0[0], l0[1], l1[0], l1[1]});
-            }
+        for (int ks = 0; ks < 2; ++ks) {
+            u32x2 h0, l0, h1, l1;
+            h3_split4(xa[j % 3][ks][0], ea, h0, l0);
+            h3_split4(xa[j % 3][ks][1], ea, h1, l1);
+            ah[ks] = as_h(u32x4{h0[0], h0[1], h1[0], h1[1]});
+            al[ks] = as_h(u32x4{l0[0], l0[1], l1[0], l1[1]});
+        }
         const uint16_t *slot = dh3_lds + (j % DH3_RING) * (DH3_SLOT / 2);
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
@@ -131,33 +125,28 @@ __global__ __launch_bounds__(256) void dense_h3_kernel(DenseH3Args a) {
                 bh[ks] = as_h(*reinterpret_cast<const u32x4 *>(slot + off));
                 bl[ks] = as_h(*reinterpret_cast<const u32x4 *>(slot + 4096 + off));
             }
+            f32x4v c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                f32x4v c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks) {
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[t][ks], bl[ks], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[t][ks], bh[ks], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[t][ks], bh[ks], c, 0, 0, 0);
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc[t][ct][e] = __builtin_fmaf(c[e], sc, acc[t][ct][e]);
+            for (int ks = 0; ks < 2; ++ks) {
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[ks], bl[ks], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[ks], bh[ks], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[ks], bh[ks], c, 0, 0, 0);
             }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[ct][e] = __builtin_fmaf(c[e], sc, acc[ct][e]);
         }
     }
     __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-    // C row 4g + e of tile t = sample row0 + 16t + 4g + e, column ct*16 + r; the row scale back
+    // C row 4g + e = sample row0 + 4g + e, column ct*16 + r; the row scale back
     float *out = a.slab + (int64_t)z * a.S * 64;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int e = 0; e < 4; ++e) {
+        const int row = row0 + 4 * g + e;
+        if (row >= a.S) continue;
+        const int ex = h3_exp(cm[e]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int row = row0 + 16 * t + 4 * g + e;
-            if (row >= a.S) continue;
-            const int ex = h3_exp(cm[t][e]);
-#pragma unroll
-            for (int ct = 0; ct < 4; ++ct) out[(int64_t)row * 64 + ct * 16 + r] = __builtin_ldexpf(acc[t][ct][e], -ex);
-        }
+        for (int ct = 0; ct < 4; ++ct) out[(int64_t)row * 64 + ct * 16 + r] = __builtin_ldexpf(acc[ct][e], -ex);
+    }
 }
 
 }  // namespace snk
