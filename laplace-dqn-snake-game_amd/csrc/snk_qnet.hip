@@ -1075,6 +1075,7 @@ bool qnet_fused23(const QLayout &L, const float *th, const float *wt, const uint
 
 static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi,
                            const SampleRider *rider = nullptr) {
+    const int lo0 = lo;   // lo as called (the fused act forward advances lo past conv3)
     const int bs = L.bs, nc = L.ncell;
     bool fresh_in[2] = {false, false};   // QWork::wmax_fresh holds for this forward only
     for (int g = 0; g < ng; ++g) {
@@ -1093,12 +1094,14 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
     // Dense1 on dense_h3_kernel: this call runs conv_h3f (which writes the per-sample a3
     // maxima) with the DMA'd weights (w3_split_kernel also splits Dense1) and then Dense1, at a
     // slab split the kernel is instantiated for
-    bool dh3 = false;
-    if (f123 && hi >= 3 && lo <= 2 && h3f_dma(L.bs)) {
+    // (prepared also when this call stops at conv3: a later Dense1-only call can use it)
+    bool dh3prep = false;
+    if (f123 && lo <= 2 && hi >= 2 && h3f_dma(L.bs)) {
         int kc;
         const int ks = d1_split(L, S, kc);
-        dh3 = dh3_ok(L, ks, kc);
+        dh3prep = dh3_ok(L, ks, kc);
     }
+    bool dh3 = dh3prep && hi >= 3;
     if (f123 && hi >= 0 && lo <= 2) {
         for (int g = 0; g < ng; ++g) {
             const FwdNet &n = net[g];
@@ -1119,8 +1122,8 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             SNK_CHECK(!rd.out || (lo <= 2 && hi >= 1), SNK_ERR_INTERNAL, "sample rider without a launch");
             if (lo <= 2 && hi >= 1 && h3f_dma(L.bs)) {   // the conv3 weights pre-split once for every workgroup
                 const int nkk = L.Wo * L.Wo;
-                w3_split_kernel<<<W3S_BLOCKS + W2S_BLOCKS + (dh3 ? w1s_blocks(nkk) : 0), 256, 0, s>>>(
-                    img, w.wmax_part, w.wmax_n, w.w3h, w.w3e, n.wt + L.off_t2, w.w2h, dh3 ? n.wt + L.off_td : nullptr,
+                w3_split_kernel<<<W3S_BLOCKS + W2S_BLOCKS + (dh3prep ? w1s_blocks(nkk) : 0), 256, 0, s>>>(
+                    img, w.wmax_part, w.wmax_n, w.w3h, w.w3e, n.wt + L.off_t2, w.w2h, dh3prep ? n.wt + L.off_td : nullptr,
                     w.w1h, w.w1e);
                 launch_check("w3_split_kernel");
             }
@@ -1135,7 +1138,7 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
                 fa.src = n.src; fa.w1 = n.th + L.off_w1; fa.b1 = n.th + L.off_b1;
                 fa.w2 = n.wt + L.off_t2; fa.b2 = n.th + L.off_b2; fa.w3 = img; fa.wmax = w.wmax_part;
                 fa.nwmax = w.wmax_n; fa.b3 = n.th + L.off_b3; fa.out = w.a3;
-                fa.a3max = dh3 ? w.a3max : nullptr;
+                fa.a3max = dh3prep ? w.a3max : nullptr;
                 conv_h3f_launch(L.bs, L.C, fa, S, s);
             }
         }
@@ -1202,6 +1205,17 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
             }
         }
         conv_fwd<32, 64, 6, 0>(io, ng, S * L.Wo * L.Wo, bs, L.Wo, s);
+    }
+    // the nets' workspaces: which of them now hold a dense_h3-ready a3 (a forward through conv3
+    // without dense_h3 leaves a3 without its maxima)
+    if (lo0 <= 2 && hi >= 2)
+        for (int g = 0; g < ng; ++g) net[g].w->dh3_ready = dh3prep ? 1 : 0;
+    if (lo0 == 3 && hi >= 3) {   // Dense1 alone (per-layer timing): dense_h3 if the last forward prepared it
+        int kc;
+        const int ks = d1_split(L, S, kc);
+        bool ready = dh3_ok(L, ks, kc);
+        for (int g = 0; g < ng; ++g) ready = ready && net[g].w->dh3_ready;
+        dh3 = ready;
     }
     if (lo <= 3 && hi >= 3 && dh3) {   // Dense1 on the h3 split, the same slab layout
         int kc;

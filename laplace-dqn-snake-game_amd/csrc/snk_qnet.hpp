@@ -78,6 +78,8 @@ struct QWork {
     uint16_t *w1h = nullptr;         // Dense1's image pre-split for dense_h3_kernel ([Wo^2][2][64][64] halves),
     int *w1e = nullptr;              //   one exponent per (position, output)
     float *a3max = nullptr;          // per-sample max of a3 (conv_h3f_kernel's epilogue), Dense1's h3 row scale
+    int dh3_ready = 0;               // a3, a3max, w1h / w1e are those of the last conv_h3f + w3_split forward
+                                     //   (a Dense1-only call, e.g. the per-layer timing, may then use dense_h3)
     double *target = nullptr, *loss = nullptr;
     int has_train = 0;
     int64_t gen = 0;          // bumped on every reallocation (captured graphs hold the old pointers)
