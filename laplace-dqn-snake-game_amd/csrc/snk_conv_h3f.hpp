@@ -690,18 +690,27 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
                 }
             }
         }
+        // per-sample maxima for Dense1's h3 scale: DPP within each 16-lane row (no readlane
+        // chain), the 4 row maxima of each wave to LDS, 32 values per sample after the barrier
+        __shared__ float a3red[8][4][4];   // [wave][row][sample]
         if (a.a3max) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                vm[e] = wave_max(vm[e]);
-                if (lane == 0) red[wave][e] = vm[e];
+                float v = vm[e];
+                v = dpp_max<0xB1>(v);
+                v = dpp_max<0x4E>(v);
+                v = dpp_max<0x141>(v);
+                v = dpp_max<0x140>(v);
+                if (r == 0) a3red[wave][g][e] = v;
             }
         }
         __syncthreads();
         if (a.a3max && tid < ns) {
-            float m = red[0][tid];
+            float m = 0.0f;
 #pragma unroll
-            for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w][tid]);
+            for (int w = 0; w < 8; ++w)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) m = fmaxf(m, a3red[w][q][tid]);
             a.a3max[s0 + tid] = m;
         }
         const int n4o = ns * ho2 * 16;
