@@ -185,6 +185,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     }
     extern __shared__ __attribute__((aligned(16))) u32x4 h3f_lds[];
     __shared__ float red[8][7];
+    __shared__ float a3red[8][4][4];   // [wave][row][sample]: the epilogue's per-sample a3 maxima
     u32x4 *Bs = h3f_lds;               // conv3 B [NBUF][NB]
     u32x4 *As = h3f_lds + NBUF * NB;   // conv3 A image; during conv2: A1 image, B2 image
     u32x2 *Bs2 = reinterpret_cast<u32x2 *>(Bs);
@@ -691,8 +692,9 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             }
         }
         // per-sample maxima for Dense1's h3 scale: DPP within each 16-lane row (no readlane
-        // chain), the 4 row maxima of each wave to LDS, 32 values per sample after the barrier
-        __shared__ float a3red[8][4][4];   // [wave][row][sample]
+        // chain), the 4 row maxima of each wave to LDS (a3red: kernel scope, as waves of
+        // different tile counts run different instantiations of this lambda), 32 values per
+        // sample after the barrier
         if (a.a3max) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
