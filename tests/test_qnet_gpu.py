@@ -385,8 +385,8 @@ np.save(sys.argv[3], m.get_params())
 def test_dense_h3_act_forward(tmp_path):
     """Dense1 of the 4096-state act forward on dense_h3_kernel (fp16 h3 split, per-sample
     a3 scale from conv_h3f's epilogue, per-(position, output) weight scales from
-    w3_split_kernel) against the same forward with Dense1 on the x6 kernel (SNK_DH3=0)
-    and against the fp64 oracle: 1e-5 * max(1, |q|) both ways."""
+    w3_split_kernel) against the same forward with Dense1 on the x6 kernel (SNK_DH3=0):
+    2e-6 * max(1, |q|) at most, 3e-7 on average; both against the fp64 oracle at 1e-5."""
     import os
     import subprocess
     import sys
@@ -401,8 +401,11 @@ def test_dense_h3_act_forward(tmp_path):
     qx, _ = out["0"]
     assert np.array_equal(p, out["0"][1])
     assert not np.array_equal(qh, qx), "SNK_DH3 did not switch the Dense1 kernel"
-    tol = 1e-5 * np.maximum(1.0, np.abs(qx))
-    assert (np.abs(qh - qx) <= tol).all(), float((np.abs(qh - qx) / np.maximum(1.0, np.abs(qx))).max())
+    # measured spread of the two exact-split paths: max 3.7e-7, mean 6.9e-8 (round 4); a wrong
+    # row or column scale (the round-4 a3-max bug) shows up far above these bounds
+    rel = np.abs(qh - qx) / np.maximum(1.0, np.abs(qx))
+    print(f"dense_h3 vs x6: max {rel.max():.3e}, mean {rel.mean():.3e}")
+    assert rel.max() <= 2e-6 and rel.mean() <= 3e-7, (float(rel.max()), float(rel.mean()))
     rng = np.random.default_rng(6)
     x = rng.integers(-1, 3, size=(4096, 2, 144)).astype(np.float32)
     sel = np.arange(0, 4096, 16)
