@@ -49,9 +49,10 @@ def update_flop(B: int, bs: int, C: int) -> float:
     """Algorithmic FLOP of one B-sample DQN update (BASELINE.md's DQN-update row,
     4 B F): forward of q_net and of t_net over the batch (2 F each sample) and
     the backward of q_net (2 F: dX and dW). F = the fused conv stack + Dense
-    3136->256 + Dense 256->3 of one state."""
+    Wo^2*64 -> 64 + Dense 64 -> 3 of one state (the reference net,
+    structs.jl:133-134): 9,037,184 at 12x12, C = 2, so 2,313,519,104 at B = 64."""
     wo = bs - 5
-    f = act_forward_flop(1, bs, C) + 2.0 * (wo * wo * 64 * 256 + 256 * 3)
+    f = act_forward_flop(1, bs, C) + 2.0 * (wo * wo * 64 * 64 + 64 * 3)
     return 4.0 * B * f
 
 
@@ -614,8 +615,7 @@ def main():
                    "hipgraph": graph,
                    "gemm_arithmetic": ("act-forward conv2 + conv3: f32 operands as fp16 hi/lo parts of power-of-two-scaled "
                                        "values, 3 f16 MFMA products; other GEMMs: 3-way bf16 split, 6 bf16 MFMA "
-                                       "products; f32 accumulation throughout" if os.environ.get("SNK_CONV", "") != "fp32"
-                                       else "native f32 MFMA")},
+                                       "products; f32 accumulation throughout")},
         "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
                         "food_faults": faults},
         "roofline": None,
@@ -643,11 +643,11 @@ def main():
         dom_ms = loop_ms.value if loop_ms.value > 0 else ms[2]
         tf = flop_dom / (dom_ms * 1e-3) / 1e12
         # the forward GEMMs run fp32 products as 6 exact bf16 split products on the
-        # bf16 MFMA (SNK_CONV=fp32: native f32 MFMA): the fp32-equivalent peak is
+        # bf16 MFMA (snk.arith(conv_fp32=True): native f32 MFMA): the fp32-equivalent peak is
         # the bf16 dense peak / 6
-        x6 = os.environ.get("SNK_CONV", "") != "fp32"
+        x6 = not snk.get_arith("conv_fp32")
         # >= 1024 samples at bs 8..13: conv_h3s_kernel (3 fp16 products per fp32 product)
-        h3 = x6 and os.environ.get("SNK_H3S", "1") != "0" and n >= 1024 and 8 <= bs <= 13
+        h3 = x6 and snk.get_arith("h3s") and n >= 1024 and 8 <= bs <= 13
         nprod = H3_PRODUCTS if h3 else X6_PRODUCTS
         peak = PEAK_BF16_TFLOPS / nprod if x6 else PEAK_FP32_TFLOPS
         kname = ("conv_h3f_kernel: conv1 (fp32 VALU) + conv2 + conv3 (fp16 h3 split on v_mfma_f32_16x16x32_f16) "

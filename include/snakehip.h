@@ -46,6 +46,21 @@ int snk_set_device(int32_t device);
 /* hipStream_t to enqueue on; NULL restores the library's own stream */
 int snk_set_stream(void *hip_stream);
 int snk_synchronize(void);
+/* GEMM arithmetic selection, process-wide (no reference counterpart: the
+ * reference computes in Flux fp32). Every knob defaults to the production
+ * path; tests switch one to compare the production kernel against an
+ * alternative of the same error class. Read when a kernel is launched (a
+ * captured trainer graph keeps what it was captured with); SNK_ARITH_CONV_FP32
+ * is read when a model is created. value: 0 or 1. */
+#define SNK_ARITH_X6S 0          /* 1: conv3 x6 forward on conv_x6s (4 samples in LDS); 0: x6m16 */
+#define SNK_ARITH_H3S 1          /* 1: act-forward conv3 on the fp16 h3 split; 0: bf16 x6 */
+#define SNK_ARITH_DH3 2          /* 1: act-forward Dense1 on dense_h3_kernel; 0: x6 GEMM */
+#define SNK_ARITH_H3C2 3         /* 1: conv2 fused into the h3 act forward (conv_h3f); 0: conv3 only */
+#define SNK_ARITH_CONV_FP32 4    /* 1: models created from now on use native f32 MFMA (no split) */
+#define SNK_ARITH_SYRK_H3_32 5   /* 1: Jacobian Gram on the round-2 32x32x16 kernel; 0: syrk_h3q */
+#define SNK_ARITH_COUNT 6
+int snk_set_arith(int32_t knob, int32_t value);
+int snk_get_arith(int32_t knob, int32_t *value_out);
 int snk_malloc(void **dev_out, int64_t bytes);
 int snk_free(void *dev);
 int snk_memcpy_h2d(void *dst_dev, const void *src_host, int64_t bytes);
@@ -218,7 +233,7 @@ typedef struct {
     double gamma;               /* 0.97 (utils.jl:451) */
     uint64_t seed;              /* counter-RNG seed for actions and sampling */
     int64_t loss_log_capacity;  /* ring of per-update losses (tr.losses) */
-    int32_t graph_unroll;       /* lockstep iterations per captured hipGraph (0 = 8) */
+    int32_t graph_unroll;       /* lockstep iterations per captured hipGraph (0 = 8, at most 64) */
 } snk_trainer_cfg_t;
 typedef struct {
     int32_t struct_size;        /* = sizeof(snk_trainer_stats_t) = 80, set by the caller */
@@ -248,8 +263,8 @@ int snk_trainer_set_nb(snk_trainer t, int64_t nb);
  * of snk_dqn_buffer_ptr) is also copied to grad_ring_dev + slot * P, where
  * slot = (i x updates_per_iter + u) % slots for update u of iteration i, and i counts
  * the iterations of ONE launch sequence: within a captured graph (a graph replay
- * restarts at i = 0: graphs of graph_unroll iterations, then single-iteration graphs
- * for the remainder) or within an eager snk_trainer_run call (i = 0, 1, ... mod 2^20).
+ * restarts at i = 0: graphs of graph_unroll iterations, then one graph of the
+ * remaining iterations; only the latest remainder length stays cached) or within an eager snk_trainer_run call (i = 0, 1, ... mod 2^20).
  * A ring of graph_unroll x updates_per_iter slots therefore maps one graph replay
  * slot for slot. One device-to-device copy per update, appended to the same graphs
  * (which are re-captured). NULL turns it off. */

@@ -5,7 +5,7 @@ directory to that name). All compute runs in libsnakehip.so (HIP, gfx950);
 this package is the host-side mirror of the reference's Julia API.
 """
 from ._lib import (BufferSizeError, DeviceArray, FoodListExhausted, SnakeHipError,  # noqa: F401
-                   device_count, header_symbols, load)
+                   arith, device_count, get_arith, header_symbols, load, set_arith)
 from .env import (ALL_ACTIONS, D, L, NULL_ACTION, R, U, SnakeGame, assemble_state_,  # noqa: F401
                   available_action_codes, available_actions, food_list, reset_, step_,
                   step_indices_dev, synth_actions_dev, virtual_step)

@@ -58,6 +58,8 @@ _PROTOS = {
     "snk_set_device": [i32],
     "snk_set_stream": [vp],
     "snk_synchronize": [],
+    "snk_set_arith": [i32, i32],
+    "snk_get_arith": [i32, P(i32)],
     "snk_malloc": [P(vp), i64],
     "snk_free": [vp],
     "snk_memcpy_h2d": [vp, vp, i64],
@@ -223,6 +225,43 @@ def ptr(a: np.ndarray | None):
         return None
     assert a.flags["C_CONTIGUOUS"], "host arrays must be C-contiguous"
     return a.ctypes.data_as(vp)
+
+
+# snk_set_arith knobs (include/snakehip.h SNK_ARITH_*): name -> knob
+ARITH = {"x6s": 0, "h3s": 1, "dh3": 2, "h3c2": 3, "conv_fp32": 4, "syrk_h3_32": 5}
+
+
+def set_arith(name: str, value: bool) -> bool:
+    """Select a GEMM arithmetic path process-wide (SNK_ARITH_*); returns the previous
+    value. Production defaults: x6s, h3s, dh3, h3c2 on; conv_fp32, syrk_h3_32 off."""
+    old = get_arith(name)
+    call("snk_set_arith", ARITH[name], int(bool(value)))
+    return old
+
+
+def get_arith(name: str) -> bool:
+    v = i32(0)
+    call("snk_get_arith", ARITH[name], C.byref(v))
+    return bool(v.value)
+
+
+class arith:
+    """Context manager: `with arith(dh3=False): ...` runs the block on the
+    comparison path and restores the previous selection."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.old[k] = set_arith(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_arith(k, v)
+        return False
 
 
 def device_count() -> int:

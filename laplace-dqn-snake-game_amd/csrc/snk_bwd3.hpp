@@ -171,7 +171,7 @@ __device__ __forceinline__ void c3_dx_block(const Conv3BwdArgs &a, int s, int cg
     uint16_t *Wh = reinterpret_cast<uint16_t *>(sm), *Wl = Wh + NN * 64;
     uint16_t *Dh = Wl + NN * 64, *Dl = Dh + WO2 * 64;
     float *Tl = sm;
-    __shared__ float red[4][2];
+    __shared__ float red[4][2];   // lds: one per kernel (conv3_bwd / conv2_bwd call this block helper once)
     // relu-mask values of this block's outputs, loaded now (used by the col2im)
     float mk[NMK];
 #pragma unroll
@@ -473,7 +473,7 @@ __device__ __forceinline__ void c2_dx_block(const Conv2BwdArgs &a, int s, int xb
     uint16_t *Dh = reinterpret_cast<uint16_t *>(sm), *Dl = Dh + npos * C2X_PS;
     uint16_t *Wh = Dl + npos * C2X_PS, *Wl = Wh + 144 * 32;
     float *Xb = reinterpret_cast<float *>(Wl + 144 * 32);
-    __shared__ float red[4][2];
+    __shared__ float red[4][2];   // lds: one per kernel (conv3_bwd / conv2_bwd call this block helper once)
     // dz2[s] (bs^2 x 32) and W2 [kk][ci][co] (144 x 32) into registers: 8 float4 per position,
     // 8 per weight row (boards up to 13 x 13 fit NU; larger ones read the rest twice from L2)
     constexpr int NU = 6;   // 169 * 8 = 1352 <= 6 * 256

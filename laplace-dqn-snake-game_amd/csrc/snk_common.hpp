@@ -17,6 +17,10 @@ namespace snk {
 
 void set_error(const char *fmt, ...);
 hipStream_t stream();   // the library's current stream (snk_set_stream)
+// process-wide GEMM arithmetic selection (snk_set_arith, include/snakehip.h): the
+// production kernels unless a test selects a comparison path; read at launch
+// (a captured graph keeps the kernels it was captured with)
+int arith(int knob);
 
 struct Error {
     int code;

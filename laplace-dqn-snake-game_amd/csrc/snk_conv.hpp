@@ -60,7 +60,7 @@ __device__ __forceinline__ void conv_mfma_body(const ConvPair &pr, dim3 bid) {
     constexpr int KB = CK / 8;
     constexpr int LDB = CK + 4;
     constexpr int NV = (CK * CN / 4 + 255) / 256;  // float4 staging loads per thread
-    __shared__ __attribute__((aligned(16))) float Bs[2][CN * LDB + 4];   // + pad slot for idle stagers
+    __shared__ __attribute__((aligned(16))) float Bs[2][CN * LDB + 4];   // + pad slot for idle stagers; lds: one per kernel (a paired launch's two bodies never share it)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;

@@ -91,7 +91,7 @@ __device__ __forceinline__ void conv_x6_body(const ConvPair &pr, dim3 bid) {
     constexpr int PLANE = CN * LDB;              // bf16 per LDS plane
     constexpr int NE = BSPLIT ? CN * CK / 8 : 3 * CN * CK / 8;   // staged units per block: 8-channel
     constexpr int NV = (NE + 255) / 256;                          //   pieces (BSPLIT) or 16-byte plane pieces
-    __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * PLANE + 8];   // + pad piece for idle stagers
+    __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * PLANE + 8];   // + pad piece for idle stagers; lds: one per kernel (a paired launch's two bodies never share it)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 31, h = lane >> 5;

@@ -209,9 +209,8 @@ extern "C" int snk_dqn_create(snk_dqn *out, int32_t bs, int32_t C, float lr, flo
         SNK_HIP(hipMemcpyAsync(h->tmp, flux.data(), P * 4, hipMemcpyHostToDevice, s));
         h->wt_q = dalloc<float>(h->L.T);
         h->wt_t = dalloc<float>(h->L.T);
-        // forward GEMMs on the exact bf16x6 split (default) or plain fp32 MFMA (SNK_CONV=fp32)
-        const char *cm = getenv("SNK_CONV");
-        if (!(cm && strcmp(cm, "fp32") == 0)) {
+        // forward GEMMs on the exact bf16x6 split (default) or plain fp32 MFMA (SNK_ARITH_CONV_FP32)
+        if (!arith(SNK_ARITH_CONV_FP32)) {
             h->wtb_q = dalloc<uint16_t>(3 * h->L.T);
             h->wtb_t = dalloc<uint16_t>(3 * h->L.T);
         }

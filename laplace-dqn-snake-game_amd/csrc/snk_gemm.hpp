@@ -29,7 +29,7 @@ __device__ __forceinline__ int acc_row(int g, int lane) { return (g & 3) + 8 * (
 template <int NT, int KW, class AL, class BL, class EP>
 __device__ __forceinline__ void gemm_body(const AL &al, const BL &bl, const EP &ep, int M, int K, int kchunk,
                                           dim3 bid) {
-    __shared__ float red[KW > 1 ? KW * NT * 16 * 64 : 1];
+    __shared__ float red[KW > 1 ? KW * NT * 16 * 64 : 1];   // lds: one per kernel (a paired launch's two bodies never share it)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m0 = bid.x * 32;
     const int r = lane & 31, h = lane >> 5;

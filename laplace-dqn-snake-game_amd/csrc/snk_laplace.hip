@@ -231,9 +231,9 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s, int r
     dim3 grid((unsigned)a.ntiles, (unsigned)z);
     if (a.xh) {   // pre-split rows (h3): fp16 parts, 3 products per fp32 product
         SNK_CHECK(out == SYRK_F32 && z == 1 && a.ldh % SY_KS == 0 && a.xe, SNK_ERR_INTERNAL, "syrk h3 arguments");
-        // production: syrk_h3q_kernel (v_mfma_f32_16x16x32_f16); SNK_SYRK=h3 selects the
-        // round-2 32x32x16 kernel (same results class, parity-tested)
-        static const char *kind = getenv("SNK_SYRK");
+        // production: syrk_h3q_kernel (v_mfma_f32_16x16x32_f16); SNK_ARITH_SYRK_H3_32 selects
+        // the round-2 32x32x16 kernel (same results class, parity-tested)
+        const bool h3_32 = arith(SNK_ARITH_SYRK_H3_32) != 0;
 #ifdef SNK_SYRK_MEASURE
         // measurement build only (make measure: libsnakehip_measure.so, never shipped):
         // SNK_SYRK_VAR = 1 / 2 run the kernel without MFMAs / without stage DMAs, i.e.
@@ -242,7 +242,7 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s, int r
 #else
         constexpr int var = 0;
 #endif
-        if (!(kind && !strcmp(kind, "h3"))) {
+        if (!h3_32) {
 #ifdef SNK_SYRK_MEASURE
             if (var == 1) syrk_h3q_kernel<1><<<grid, 512, 0, s>>>(a);
             else if (var == 2) syrk_h3q_kernel<2><<<grid, 512, 0, s>>>(a);

@@ -260,8 +260,8 @@ static void conv_launch(const ConvArgs *ga, int ng, int splits, hipStream_t s, c
                 if (a.xb) {   // pre-split input, 32-channel chunks: the 16x16x32 layouts
                     if constexpr (CN == 64 && PAD == 0 && CK == 32 && KS == 6 && EPI == EPI_BIAS_RELU) {
                         // large batches: four samples' planes resident in LDS per workgroup
-                        // SNK_X6S=0 (tests): x6m16 instead, the same sums in the same order
-                        static const bool x6s = !getenv("SNK_X6S") || atoi(getenv("SNK_X6S")) != 0;
+                        // SNK_ARITH_X6S = 0 (tests): x6m16 instead, the same sums in the same order
+                        const bool x6s = arith(SNK_ARITH_X6S) != 0;
                         constexpr int smin = 1024;
                         const int ho2 = a.HOUT * a.HOUT;
                         const int S = a.M / ho2;
@@ -963,9 +963,9 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
 // ---------------------------------------------------------------- forward
 // conv1 .. Dense1 (layers lo..hi) of ng nets over S samples each, one launch per layer
 // conv3 of this forward on the fp16 h3 kernel (snk_conv_h3.hpp): split-precision
-// (x6) nets, large batches, one unsplit launch. SNK_H3S=0: the bf16 x6 kernels.
+// (x6) nets, large batches, one unsplit launch. SNK_ARITH_H3S = 0: the bf16 x6 kernels.
 static bool h3s_ok(const QLayout &L, const FwdNet *net, int ng, int64_t S) {
-    static const bool on = !getenv("SNK_H3S") || atoi(getenv("SNK_H3S")) != 0;   // tests: x6 comparisons
+    const bool on = arith(SNK_ARITH_H3S) != 0;   // tests: x6 comparisons
     constexpr int smin = 1024;
     for (int g = 0; g < ng; ++g)
         if (!net[g].wtb) return false;
@@ -1004,7 +1004,7 @@ static bool h3f_dma(int bs) { return bs <= 12; }
 
 // dense_h3_kernel instantiations: KPZ positions per slab (d1_split's kk_per), all slabs full
 static bool dh3_ok(const QLayout &L, int ks, int kpz) {
-    static const bool on = !getenv("SNK_DH3") || atoi(getenv("SNK_DH3")) != 0;   // tests: x6 comparisons
+    const bool on = arith(SNK_ARITH_DH3) != 0;   // tests: x6 comparisons
     return on && kpz == 7 && ks * kpz == L.Wo * L.Wo;
 }
 static void dh3_launch(const DenseH3Args &a, int ks, int kpz, hipStream_t s) {
@@ -1062,10 +1062,7 @@ static void conv_h3c2_launch(const QLayout &L, const FwdNet &n, int64_t S, hipSt
     }
 }
 
-static bool h3c2_on() {
-    static const bool on = !getenv("SNK_H3C2") || atoi(getenv("SNK_H3C2")) != 0;
-    return on;
-}
+static bool h3c2_on() { return arith(SNK_ARITH_H3C2) != 0; }
 
 // whether an act forward (no training work) of S samples runs conv2 + conv3 as conv_h3f_kernel
 bool qnet_fused23(const QLayout &L, const float *th, const float *wt, const uint16_t *wtb, int64_t S, QWork &w) {
@@ -1667,9 +1664,13 @@ struct UpdArgs {
 // section): the sum of their K-split slabs (z ascending, float4 slab loads, sixteen in
 // flight per batch) or the value already there
 // (part / nparts: only slabs [zc * part / nparts, zc * (part + 1) / nparts), for blocks that
-// split a parameter's slab run over several threads)
+// split a parameter's slab run over several threads). Where no K-split covers the
+// parameters (z <= 1: the gradient was written straight into grad, e.g. conv2's one-slab
+// plan at B = 1), part 0 returns grad and the other parts zero, so the parts still sum to
+// the gradient.
 __device__ __forceinline__ f32x4 finish4(const UpdArgs &a, int64_t i0, int part = 0, int nparts = 1) {
-    f32x4 g = *reinterpret_cast<const f32x4 *>(a.grad + i0);
+    f32x4 g = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (part == 0) g = *reinterpret_cast<const f32x4 *>(a.grad + i0);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int64_t j = i0 - a.g.off[k];
@@ -1733,8 +1734,8 @@ static_assert(GU_WMAX_BLOCKS == 36 * (32 / GU_ROWS), "conv3 image blocks");
 // wmax: where this block's max |new theta| goes (the conv3 section, UpdateTarget::wmax_out)
 __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb, bool due, float omr,
                                float *wmax = nullptr) {
-    __shared__ __attribute__((aligned(16))) float th_s[GU_ROWS * 64];
-    __shared__ float red4[4];
+    __shared__ __attribute__((aligned(16))) float th_s[GU_ROWS * 64];   // lds: one per kernel (grad_update_kernel only)
+    __shared__ float red4[4];   // lds: one per kernel (grad_update_kernel only)
     const int CN = S.CN, n_el = GU_ROWS * CN;
     const int64_t p0 = S.off + ((int64_t)kk * S.CK + cb * GU_ROWS) * CN;   // a multiple of 4
     float m = 0.0f;
@@ -1744,7 +1745,7 @@ __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb,
     const bool split = a.finish && n_el == 512;
     f32x4 g2 = {0.0f, 0.0f, 0.0f, 0.0f};
     if (split) {
-        __shared__ f32x4 part[128];
+        __shared__ f32x4 part[128];   // lds: one per kernel (grad_update_kernel only)
         const int grp = threadIdx.x & 127, hf = threadIdx.x >> 7;
         const f32x4 pv = finish4(a, p0 + 4 * grp, hf, 2);
         if (hf) part[grp] = pv;

@@ -197,7 +197,7 @@ struct PostUpdate {
 // only what the update's earlier launches wrote and *updates, which nothing but the
 // bookkeeping below advances, so any block of the update pass may run it
 __device__ inline void post_loss_block(const PostUpdate &p) {   // 256 threads
-    __shared__ double sh[256];
+    __shared__ double sh[256];   // lds: one per kernel (one caller per update kernel)
     int64_t upd = 0;
     if (threadIdx.x == 0 && p.log) upd = *p.updates;
     double v = 0.0;

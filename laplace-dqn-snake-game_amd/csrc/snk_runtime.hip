@@ -14,6 +14,8 @@ namespace snk {
 static thread_local std::string g_err;
 static thread_local hipStream_t g_user_stream = nullptr;
 static thread_local bool g_user_stream_set = false;
+// snk_set_arith knobs, production defaults (SNK_ARITH_* in include/snakehip.h)
+static int g_arith[SNK_ARITH_COUNT] = {1, 1, 1, 1, 0, 0};
 static hipStream_t g_own_stream[64] = {};
 
 void set_error(const char *fmt, ...) {
@@ -36,6 +38,8 @@ void set_lds_limit(const void *kernel, size_t bytes) {
     SNK_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     have = bytes;
 }
+
+int arith(int knob) { return g_arith[knob]; }
 
 hipStream_t stream() {
     if (g_user_stream_set) return g_user_stream;
@@ -174,6 +178,22 @@ extern "C" int snk_set_stream(void *s) {
     return guard([&] {
         g_user_stream = reinterpret_cast<hipStream_t>(s);
         g_user_stream_set = s != nullptr;
+    });
+}
+
+extern "C" int snk_set_arith(int32_t knob, int32_t value) {
+    return guard([&] {
+        SNK_CHECK(knob >= 0 && knob < SNK_ARITH_COUNT, SNK_ERR_INVALID, "unknown arithmetic knob %d", knob);
+        SNK_CHECK(value == 0 || value == 1, SNK_ERR_INVALID, "arithmetic knob %d: value %d is not 0 or 1", knob,
+                  value);
+        g_arith[knob] = value;
+    });
+}
+
+extern "C" int snk_get_arith(int32_t knob, int32_t *value) {
+    return guard([&] {
+        SNK_CHECK(value && knob >= 0 && knob < SNK_ARITH_COUNT, SNK_ERR_INVALID, "unknown arithmetic knob %d", knob);
+        *value = g_arith[knob];
     });
 }
 

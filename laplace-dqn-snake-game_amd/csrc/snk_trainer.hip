@@ -60,7 +60,8 @@ struct snk_trainer_s {
     // through device counters, so a longer graph is the same launch sequence with the
     // per-graph launch gap and the first iteration's weight-max scan paid once per graph):
     // n = `unroll`, and n = the remainder of a run that is not a multiple of it (one graph
-    // for the tail instead of one single-iteration graph per leftover iteration)
+    // for the tail instead of one single-iteration graph per leftover iteration; only the
+    // most recent tail length stays cached per learn mode, see snk_trainer_run)
     static constexpr int MAXG = 64;
     hipGraph_t graph[2][MAXG + 1] = {};
     hipGraphExec_t exec[2][MAXG + 1] = {};
@@ -231,6 +232,9 @@ extern "C" int snk_trainer_create(snk_trainer *out, snk_env env, snk_dqn dqn, sn
         // counters, so a longer graph is the same launch sequence with the
         // graph launch gap paid once per `unroll` (measured 12.34 M env-steps/s
         // at 8 against 12.28 M at 1)
+        SNK_CHECK(cfg->graph_unroll <= snk_trainer_s::MAXG, SNK_ERR_INVALID,
+                  "graph_unroll %d: at most %d iterations per captured graph", cfg->graph_unroll,
+                  snk_trainer_s::MAXG);
         h->unroll = cfg->graph_unroll > 0 ? cfg->graph_unroll : 8;
         TrainStats st{};
         st.epsilon = cfg->epsilon;
@@ -306,8 +310,21 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
         if (learn && upi > 0) trainer_check_replay(h);
         trainer_refresh(h);
         const int g = learn ? 1 : 0;
+        const int U = h->unroll;
         auto capture = [&](int n) {   // the n-iteration graph, captured once
             if (h->exec[g][n]) return h->exec[g][n];
+            if (n != U) {   // a new tail length: drop the previous tail graph (each holds n iterations)
+                bool sync = false;
+                for (int m = 1; m <= snk_trainer_s::MAXG; ++m) {
+                    if (m == U || !h->exec[g][m]) continue;
+                    if (!sync) SNK_HIP(hipStreamSynchronize(s));
+                    sync = true;
+                    (void)hipGraphExecDestroy(h->exec[g][m]);
+                    (void)hipGraphDestroy(h->graph[g][m]);
+                    h->exec[g][m] = nullptr;
+                    h->graph[g][m] = nullptr;
+                }
+            }
             SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             try {
                 for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s, i, i > 0, i + 1 < n);
@@ -325,7 +342,6 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
                 trainer_iteration(h, learn != 0, upi, s, (int)(i % (1 << 20)), i > 0, i + 1 < iters);
             return;
         }
-        const int U = std::min(h->unroll, (int)snk_trainer_s::MAXG);
         if (U <= 1) {
             hipGraphExec_t e = capture(1);
             for (int64_t i = 0; i < iters; ++i) SNK_HIP(hipGraphLaunch(e, s));

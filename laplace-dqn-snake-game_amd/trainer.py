@@ -93,6 +93,9 @@ class Trainer:
         if ring is None:
             call("snk_trainer_set_trace", self._h, None, 0)
         else:
+            if ring.dtype != np.float32 or len(ring.shape) != 2 or ring.shape[1] != self.model.P:
+                raise ValueError(f"gradient trace ring must be float32 [slots, {self.model.P}], got "
+                                 f"{ring.dtype} {ring.shape}")
             call("snk_trainer_set_trace", self._h, ring.ptr, int(ring.shape[0]))
         self._trace = ring
 
@@ -104,6 +107,12 @@ class Trainer:
         if acts is None:
             call("snk_trainer_set_act_trace", self._h, None, None, 0)
         else:
+            # the library copies n_envs bytes (and n_envs x 3 floats) per slot inside the
+            # captured graphs: a smaller ring would be written out of bounds
+            if acts.dtype != np.uint8 or len(acts.shape) != 2 or acts.shape[1] != self.game.n_envs:
+                raise ValueError(f"act trace ring must be uint8 [slots, {self.game.n_envs}], got {acts.dtype} {acts.shape}")
+            if q is not None and (q.dtype != np.float32 or tuple(q.shape[1:]) != (self.game.n_envs, 3)):
+                raise ValueError(f"Q trace ring must be float32 [slots, {self.game.n_envs}, 3], got {q.dtype} {q.shape}")
             if q is not None and q.shape[0] != acts.shape[0]:
                 raise ValueError("act and Q trace rings need the same slot count")
             call("snk_trainer_set_act_trace", self._h, acts.ptr, q.ptr if q is not None else None,

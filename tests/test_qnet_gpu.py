@@ -110,11 +110,14 @@ def test_loss_and_grad_vs_oracle(snk, bs, C):
     assert loss2 == loss and np.array_equal(m.grad, grad)
 
 
-@pytest.mark.parametrize("bs,B", [(12, 37), (13, 64), (8, 5)])
+@pytest.mark.parametrize("bs,B", [(12, 37), (13, 64), (8, 5), (12, 1), (10, 1), (12, 3)])
 def test_conv3_backward_odd_batches_vs_oracle(snk, bs, B):
     """conv3_bwd_kernel (snk_bwd3.hpp): two-sample weight-gradient chunks (an odd
     batch leaves a one-sample chunk), the data gradient's dense GEMM + col2im,
-    at the smallest and largest boards it takes (Wo 3 and 8) and between."""
+    at the smallest and largest boards it takes (Wo 3 and 8) and between.
+    B = 1: conv2's gradient plan has a single slab (written straight into grad,
+    no K-split), which grad_update_kernel's two-thread conv2 finish once counted
+    twice (a doubled conv2 gradient and RMSProp step at B = 1)."""
     g, rb = _random_replay(snk, bs, 2, n=48, T=6, seed=bs)
     m = snk.DQNModel(bs, 3, n_frames=2, seed=bs + 3)
     rng = np.random.default_rng(B)
@@ -187,17 +190,16 @@ def test_trainer_schedule_and_graph_determinism(snk):
 
 
 @pytest.mark.parametrize("bs,C,B", [(12, 2, 300), (10, 1, 257)])
-def test_x6_split_forward_matches_fp32_and_oracle(snk, bs, C, B, monkeypatch):
+def test_x6_split_forward_matches_fp32_and_oracle(snk, bs, C, B):
     """The bf16x6 split-precision forward (default) has the error class of the
-    exact-fp32 MFMA forward (SNK_CONV=fp32): at the init scale both meet the
+    exact-fp32 MFMA forward (snk.arith(conv_fp32=True)): at the init scale both meet the
     1e-5 bar against the fp64 oracle; with 3x larger weights (|Q| ~ 100 with
     heavy cancellation, where fp32 itself exceeds 1e-5) the x6 error stays
     within 2x the fp32 error, element-max and mean."""
     rng = np.random.default_rng(bs * 100 + B)
     m6 = snk.DQNModel(bs, 3, n_frames=C, seed=5)
-    monkeypatch.setenv("SNK_CONV", "fp32")
-    m32 = snk.DQNModel(bs, 3, n_frames=C, seed=5)
-    monkeypatch.delenv("SNK_CONV")
+    with snk.arith(conv_fp32=True):
+        m32 = snk.DQNModel(bs, 3, n_frames=C, seed=5)
     x = rng.integers(-1, 3, size=(B, C, bs * bs)).astype(np.float32)
     p0 = m6.get_params()
     for scale in (1.0, 3.0):
@@ -243,10 +245,10 @@ def test_large_batch_forward_h3_board_sizes(snk, bs, C):
 
 
 @pytest.mark.parametrize("scale", [1.0, 3.0, 1e-3, 40.0])
-def test_h3s_error_class_vs_fp32(snk, scale, monkeypatch):
+def test_h3s_error_class_vs_fp32(snk, scale):
     """The h3 conv3 (fp16 parts of power-of-two-scaled operands, 3 MFMAs per
     product) keeps the error class of the exact-fp32 MFMA forward
-    (SNK_CONV=fp32) across weight scales that move activations over 10+
+    (snk.arith(conv_fp32=True)) across weight scales that move activations over 10+
     binades (1e-3x: tiny activations, where unscaled fp16 would underflow;
     40x: |Q| ~ 1e8, where it would overflow): element-max and mean error
     against the fp64 oracle within 4x the fp32 forward's (its operands carry
@@ -255,9 +257,8 @@ def test_h3s_error_class_vs_fp32(snk, scale, monkeypatch):
     bs, C, B = 12, 2, 1030
     rng = np.random.default_rng(7)
     mh = snk.DQNModel(bs, 3, n_frames=C, seed=5)
-    monkeypatch.setenv("SNK_CONV", "fp32")
-    m32 = snk.DQNModel(bs, 3, n_frames=C, seed=5)
-    monkeypatch.delenv("SNK_CONV")
+    with snk.arith(conv_fp32=True):
+        m32 = snk.DQNModel(bs, 3, n_frames=C, seed=5)
     x = rng.integers(-1, 3, size=(B, C, bs * bs)).astype(np.float32)
     p = mh.get_params() * np.float32(scale)
     mh.set_params(p)
@@ -275,37 +276,24 @@ def test_h3s_error_class_vs_fp32(snk, scale, monkeypatch):
     assert eh.mean() <= 4 * e32.mean() + 1e-8, (scale, eh.mean(), e32.mean())
 
 
-_X6S_SCRIPT = r"""
-import sys, numpy as np
-sys.path.insert(0, sys.argv[1])
-import snake_amd as snk
-snk.load()
-rng = np.random.default_rng(4)
-m = snk.DQNModel(12, 3, n_frames=2, seed=21)
-x = rng.integers(-1, 3, size=(2050, 2, 144)).astype(np.float32)
-np.save(sys.argv[2], m(x))
-"""
-
-
-def test_x6s_bitexact_with_x6m16_and_h3s_close(tmp_path):
-    """With the h3 kernel off (SNK_H3S=0), conv_x6s accumulates the six part
-    products in x6m16's order: the Q values of a 2050-sample forward are
-    identical with SNK_X6S=1 and 0. The default forward (conv2 and conv3 on
-    h3) and the h3-conv3-only one (SNK_H3C2=0) agree with them to
-    1e-5 * max(1, |q|)."""
-    import os
-    import subprocess
-    import sys
-    repo = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+def test_x6s_bitexact_with_x6m16_and_h3s_close(snk):
+    """With the h3 kernel off (snk.arith(h3s=False)), conv_x6s accumulates the six
+    part products in x6m16's order: the Q values of a 2050-sample forward are
+    identical with x6s on and off. The default forward (conv2 and conv3 on h3)
+    and the h3-conv3-only one (h3c2=False) agree with them to 1e-5 * max(1, |q|).
+    The knobs are the snk_set_arith ABI call (no environment variable changes the
+    shipping library's arithmetic)."""
     out = {}
-    for tag, envs in (("x6s", {"SNK_H3S": "0", "SNK_X6S": "1"}), ("m16", {"SNK_H3S": "0", "SNK_X6S": "0"}),
-                      ("h3c3", {"SNK_H3C2": "0"}), ("h3s", {})):
-        f = str(tmp_path / f"q{tag}.npy")
-        env = dict(os.environ, **envs)
-        subprocess.run([sys.executable, "-c", _X6S_SCRIPT, repo, f], env=env, check=True, timeout=300)
-        out[tag] = np.load(f)
+    for tag, knobs in (("x6s", dict(h3s=False, x6s=True)), ("m16", dict(h3s=False, x6s=False)),
+                       ("h3c3", dict(h3c2=False)), ("h3s", {})):
+        rng = np.random.default_rng(4)
+        m = snk.DQNModel(12, 3, n_frames=2, seed=21)
+        x = rng.integers(-1, 3, size=(2050, 2, 144)).astype(np.float32)
+        with snk.arith(**knobs):
+            out[tag] = m(x)
     assert np.array_equal(out["x6s"], out["m16"])
     assert _qclose(out["h3s"], out["x6s"]) and _qclose(out["h3c3"], out["x6s"])
+    assert not np.array_equal(out["h3s"], out["x6s"]), "snk.arith(h3s=False) did not switch the conv3 kernel"
 
 
 def test_train_episode_schedule(snk):
@@ -369,38 +357,23 @@ def test_trainer_episode_stats_fold(snk, n_envs):
     assert len(tr.buffer) == min(60 * n_envs, 4 * n_envs)
 
 
-_DH3_SCRIPT = r"""
-import sys, numpy as np
-sys.path.insert(0, sys.argv[1])
-import snake_amd as snk
-snk.load()
-rng = np.random.default_rng(6)
-m = snk.DQNModel(12, 3, n_frames=2, seed=23)
-x = rng.integers(-1, 3, size=(4096, 2, 144)).astype(np.float32)
-np.save(sys.argv[2], m(x))
-np.save(sys.argv[3], m.get_params())
-"""
-
-
-def test_dense_h3_act_forward(tmp_path):
+def test_dense_h3_act_forward(snk):
     """Dense1 of the 4096-state act forward on dense_h3_kernel (fp16 h3 split, per-sample
     a3 scale from conv_h3f's epilogue, per-(position, output) weight scales from
-    w3_split_kernel) against the same forward with Dense1 on the x6 kernel (SNK_DH3=0):
-    2e-6 * max(1, |q|) at most, 3e-7 on average; both against the fp64 oracle at 1e-5."""
-    import os
-    import subprocess
-    import sys
-    repo = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    w3_split_kernel) against the same forward with Dense1 on the x6 kernel
+    (snk.arith(dh3=False)): 2e-6 * max(1, |q|) at most, 3e-7 on average; both against
+    the fp64 oracle at 1e-5."""
     out = {}
-    for flag in ("1", "0"):
-        env = dict(os.environ, SNK_DH3=flag)
-        q, p = tmp_path / f"q{flag}.npy", tmp_path / f"p{flag}.npy"
-        subprocess.run([sys.executable, "-c", _DH3_SCRIPT, repo, str(q), str(p)], env=env, check=True, timeout=240)
-        out[flag] = (np.load(q), np.load(p))
-    qh, p = out["1"]
-    qx, _ = out["0"]
-    assert np.array_equal(p, out["0"][1])
-    assert not np.array_equal(qh, qx), "SNK_DH3 did not switch the Dense1 kernel"
+    for flag in (True, False):
+        rng = np.random.default_rng(6)
+        m = snk.DQNModel(12, 3, n_frames=2, seed=23)
+        x = rng.integers(-1, 3, size=(4096, 2, 144)).astype(np.float32)
+        with snk.arith(dh3=flag):
+            out[flag] = (m(x), m.get_params())
+    qh, p = out[True]
+    qx, _ = out[False]
+    assert np.array_equal(p, out[False][1])
+    assert not np.array_equal(qh, qx), "snk.arith(dh3=False) did not switch the Dense1 kernel"
     # measured spread of the two exact-split paths: max 3.7e-7, mean 6.9e-8 (round 4); a wrong
     # row or column scale (the round-4 a3-max bug) shows up far above these bounds
     rel = np.abs(qh - qx) / np.maximum(1.0, np.abs(qx))
