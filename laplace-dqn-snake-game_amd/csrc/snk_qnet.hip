@@ -720,7 +720,10 @@ __global__ __launch_bounds__(256) void head_pair_kernel(HeadNet tn, HeadNet qn, 
 // f64 16x16x4 operand map: lane l holds A[l & 15][k = l >> 4], B[k = l >> 4][l & 15]; D row
 // (l >> 4) + 4i, column l & 15.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-constexpr int D1B_F = 32, D1B_P = 66, D1B_PA = 48;   // features per block, LDS row pitches (floats)
+constexpr int D1B_F = 32, D1B_P = 98, D1B_PA = 48;   // features per block, LDS row pitches (floats)
+// D1B_P = 98 (34 mod 64): the dX fragment reads (row r, column kq: 34r + kq) and the dW reads
+// of dz1 (row kq, column r: 34kq + r) both land on distinct banks per 32-lane half (66 made
+// the dW reads 2-way)
 __global__ __launch_bounds__(512) void d1_bwd_kernel(const float *__restrict__ a3, const float *__restrict__ dz1,
                                                      const float *__restrict__ w1, float *__restrict__ dz3,
                                                      float *__restrict__ dw, int S, int K1, int nfb) {
@@ -1734,9 +1737,11 @@ static_assert(GU_WMAX_BLOCKS == 36 * (32 / GU_ROWS), "conv3 image blocks");
 // wmax: where this block's max |new theta| goes (the conv3 section, UpdateTarget::wmax_out)
 __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb, bool due, float omr,
                                float *wmax = nullptr) {
-    __shared__ __attribute__((aligned(16))) float th_s[GU_ROWS * 64];   // lds: one per kernel (grad_update_kernel only)
+    // rows of CN + 4 floats: the image pass below reads column n of rows c4 .. c4 + 3 with
+    // lane groups spanning four c4 values, which a CN-float pitch put on one bank (4-way)
+    __shared__ __attribute__((aligned(16))) float th_s[GU_ROWS * (64 + 4)];   // lds: one per kernel (grad_update_kernel only)
     __shared__ float red4[4];   // lds: one per kernel (grad_update_kernel only)
-    const int CN = S.CN, n_el = GU_ROWS * CN;
+    const int CN = S.CN, n_el = GU_ROWS * CN, lcn = CN == 64 ? 6 : 5;   // CN: 32 or 64
     const int64_t p0 = S.off + ((int64_t)kk * S.CK + cb * GU_ROWS) * CN;   // a multiple of 4
     float m = 0.0f;
     // sections of 128 float4 per block (conv2: 16 x 32) with the finish to do: two threads per
@@ -1783,7 +1788,7 @@ __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb,
         *reinterpret_cast<f32x4 *>(a.u.acc + i) = qd;
         *reinterpret_cast<f32x4 *>(a.u.theta + i) = tn;
         if (due) *reinterpret_cast<f32x4 *>(a.u.theta_t + i) = tn;
-        *reinterpret_cast<f32x4 *>(&th_s[e]) = tn;
+        *reinterpret_cast<f32x4 *>(&th_s[(e >> lcn) * (CN + 4) + (e & (CN - 1))]) = tn;
         m = fmaxf(m, fmaxf(fmaxf(fabsf(tn[0]), fabsf(tn[1])), fmaxf(fabsf(tn[2]), fabsf(tn[3]))));
     }
     if (!a.apply) return;
@@ -1797,8 +1802,8 @@ __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb,
     // 3*base + kk*3*CK*CN + p*CK*CN + n*CK + c
     for (int it = threadIdx.x; it < CN * (GU_ROWS / 4); it += 256) {
         const int n = it / (GU_ROWS / 4), c4 = (it % (GU_ROWS / 4)) * 4;
-        const float v0 = th_s[(c4 + 0) * CN + n], v1 = th_s[(c4 + 1) * CN + n];
-        const float v2 = th_s[(c4 + 2) * CN + n], v3 = th_s[(c4 + 3) * CN + n];
+        const float v0 = th_s[(c4 + 0) * (CN + 4) + n], v1 = th_s[(c4 + 1) * (CN + 4) + n];
+        const float v2 = th_s[(c4 + 2) * (CN + 4) + n], v3 = th_s[(c4 + 3) * (CN + 4) + n];
         const int64_t t = S.base + (int64_t)kk * S.CK * CN + (int64_t)n * S.CK + cb * GU_ROWS + c4;
         const f32x4 w4 = {v0, v1, v2, v3};
         *reinterpret_cast<f32x4 *>(a.u.wt + t) = w4;

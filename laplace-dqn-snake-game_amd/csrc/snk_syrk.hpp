@@ -214,6 +214,9 @@ struct SyrkArgs {
     int64_t ntiles;          // tiles of this launch: [t0, t0 + ntiles) of the order
     int64_t t0;
     const int2 *tiles;       // optional tile order (bi, bj), indexed by the XCD remap; null: row-major
+    int direct;              // tiles[t0 + blockIdx.x] as is (the table already interleaves the XCDs)
+    uint64_t *stamps;        // measurement builds (SNK_SYRK_MEASURE): per workgroup s_memtime /
+                             // s_memrealtime at start and end, 4 words
     float *g32;              // SYRK_F32 (h3q): G [N][ldg]
     double *g64;             // SYRK_SLAB64: slab [z][N][N]
     int64_t ldg;
@@ -326,7 +329,7 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
     __shared__ __attribute__((aligned(16))) uint16_t lds[SH_BUF * 2 * 2 * SY_T * SH_ROW];   // 128 KB
     int bi, bj;
     {
-        const int64_t t = a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
+        const int64_t t = a.t0 + (a.direct ? (int64_t)blockIdx.x : syrk_xcd_remap(blockIdx.x, a.ntiles));
         if (a.tiles) {
             const int2 tb = a.tiles[t];
             bi = tb.x;
@@ -519,13 +522,23 @@ __device__ __forceinline__ int syrk_swz16(int row) { return (-(row >> 2)) & 3; }
 // accumulators are folded at the segment ends, hook_a / hook_z below; the
 // a3 segment (K1 = 576 at 12x12) accumulates in fp32 like one flush interval of
 // the conv Gram)
-template <int VAR = 0, int NB = 4, bool DENSE = false>
+// SB: stages per barrier. 1: one barrier per 32-k stage, stage st + NB - 1 issued at step st;
+// 2 (NB = 4): the stages go in pairs, one barrier per pair, the next pair's two stages issued
+// right after the barrier that freed their buffers (the same 2-stage lead).
+template <int VAR = 0, int NB = 4, bool DENSE = false, int SB = 1>
 __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
+    static_assert(SB == 1 || (SB == 2 && NB == 4), "stage pairs need four buffers");
     constexpr int NJ = 4;   // DMA jobs per wave and stage (32 KB / 8 waves / 1 KB)
     __shared__ __attribute__((aligned(16))) uint16_t lds[NB * 2 * 2 * SY_T * SH_ROW];
+#ifdef SNK_SYRK_MEASURE
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[4 * blockIdx.x] = __builtin_amdgcn_s_memtime();
+        a.stamps[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     int bi, bj;
     {
-        const int64_t t = a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
+        const int64_t t = a.t0 + (a.direct ? (int64_t)blockIdx.x : syrk_xcd_remap(blockIdx.x, a.ntiles));
         if (a.tiles) {
             const int2 tb = a.tiles[t];
             bi = tb.x;
@@ -685,8 +698,8 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
         }
     };
 #pragma unroll
-    for (int q = 0; q < NB - 1; ++q) dma(q, q);
-    __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));
+    for (int q = 0; q < (SB == 1 ? NB - 1 : 2); ++q) dma(q, q);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(SB == 1 ? (NB - 2) * NJ : 0));
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     FA lo, hi;
@@ -708,10 +721,19 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         mfma_half(lo, bc, 0, 1);
         __builtin_amdgcn_sched_barrier(0);
-        dma(st + NB - 1, (B + NB - 1) % NB);
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));   // my part of stage st+1 landed
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_s_barrier();
+        if constexpr (SB == 1) {
+            dma(st + NB - 1, (B + NB - 1) % NB);
+            __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));   // my part of stage st+1 landed
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+        } else if constexpr (B % 2 == 0) {   // pair start: the next pair into the previous pair's buffers
+            dma(st + 2, (B + 2) % NB);
+            dma(st + 3, (B + 3) % NB);
+        } else {                              // pair end: the next pair landed, this pair's reads done
+            __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+        }
         __builtin_amdgcn_sched_barrier(0);
         frag_a((B + 1) % NB, 0, lo);
         frag_b((B + 1) % NB, bn);
@@ -779,6 +801,12 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
         return;
     }
     flush();
+#ifdef SNK_SYRK_MEASURE
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
+        a.stamps[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -802,7 +830,7 @@ __global__ __launch_bounds__(256) void syrk_slab_kernel(SyrkArgs a) {
     __shared__ __attribute__((aligned(16))) SyrkX6Lds sm;
     int bi, bj;
     {
-        const int64_t t = a.t0 + syrk_xcd_remap(blockIdx.x, a.ntiles);
+        const int64_t t = a.t0 + (a.direct ? (int64_t)blockIdx.x : syrk_xcd_remap(blockIdx.x, a.ntiles));
         if (a.tiles) {
             const int2 tb = a.tiles[t];
             bi = tb.x;

@@ -119,8 +119,10 @@ def _gram_worker(rank, world, port, q):
 
 def test_gram_shards_gloo_world2_and_4():
     """D(50k) across ranks: the tile shards of every rank are disjoint, cover
-    the lower triangle exactly once, are balanced to within one tile, and
-    reassemble (with the mirror) to the full Gram."""
+    the lower triangle exactly once, are balanced to within 8 tiles (shard
+    boundaries fall on multiples of 8, so each shard's workgroup numbering keeps
+    the tile table's XCD interleave), and reassemble (with the mirror) to the
+    full Gram."""
     for world in (2, 4):
         port = _free_port()
         ctx = mp.get_context("spawn")
@@ -134,4 +136,4 @@ def test_gram_shards_gloo_world2_and_4():
             assert p.exitcode == 0
         for n, (covered, equal, counts) in res[0].items():
             assert covered and equal, (world, n)
-            assert max(counts) - min(counts) <= 1, counts
+            assert max(counts) - min(counts) <= 8, counts
