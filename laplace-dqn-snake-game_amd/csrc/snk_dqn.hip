@@ -134,8 +134,8 @@ void dqn_loss_grad(snk_dqn_s *h, const BoardSrc &s_src, const BoardSrc &sn_src, 
     la.dz1 = h->trn.dz1;
     const FwdNet nets[2] = {FwdNet{h->theta_t, h->wt_t, h->wtb_t, sn_src, &h->tgt},
                             FwdNet{h->theta_q, h->wt_q, h->wtb_q, s_src, &h->trn}};
-    qnet_forward_update_pair(h->L, nets, B, s);
-    qnet_head_pair(h->L, h->theta_t, h->tgt, h->theta_q, h->trn, B, la, s);
+    const int ks = qnet_forward_update_pair(h->L, nets, B, s, &la);
+    if (ks > 0) qnet_head_pair(h->L, h->theta_t, h->tgt, h->theta_q, h->trn, B, la, s, ks);
     if (o.loss_mean) loss_mean_launch(h->trn.loss, B, h->loss_dev, s);
     BwdOpts bo;
     bo.defer = o.defer;

@@ -523,11 +523,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(Conv1Pair cp, int64_t S,
 }
 
 // ---------------------------------------------------------------- heads
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+// (wave_sum: snk_upd_fwd.hpp)
 
 template <int MODE>
 __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ slab, int ks, int64_t S,
@@ -617,93 +613,12 @@ __global__ __launch_bounds__(256) void head_kernel(const float *__restrict__ sla
 }
 
 // HEAD_TARGET of t_net then HEAD_LOSS of q_net for the same sample in one wave
-// (the loss needs exactly that sample's target): the two head launches of an
-// update in one, same arithmetic as head_kernel<HEAD_TARGET> / <HEAD_LOSS>.
-struct HeadNet {
-    const float *slab, *theta;
-    float *h1, *q;
-};
+// (head_pair_one, snk_upd_fwd.hpp): the two head launches of an update in one
 __global__ __launch_bounds__(256) void head_pair_kernel(HeadNet tn, HeadNet qn, int ks, int64_t S, QLayout L,
                                                         HeadArgs ha) {
-    const int lane = threadIdx.x & 63;
     const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= S) return;
-    const int64_t m = ha.idx ? ha.idx[s] : s;
-    // every independent load of both nets up front (the kernel is load-latency bound: the
-    // q_net half used to start its loads only after the t_net half's reductions)
-    constexpr int KMAX = 16;
-    float zt[KMAX], zq[KMAX];
-#pragma unroll
-    for (int z = 0; z < KMAX; ++z) {
-        if (z < ks) {
-            zt[z] = tn.slab[((int64_t)z * S + s) * 64 + lane];
-            zq[z] = qn.slab[((int64_t)z * S + s) * 64 + lane];
-        }
-    }
-    float wt2[3], wq2[3], bt2[3], bq2[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        wt2[a] = tn.theta[L.off_d2w + a * 64 + lane];
-        wq2[a] = qn.theta[L.off_d2w + a * 64 + lane];
-        bt2[a] = tn.theta[L.off_d2b + a];
-        bq2[a] = qn.theta[L.off_d2b + a];
-    }
-    const float bt1 = tn.theta[L.off_d1b + lane], bq1 = qn.theta[L.off_d1b + lane];
-    const uint8_t mk = ha.mask[m], dn = ha.done[m];
-    const float rw = ha.rew[m];
-    const int a_taken = ha.act_idx[m] % 3;
-    // t_net(s'): TD target (utils.jl:448-451)
-    float h = bt1;
-    if (ks <= KMAX) {
-#pragma unroll
-        for (int z = 0; z < KMAX; ++z)
-            if (z < ks) h += zt[z];
-    } else {
-        for (int z = 0; z < ks; ++z) h += tn.slab[((int64_t)z * S + s) * 64 + lane];
-    }
-    h = h > 0.0f ? h : 0.0f;
-    tn.h1[s * 64 + lane] = h;
-    float q[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) q[a] = bt2[a] + wave_sum(wt2[a] * h);
-    float mx = -INFINITY;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float v = ((mk >> a) & 1) ? -100.0f : q[a];
-        mx = v > mx ? v : mx;
-    }
-    const double tgt = (double)rw + ha.gamma * (double)mx * (double)(1 - (int)dn);
-    if (lane == 0) {
-        tn.q[s * 3 + 0] = q[0];
-        tn.q[s * 3 + 1] = q[1];
-        tn.q[s * 3 + 2] = q[2];
-        ha.target[s] = tgt;
-    }
-    // q_net(s): Huber loss, dq and dz1 (utils.jl:453-464)
-    h = bq1;
-    if (ks <= KMAX) {
-#pragma unroll
-        for (int z = 0; z < KMAX; ++z)
-            if (z < ks) h += zq[z];
-    } else {
-        for (int z = 0; z < ks; ++z) h += qn.slab[((int64_t)z * S + s) * 64 + lane];
-    }
-    h = h > 0.0f ? h : 0.0f;
-    qn.h1[s * 64 + lane] = h;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) q[a] = bq2[a] + wave_sum(wq2[a] * h);
-    const int a = a_taken;
-    const double e = (double)q[a] - tgt;
-    const double ae = fabs(e);
-    const double g = (ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / (double)ha.B;
-    if (ha.dz1) ha.dz1[s * 64 + lane] = h > 0.0f ? (float)g * (a == 0 ? wq2[0] : a == 1 ? wq2[1] : wq2[2]) : 0.0f;
-    if (lane != 0) return;
-    qn.q[s * 3 + 0] = q[0];
-    qn.q[s * 3 + 1] = q[1];
-    qn.q[s * 3 + 2] = q[2];
-    ha.loss[s] = ae < 1.0 ? 0.5 * e * e : ae - 0.5;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ha.dq[s * 3 + k] = k == a ? (float)g : 0.0f;
+    head_pair_one(tn, qn, ks, S, L, ha, s, threadIdx.x & 63);
 }
 
 // backward of Dense2 + relu: dz1[s][o] = (h1 > 0) * sum_a dq[s][a] W2[a][o]
@@ -884,7 +799,7 @@ void qwork_free(QWork &w) {
     for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a2b, (void *)w.a1b, (void *)w.a3, (void *)w.slab, (void *)w.cslab,
                     (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.x0, (void *)w.target,
-                    (void *)w.loss, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e,
+                    (void *)w.loss, (void *)w.upd_ticket, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e,
                     (void *)w.w2h, (void *)w.w1h, (void *)w.w1e, (void *)w.a3max})
         dfree(p);
     w = QWork{};
@@ -960,6 +875,8 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
         w.x0 = dalloc<float>((size_t)cap * L.ncell * L.C);
         w.target = dalloc<double>(cap);
         w.loss = dalloc<double>(cap);
+        w.upd_ticket = dalloc<uint32_t>(cap);
+        SNK_HIP(hipMemsetAsync(w.upd_ticket, 0, (size_t)cap * 4, stream()));
     }
 }
 
@@ -1345,25 +1262,36 @@ __global__ __launch_bounds__(512) void dense1_upd_kernel(D1UpdNet n0, D1UpdNet n
     }
 }
 
-void qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s) {
+// returns the number of Dense1 partial slabs the head sums: 2 when the update forward ran
+// Dense1 itself (phase 4 of upd_fwd_kernel, S <= 64), else d1_split's; 0 when it also ran
+// both heads (phase 5, `head` given: HEAD_LOSS arguments and the two nets' thetas)
+int qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s, const HeadArgs *head) {
+    int kc;
+    const int ks = d1_split(L, S, kc);
     // the x6 weight planes of both nets are kept current by every theta change
     if (net[0].wtb && net[1].wtb && (L.C == 1 || L.C == 2) && S >= 1 && S <= 4096) {
         UpdFwdArgs a{};
         a.L = L;
         a.S = (int)S;
+        a.d1 = S <= 64 && net[0].w->slab_floats >= 2 * S * 64 && net[1].w->slab_floats >= 2 * S * 64;
         for (int g = 0; g < 2; ++g) {
             QWork &w = *net[g].w;
             const bool train = w.has_train != 0;
             a.net[g] = UpdFwdNet{net[g].src, net[g].th, net[g].wtb, train ? w.a1 : nullptr, train ? w.a2 : nullptr,
-                                 w.a3, train ? w.x0 : nullptr};
+                                 w.a3, train ? w.x0 : nullptr, w.slab};
+            a.hn[g] = HeadNet{w.slab, net[g].th, w.h1, w.q};
+        }
+        a.head = a.d1 && head && net[1].w->upd_ticket && net[1].w->cap >= S;
+        if (a.head) {
+            a.ha = *head;
+            a.ticket = net[1].w->upd_ticket;
         }
         if (upd_fwd_launch(a, s)) {
             for (int g = 0; g < 2; ++g) {
                 net[g].w->x0_valid = net[g].w->has_train ? 1 : 0;
                 net[g].w->wmax_n = 0;   // no conv3 weight-max partials from this path
             }
-            int kc;
-            const int ks = d1_split(L, S, kc);
+            if (a.d1) return a.head ? 0 : 2;   // Dense1 (and the heads) done in the same launch
             if (S <= 64 && kc * 64 <= D1U_FMAX) {   // Dense1 slabs on dense1_upd_kernel
                 const D1UpdNet d0{net[0].w->a3, net[0].th + L.off_d1w, net[0].w->slab};
                 const D1UpdNet d1{net[1].w->a3, net[1].th + L.off_d1w, net[1].w->slab};
@@ -1374,16 +1302,15 @@ void qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hi
             } else {
                 forward_layers(L, net, 2, S, s, 3, 3);   // Dense1 slabs
             }
-            return;
+            return ks;
         }
     }
     forward_layers(L, net, 2, S, s, 0, 3);
+    return ks;
 }
 
 void qnet_head_pair(const QLayout &L, const float *th_t, QWork &wt_, const float *th_q, QWork &wq, int64_t S,
-                    const HeadArgs &ha, hipStream_t s) {
-    int kc;
-    const int ks = d1_split(L, S, kc);
+                    const HeadArgs &ha, hipStream_t s, int ks) {
     head_pair_kernel<<<ceil_div(S, 4), 256, 0, s>>>(HeadNet{wt_.slab, th_t, wt_.h1, wt_.q},
                                                     HeadNet{wq.slab, th_q, wq.h1, wq.q}, ks, S, L, ha);
     launch_check("head_pair_kernel");

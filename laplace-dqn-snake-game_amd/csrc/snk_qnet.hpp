@@ -81,6 +81,8 @@ struct QWork {
     int dh3_ready = 0;               // a3, a3max, w1h / w1e are those of the last conv_h3f + w3_split forward
                                      //   (a Dense1-only call, e.g. the per-layer timing, may then use dense_h3)
     double *target = nullptr, *loss = nullptr;
+    uint32_t *upd_ticket = nullptr;  // training: per-sample arrivals of the update forward's four workgroups
+                                     //   (upd_fwd_kernel phase 5), 0 between launches
     int has_train = 0;
     int64_t gen = 0;          // bumped on every reallocation (captured graphs hold the old pointers)
 };
@@ -130,11 +132,15 @@ void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream
 void h3f_timing_hook(hipEvent_t a, hipEvent_t b);
 // the update's two forwards (net[0] = t_net on s', net[1] = q_net on s, which keeps the
 // training activations) up to the Dense1 slabs: conv1-conv3 in one launch
-// (snk_upd_fwd.hpp) when the geometry allows, else the layer-by-layer path
-void qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s);
-// TD-target head of t_net and loss head of q_net (HeadArgs as for HEAD_LOSS) in one launch
+// (snk_upd_fwd.hpp, with Dense1 at S <= 64) when the geometry allows, else the layer-by-layer
+// path; returns the number of Dense1 partial slabs for the head
+// (and, given `head` (HEAD_LOSS arguments), both heads in the same launch: returns 0)
+int qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s,
+                             const HeadArgs *head = nullptr);
+// TD-target head of t_net and loss head of q_net (HeadArgs as for HEAD_LOSS) in one launch,
+// over ks Dense1 slabs (qnet_forward_update_pair's count)
 void qnet_head_pair(const QLayout &L, const float *theta_t, QWork &wt, const float *theta_q, QWork &wq, int64_t S,
-                    const HeadArgs &ha, hipStream_t s);
+                    const HeadArgs &ha, hipStream_t s, int ks);
 // the head (Dense1 bias + relu, Dense2, mode epilogue) after the layers
 void qnet_head(const QLayout &L, const float *theta, int64_t S, QWork &w, HeadMode mode, const HeadArgs &ha,
                hipStream_t s);

@@ -322,7 +322,9 @@ constexpr int SH_BUF = 4, SH_ROW = 32;   // halves per LDS row (one 32-k stage)
 // half the fragment reads per MFMA)
 // VAR (measurement builds selected by SNK_SYRK_VAR): 0 the kernel, 1 no MFMA (the
 // fragments feed one VALU op each: data movement + LDS reads + barriers alone),
-// 2 no stage DMA after the prologue (MFMAs + fragment reads + barriers alone)
+// 2 no stage DMA after the prologue (MFMAs + fragment reads + barriers alone),
+// 3 (syrk_h3q_kernel) the B operand's stages not reloaded: half the DMA stream, as a tile
+// twice as wide would have per FLOP
 template <int NW, int VAR = 0>
 __global__ __launch_bounds__(64 * NW) void syrk_h3_kernel(SyrkArgs a) {
     constexpr int NC = NW == 4 ? 2 : 1, NJ = 32 / NW;   // column tiles per wave, DMA jobs per wave and stage
@@ -569,6 +571,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
     const int64_t qstride = 16 * 2 * a.ldh;
     auto dma = [&](int st, int buf) __attribute__((always_inline)) {
         if (VAR == 2 && st > NB - 2) return;
+        if (VAR == 3 && st > NB - 2 && wave >= 4) return;   // B (waves 4-7) loaded once: half the stream
         const int64_t k = (int64_t)min(st, nst - 1) * 2 * SY_KS;
 #pragma unroll
         for (int q = 0; q < NJ; ++q)

@@ -20,8 +20,19 @@
 //            LDS image, B (the weight planes the update keeps current) staged
 //            through LDS three offsets at a time (double-buffered, loaded two stages
 //            ahead); bias + relu -> a3.
+//   phase 4  (d1) Dense1 over this workgroup's half of the features: the sample's a3
+//            channels of this half (NO positions x 32) from LDS against the W1 rows
+//            (p * 64 + 32 half + c) straight from L2 (fp32 float4 rows, fp64 FMA sums per
+//            channel, the 32 channel sums added in channel order, rounded once) -> the
+//            half's partial slab; the head adds the two halves (ks = 2). This replaced
+//            dense1_upd_kernel (8.8 us) and its launch boundary in round 5: the 64 samples'
+//            W1 re-reads (401 KB per workgroup at 12x12) stay in L2.
+//   phase 5  (head) the last of the sample's four workgroups (its two halves in both nets,
+//            an agent-scope ticket per sample) runs both heads for it (head_pair_one: the
+//            t_net TD target, the q_net Huber loss, dq and dz1), which replaced the
+//            head_pair_kernel launch.
 // conv1 and conv2 run in both halves of a sample (they are ~20 % of the work);
-// only half 0 writes a1, a2 and x0. Dense1 and the heads follow as before.
+// only half 0 writes a1, a2 and x0.
 #pragma once
 
 #include "snk_conv_h3.hpp"
@@ -43,17 +54,119 @@ __device__ uint64_t *g_upd_clk;
 #define UPD_CLK(slot) do { } while (0)
 #endif
 
+// HEAD_TARGET of t_net then HEAD_LOSS of q_net for the same sample s in one wave
+// (the loss needs exactly that sample's target): same arithmetic as
+// head_kernel<HEAD_TARGET> / <HEAD_LOSS> (snk_qnet.hip), the ks Dense1 slabs added to the
+// bias in slab order. Run by head_pair_kernel (one wave per sample) and by the last of a
+// sample's four update-forward workgroups (upd_fwd_kernel phase 5).
+struct HeadNet {
+    const float *slab, *theta;
+    float *h1, *q;
+};
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ void head_pair_one(const HeadNet &tn, const HeadNet &qn, int ks, int64_t S,
+                                              const QLayout &L, const HeadArgs &ha, int64_t s, int lane) {
+    const int64_t m = ha.idx ? ha.idx[s] : s;
+    // every independent load of both nets up front (the kernel is load-latency bound: the
+    // q_net half used to start its loads only after the t_net half's reductions)
+    constexpr int KMAX = 16;
+    float zt[KMAX], zq[KMAX];
+#pragma unroll
+    for (int z = 0; z < KMAX; ++z) {
+        if (z < ks) {
+            zt[z] = tn.slab[((int64_t)z * S + s) * 64 + lane];
+            zq[z] = qn.slab[((int64_t)z * S + s) * 64 + lane];
+        }
+    }
+    float wt2[3], wq2[3], bt2[3], bq2[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        wt2[a] = tn.theta[L.off_d2w + a * 64 + lane];
+        wq2[a] = qn.theta[L.off_d2w + a * 64 + lane];
+        bt2[a] = tn.theta[L.off_d2b + a];
+        bq2[a] = qn.theta[L.off_d2b + a];
+    }
+    const float bt1 = tn.theta[L.off_d1b + lane], bq1 = qn.theta[L.off_d1b + lane];
+    const uint8_t mk = ha.mask[m], dn = ha.done[m];
+    const float rw = ha.rew[m];
+    const int a_taken = ha.act_idx[m] % 3;
+    // t_net(s'): TD target (utils.jl:448-451)
+    float h = bt1;
+    if (ks <= KMAX) {
+#pragma unroll
+        for (int z = 0; z < KMAX; ++z)
+            if (z < ks) h += zt[z];
+    } else {
+        for (int z = 0; z < ks; ++z) h += tn.slab[((int64_t)z * S + s) * 64 + lane];
+    }
+    h = h > 0.0f ? h : 0.0f;
+    tn.h1[s * 64 + lane] = h;
+    float q[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) q[a] = bt2[a] + wave_sum(wt2[a] * h);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float v = ((mk >> a) & 1) ? -100.0f : q[a];
+        mx = v > mx ? v : mx;
+    }
+    const double tgt = (double)rw + ha.gamma * (double)mx * (double)(1 - (int)dn);
+    if (lane == 0) {
+        tn.q[s * 3 + 0] = q[0];
+        tn.q[s * 3 + 1] = q[1];
+        tn.q[s * 3 + 2] = q[2];
+        ha.target[s] = tgt;
+    }
+    // q_net(s): Huber loss, dq and dz1 (utils.jl:453-464)
+    h = bq1;
+    if (ks <= KMAX) {
+#pragma unroll
+        for (int z = 0; z < KMAX; ++z)
+            if (z < ks) h += zq[z];
+    } else {
+        for (int z = 0; z < ks; ++z) h += qn.slab[((int64_t)z * S + s) * 64 + lane];
+    }
+    h = h > 0.0f ? h : 0.0f;
+    qn.h1[s * 64 + lane] = h;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) q[a] = bq2[a] + wave_sum(wq2[a] * h);
+    const int a = a_taken;
+    const double e = (double)q[a] - tgt;
+    const double ae = fabs(e);
+    const double g = (ae < 1.0 ? e : (e > 0 ? 1.0 : -1.0)) / (double)ha.B;
+    if (ha.dz1) ha.dz1[s * 64 + lane] = h > 0.0f ? (float)g * (a == 0 ? wq2[0] : a == 1 ? wq2[1] : wq2[2]) : 0.0f;
+    if (lane != 0) return;
+    qn.q[s * 3 + 0] = q[0];
+    qn.q[s * 3 + 1] = q[1];
+    qn.q[s * 3 + 2] = q[2];
+    ha.loss[s] = ae < 1.0 ? 0.5 * e * e : ae - 0.5;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ha.dq[s * 3 + k] = k == a ? (float)g : 0.0f;
+}
+
 struct UpdFwdNet {
     BoardSrc src;
-    const float *th;        // packed theta: conv1 weights/bias, conv2/conv3 biases
+    const float *th;        // packed theta: conv1 weights/bias, conv2/conv3 biases, Dense1 weights
     const uint16_t *wtb;    // x6 split planes of the forward weight image
     float *a1, *a2, *a3;    // a1/a2 may be null (target net: only a3 is consumed)
     float *x0;              // the input planes as floats [S][C][bs^2] (training net) or null
+    float *slab;            // d1: Dense1 partial slabs [2 halves][S][64] (the head sums the two)
 };
 struct UpdFwdArgs {
     UpdFwdNet net[2];
     QLayout L;
     int S;
+    int d1;                 // phase 4 (Dense1 of this workgroup's 32 channels) on
+    // phase 5 (d1 and head): the heads of both nets (head_pair_one: net[0] = t_net's TD target,
+    // net[1] = q_net's loss, dq, dz1) run by the last of each sample's four workgroups
+    int head;
+    HeadNet hn[2];
+    HeadArgs ha;
+    uint32_t *ticket;       // [S] arrivals, 0 between launches (the last arriver resets it)
 };
 
 // LDS strides (halves): A1 position record 3 planes x 16 ch + 8 pad
@@ -435,6 +548,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
         }
         UPD_CLK(4);
         const float bv = b3[col];
+        float a3v[NTW][4];
 #pragma unroll
         for (int u = 0; u < NTW; ++u) {
             const int t = rt0 + 4 * u;
@@ -442,10 +556,71 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int qi = (4 * g + e) % TW, qj = t * RPT + (4 * g + e) / TW;
-                if (qi < WO && qj < WO)
-                    n.a3[((int64_t)s * NO + qi + qj * WO) * 64 + col] = fmaxf((acc[u][0][e] + acc[u][1][e]) + bv, 0.f);
+                a3v[u][e] = fmaxf((acc[u][0][e] + acc[u][1][e]) + bv, 0.f);
+                if (qi < WO && qj < WO) n.a3[((int64_t)s * NO + qi + qj * WO) * 64 + col] = a3v[u][e];
             }
         }
+        if (!args.d1) return;
+        // ---- phase 4: Dense1 over this half's 32 channels ------------------------------------
+        // every wave's conv3 reads of the images and the ring are done past this barrier
+        __syncthreads();
+        float *a3s = reinterpret_cast<float *>(updf_lds);                        // [NO][32]
+        double *red = reinterpret_cast<double *>(updf_lds + ((NO * 32 * 4 + 15) & ~15));   // [32 c][64 o]
+#pragma unroll
+        for (int u = 0; u < NTW; ++u) {
+            const int t = rt0 + 4 * u;
+            if (t >= T3) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int qi = (4 * g + e) % TW, qj = t * RPT + (4 * g + e) / TW;
+                if (qi < WO && qj < WO) a3s[(qi + qj * WO) * 32 + ct * 16 + r] = a3v[u][e];
+            }
+        }
+        __syncthreads();
+        {
+            const int o4 = tid & 15, c = tid >> 4;   // outputs 4 o4 .. +3, channel c of this half
+            const f32x4 *w1 = reinterpret_cast<const f32x4 *>(n.th + L.off_d1w + (int64_t)(32 * half + c) * 64 + 4 * o4);
+            double z0 = 0.0, z1 = 0.0, z2 = 0.0, z3 = 0.0;
+            constexpr int PB = 7;   // W1 rows in flight per thread
+            for (int p0 = 0; p0 < NO; p0 += PB) {
+                f32x4 wv[PB];
+#pragma unroll
+                for (int k = 0; k < PB; ++k) wv[k] = p0 + k < NO ? w1[(int64_t)(p0 + k) * 64 * 16] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < PB; ++k) {
+                    if (p0 + k >= NO) break;
+                    const double av = (double)a3s[(p0 + k) * 32 + c];
+                    z0 = __builtin_fma(av, (double)wv[k][0], z0);
+                    z1 = __builtin_fma(av, (double)wv[k][1], z1);
+                    z2 = __builtin_fma(av, (double)wv[k][2], z2);
+                    z3 = __builtin_fma(av, (double)wv[k][3], z3);
+                }
+            }
+            double *rd = red + c * 64 + 4 * o4;
+            rd[0] = z0;
+            rd[1] = z1;
+            rd[2] = z2;
+            rd[3] = z3;
+        }
+        __syncthreads();
+        if (tid >= 64) return;   // wave 0 stores the slab and, if last, runs the heads
+        double z = 0.0;
+#pragma unroll 8
+        for (int c = 0; c < 32; ++c) z += red[c * 64 + tid];
+        n.slab[((int64_t)half * args.S + s) * 64 + tid] = (float)z;
+        if (!args.head) return;
+        // ---- phase 5: the last of the sample's four workgroups (2 halves x 2 nets) runs the
+        // heads. Release: the agent-scope atomic writes back this wave's slab stores (the only
+        // ones the heads read from this workgroup) before it counts; the last arriver's acquire
+        // (same atomic) invalidates its caches, so the other three workgroups' slabs, written
+        // on any XCD, are read fresh.
+        uint32_t last = 0;
+        if (tid == 0)
+            last = __hip_atomic_fetch_add(args.ticket + s, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 3u;
+        last = __shfl(last, 0, 64);
+        if (!last) return;
+        if (tid == 0) __hip_atomic_store(args.ticket + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        head_pair_one(args.hn[0], args.hn[1], 2, args.S, L, args.ha, s, tid);
     }
 }
 

@@ -140,7 +140,9 @@ int main(int argc, char **argv) {
                      {"super8x4 sb2 nb4", 0, 2, 0, 4},          {"chip16x16 sb2 nb4", 1, 2, 0, 4},
                      {"super8x4 nb4 no-MFMA", 0, 1, 1, 4},      {"super8x4 nb4 no-DMA", 0, 1, 2, 4},
                      {"super8x4 sb1 nb3", 0, 1, 0, 3},          {"chip16x16 sb1 nb3", 1, 1, 0, 3},
-                     {"super8x4 sb1 nb5", 0, 1, 0, 5},          {"chip16x16 sb1 nb5", 1, 1, 0, 5}};
+                     {"super8x4 sb1 nb5", 0, 1, 0, 5},          {"chip16x16 sb1 nb5", 1, 1, 0, 5},
+                     {"chip16x16 nb4 no-MFMA", 1, 1, 1, 4},     {"chip16x16 nb4 no-DMA", 1, 1, 2, 4},
+                     {"chip16x16 nb4 half-DMA (B once)", 1, 1, 3, 4}};
     const int nall = sizeof(all) / sizeof(all[0]);
     const int sel = argc > 3 ? (int)strtol(argv[3], nullptr, 0) : 0x3F;   // bit v: run variant v
     std::vector<V> vv;
@@ -176,6 +178,8 @@ int main(int argc, char **argv) {
                 syrk_h3q_kernel<1, 4, false, 1><<<(unsigned)ntiles, 512>>>(a);
             else if (vs[v].var == 2)
                 syrk_h3q_kernel<2, 4, false, 1><<<(unsigned)ntiles, 512>>>(a);
+            else if (vs[v].var == 3)
+                syrk_h3q_kernel<3, 4, false, 1><<<(unsigned)ntiles, 512>>>(a);
             else if (vs[v].sb == 2)
                 syrk_h3q_kernel<0, 4, false, 2><<<(unsigned)ntiles, 512>>>(a);
             else if (vs[v].nb == 3)
