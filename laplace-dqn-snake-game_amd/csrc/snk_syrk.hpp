@@ -569,16 +569,18 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
         ddst = ((op * 2 + pl) * SY_T + rb * 16) * SH_ROW;
     }
     const int64_t qstride = 16 * 2 * a.ldh;
-    auto dma = [&](int st, int buf) __attribute__((always_inline)) {
+    auto dma_job = [&](int st, int buf, int q) __attribute__((always_inline)) {
         if (VAR == 2 && st > NB - 2) return;
         if (VAR == 3 && st > NB - 2 && wave >= 4) return;   // B (waves 4-7) loaded once: half the stream
         const int64_t k = (int64_t)min(st, nst - 1) * 2 * SY_KS;
+        __builtin_amdgcn_global_load_lds((const void *)(dsrc + k + q * qstride),
+                                         (__attribute__((address_space(3))) void *)(lds + buf * (4 * SY_T * SH_ROW) + ddst +
+                                                                                   q * 16 * SH_ROW),
+                                         16, 0, 0);
+    };
+    auto dma = [&](int st, int buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int q = 0; q < NJ; ++q)
-            __builtin_amdgcn_global_load_lds((const void *)(dsrc + k + q * qstride),
-                                             (__attribute__((address_space(3))) void *)(lds + buf * (4 * SY_T * SH_ROW) + ddst +
-                                                                                       q * 16 * SH_ROW),
-                                             16, 0, 0);
+        for (int q = 0; q < NJ; ++q) dma_job(st, buf, q);
     };
     // fragments: A row tiles 0-1 (lo) and 2-3 (hi), B column tiles 0-1 twice (this
     // stage's and the next's): [tile][plane]
@@ -824,6 +826,270 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
             }
         }
 }
+
+#ifdef SNK_SYRK_MEASURE
+// MEASURED, NOT KEPT (tools/syrk_lab.hip only; gpurun_out r05f / r05h): with the two-level
+// fp32 sum it spills (713-752 ms at n = 50,000); with one fp32 sum over all K (VAR 4: 2^-24 x
+// 2461 steps, 3.5e-6 of sqrt(G_ii G_jj) against syrk_h3q_kernel) 457-461 ms against 472-482
+// for syrk_h3q_kernel in the chip-wide order on the same box (its clock 2.1 GHz, but 59 % of
+// MFMA-busy cycles against 69 %): not worth the accuracy.
+// syrk_h3r_kernel: the conv-column Gram on RECTANGULAR 256 x 128 tiles (round 5). The
+// 128 x 128 kernel is bound by its stage stream, not by the matrix cores: at n = 50,000 its
+// build without MFMAs (tools/syrk_lab.hip, VAR 1) takes as long as the real one at a higher
+// clock, and without the stage DMAs (VAR 2) it runs in 0.63 of the time. A 256-row A block
+// against a 128-row B block moves 48 KB per 32-k stage for twice the MFMAs of the 32 KB
+// stage of a 128 x 128 tile: 3/4 of the L2 -> LDS bytes per FLOP, and 2/3 of the fragment
+// bytes per MFMA (each wave a 64 x 64 block: 4 x 4 tiles of 16 x 16, 48 MFMAs per stage
+// on 16 fragment reads instead of 24 on 12).
+// Tile (bi, bj): rows 256 bi .. +255, columns 128 bj .. +127, bj <= 2 bi + 1; only entries
+// with column <= row are stored (the mirror pass fills the rest). 8 waves: wave w owns rows
+// 64 (w >> 1) .. +63 and columns 64 (w & 1) .. +63. Stage buffer [A h][A l][B h][B l] x rows
+// x 32 halves (48 KB), NB = 3 buffers (two stages in flight), the same swizzle and LDS-DMA
+// scheme as syrk_h3q_kernel (6 jobs of 16 rows x 64 B per wave and stage).
+// Accumulation: fp32 MFMA accumulators, added every SY_FLUSH stages (1024 k) into a second
+// fp32 sum (the 64 + 64 registers of a 64 x 64 block leave no room for fp64): the error is
+// that of a 77-term fp32 sum of 1024-long fp32 dot products, <= 2^-24 (77 + 32) sum|x_i x_j|,
+// i.e. below 6.5e-6 sqrt(G_ii G_jj) in the worst case and ~1e-7 in practice.
+constexpr int SR_A = 256, SR_B = 128;
+// NW waves: 8 (two per SIMD, 64 x 64 each) or 4 (one per SIMD, 512 registers, 128 x 64 each:
+// a quarter fewer fragment reads per MFMA again)
+// GL: the stage pieces by global_load_lds with one 64-bit source per job (as syrk_h3q_kernel)
+// instead of the buffer descriptors
+template <int VAR = 0, int NB = 3, int NW = 8, int GL = 0>
+__global__ __launch_bounds__(64 * NW) void syrk_h3r_kernel(SyrkArgs a) {
+    constexpr int NJ = 48 / NW;                         // DMA jobs per wave and stage (48 KB / NW waves / 1 KB)
+    constexpr int NTA = 2 * SR_A / NW / 16;             // A row tiles per wave (4 or 8)
+    constexpr int NG = NTA / 2;                         // groups of two row tiles
+    constexpr int STG = 2 * (SR_A + SR_B) * SH_ROW;    // halves per stage buffer
+    __shared__ __attribute__((aligned(16))) uint16_t lds[NB * STG];
+#ifdef SNK_SYRK_MEASURE
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[4 * blockIdx.x] = __builtin_amdgcn_s_memtime();
+        a.stamps[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+    int bi, bj;
+    {
+        const int2 tb = a.tiles[a.t0 + blockIdx.x];
+        bi = tb.x;
+        bj = tb.y;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int wr = (wave >> 1) * (2 * SR_A / NW), wc = (wave & 1) * 64;
+    const int N = a.N;
+    const int nst = (int)(a.ldh / SY_KS);
+    // DMA job j = NJ * wave + q: j < 32: A plane j >> 4, 16-row block j & 15; else B plane
+    // (j - 32) >> 3, block (j - 32) & 7. Rows past N exist (planes padded to SW_ROWS_B rows).
+    // LDS-DMA through two buffer descriptors (the A and the B row block; T8 / T20 of the
+    // programming guide): the lane's part of every job's source is one 32-bit offset (row
+    // lane >> 2 of the 16-row block and its swizzled chunk: the swizzle of row 16 rb +
+    // (lane >> 2) does not depend on rb), the job / stage part a scalar offset, so no 64-bit
+    // address per job stays live across the loop
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const uint32_t rowb = (uint32_t)(2 * a.ldh * 2);   // bytes per plane row
+    const uint32_t lane_off = (uint32_t)(lane >> 2) * rowb + (uint32_t)(((lane & 3) ^ syrk_swz16(lane >> 2)) * 16);
+    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.xh + (int64_t)bi * SR_A * 2 * a.ldh), 0, (int)(SR_A * rowb), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.xh + (int64_t)bj * SR_B * 2 * a.ldh), 0, (int)(SR_B * rowb), 0x00020000);
+    const uint16_t *gsrc[GL ? NJ : 1];
+    if constexpr (GL) {
+#pragma unroll
+        for (int q = 0; q < NJ; ++q) {
+            const int j = NJ * wv + q, op = j >= 32 ? 1 : 0, jj = op ? j - 32 : j;
+            const int pl = op ? jj >> 3 : jj >> 4, rb = op ? jj & 7 : jj & 15;
+            const int64_t grow = (op ? (int64_t)bj * SR_B : (int64_t)bi * SR_A) + rb * 16 + (lane >> 2);
+            gsrc[q] = a.xh + grow * 2 * a.ldh + pl * SY_KS + ((lane & 3) ^ syrk_swz16(lane >> 2)) * 8;
+        }
+    }
+    auto dma = [&](int st, int buf) __attribute__((always_inline)) {
+        if (VAR == 2 && st > NB - 2) return;
+        if constexpr (GL) {
+            const int64_t k = (int64_t)min(st, nst - 1) * 2 * SY_KS;
+#pragma unroll
+            for (int q = 0; q < NJ; ++q) {
+                const int j = NJ * wv + q, op = j >= 32 ? 1 : 0, jj = op ? j - 32 : j;
+                const int pl = op ? jj >> 3 : jj >> 4, rb = op ? jj & 7 : jj & 15;
+                const int dst = ((op ? 2 * SR_A + pl * SR_B : pl * SR_A) + rb * 16) * SH_ROW;
+                __builtin_amdgcn_global_load_lds((const void *)(gsrc[q] + k),
+                                                 (__attribute__((address_space(3))) void *)(lds + buf * STG + dst), 16, 0, 0);
+            }
+            return;
+        }
+        const uint32_t kb = (uint32_t)min(st, nst - 1) * (2 * SY_KS * 2);
+#pragma unroll
+        for (int q = 0; q < NJ; ++q) {
+            const int j = NJ * wv + q, op = j >= 32 ? 1 : 0, jj = op ? j - 32 : j;
+            const int pl = op ? jj >> 3 : jj >> 4, rb = op ? jj & 7 : jj & 15;
+            const uint32_t soff = (uint32_t)(rb * 16) * rowb + (uint32_t)(pl * SY_KS * 2) + kb;
+            const int dst = ((op ? 2 * SR_A + pl * SR_B : pl * SR_A) + rb * 16) * SH_ROW;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? rsb : rsa,
+                                                     (__attribute__((address_space(3))) void *)(lds + buf * STG + dst),
+                                                     16, lane_off, soff, 0, 0);
+        }
+    };
+    typedef f16x8 FA[2][2];   // [tile][plane]
+    typedef f16x8 FB[4][2];
+    auto frag_a = [&](int buf, int t0, FA &f) __attribute__((always_inline)) {
+        const uint16_t *base = lds + buf * STG;
+#pragma unroll
+        for (int pn = 0; pn < 2; ++pn)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = wr + 16 * (t0 + i) + r;
+                f[i][pn] = as_h(*reinterpret_cast<const u32x4 *>(base + (pn * SR_A + row) * SH_ROW +
+                                                                 8 * (g ^ syrk_swz16(row))));
+            }
+    };
+    auto frag_b = [&](int buf, FB &f) __attribute__((always_inline)) {
+        const uint16_t *base = lds + buf * STG;
+#pragma unroll
+        for (int pn = 0; pn < 2; ++pn)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = wc + 16 * j + r;
+                f[j][pn] = as_h(*reinterpret_cast<const u32x4 *>(base + (2 * SR_A + pn * SR_B + row) * SH_ROW +
+                                                                 8 * (g ^ syrk_swz16(row))));
+            }
+    };
+    // VAR 4 (measurement): no second-level sum (one fp32 accumulation over all K)
+    f32x4 acc[NTA][4];
+    float mid[VAR == 4 ? 1 : NTA][4][4];
+#pragma unroll
+    for (int i = 0; i < NTA; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                acc[i][j][e] = 0.0f;
+                if (VAR != 4) mid[i][j][e] = 0.0f;
+            }
+    // half of a stage's 48 MFMAs: row tiles t0, t0+1 x the four column tiles (l*h, h*l, h*h);
+    // part 0: only the first MFMA, part 1: the other 23, part 2: all 24
+    auto mfma_half = [&](const FA &fa, const FB &fb, int t0, int part) __attribute__((always_inline)) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int i = t0 + ii;
+                const bool first = ii == 0 && j == 0;
+                if (VAR == 1) {
+                    if (part != 0 && (part == 2 || !first))
+                        acc[i][j][0] += (float)(fa[ii][0][0] * fb[j][0][0]) + (float)(fa[ii][1][1] * fb[j][1][1]);
+                    continue;
+                }
+                if (part == 2 || (part == 0) == first)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][1], fb[j][0], acc[i][j], 0, 0, 0);
+                if (part != 0) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][0], fb[j][1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][0], fb[j][0], acc[i][j], 0, 0, 0);
+                }
+            }
+    };
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (VAR == 4) return;
+#pragma unroll
+        for (int i = 0; i < NTA; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    mid[i][j][e] += acc[i][j][e];
+                    acc[i][j][e] = 0.0f;
+                }
+    };
+#pragma unroll
+    for (int q = 0; q < NB - 1; ++q) dma(q, q);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    FA f0, f1;   // row-tile groups alternate: group gi in f(gi & 1)
+    FB b0, b1;
+    frag_a(0, 0, f0);
+    frag_b(0, b0);
+    // step st (buffer B = st % NB; f0 / bc hold stage st's row-tile group 0 and B): the first
+    // MFMA, group 1's fragments, the rest of group 0; each further group's MFMAs with the next
+    // group's fragments read under them; the DMA of stage st+NB-1 (into the buffer of stage
+    // st-1), the wait for stage st+1 and the barrier; stage st+1's group 0 and B read; the
+    // last group's MFMAs (as syrk_h3q_kernel's step)
+    auto step = [&](int st, auto bc_, FB &bc, FB &bn) __attribute__((always_inline)) {
+        constexpr int B = decltype(bc_)::value;
+        mfma_half(f0, bc, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_a(B, 2, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_half(f0, bc, 0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (NG == 4) {
+            frag_a(B, 4, f0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_half(f1, bc, 2, 2);
+            __builtin_amdgcn_sched_barrier(0);
+            frag_a(B, 6, f1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_half(f0, bc, 4, 2);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        dma(st + NB - 1, (B + NB - 1) % NB);
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));   // my part of stage st+1 landed
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        frag_a((B + 1) % NB, 0, f0);
+        frag_b((B + 1) % NB, bn);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_half(f1, bc, NTA - 2, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st % SY_FLUSH == SY_FLUSH - 1) flush();
+    };
+    constexpr int U = NB % 2 ? 2 * NB : NB;
+    auto one = [&](int st0, bool tail, auto ic) __attribute__((always_inline)) {
+        constexpr int I = decltype(ic)::value;
+        if (!tail || st0 + I < nst)
+            step(st0 + I, std::integral_constant<int, I % NB>{}, I % 2 ? b1 : b0, I % 2 ? b0 : b1);
+    };
+    auto trip = [&](int st0, bool tail) __attribute__((always_inline)) {
+        static_assert(U <= 6, "unrolled trip");
+        one(st0, tail, std::integral_constant<int, 0>{});
+        one(st0, tail, std::integral_constant<int, 1>{});
+        if constexpr (U > 2) {
+            one(st0, tail, std::integral_constant<int, 2>{});
+            one(st0, tail, std::integral_constant<int, 3>{});
+        }
+        if constexpr (U > 4) {
+            one(st0, tail, std::integral_constant<int, 4>{});
+            one(st0, tail, std::integral_constant<int, 5>{});
+        }
+    };
+    int st = 0;
+    for (; st + U <= nst; st += U) trip(st, false);
+    if (st < nst) trip(st, true);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    flush();
+#ifdef SNK_SYRK_MEASURE
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
+        a.stamps[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+#pragma unroll
+    for (int i = 0; i < NTA; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int col = bj * SR_B + wc + 16 * j + r;
+            if (col >= N) continue;
+            const int ec = a.xe[col];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int row = bi * SR_A + wr + 16 * i + 4 * g + e;
+                if (row >= N || col > row) continue;
+                a.g32[(int64_t)row * a.ldg + col] = __builtin_ldexpf(VAR == 4 ? acc[i][j][e] : mid[i][j][e], -(a.xe[row] + ec));
+            }
+        }
+}
+
+#endif  // SNK_SYRK_MEASURE
 
 constexpr int SW_ROWS_B = 256;   // Jacobian-plane rows are padded to a multiple of this
 

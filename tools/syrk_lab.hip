@@ -100,6 +100,37 @@ static std::vector<int2> order_chip(int N) {
     return out;
 }
 
+// the h3r tiles (bi: 256-row blocks, bj: 128-row blocks, bj <= 2 bi + 1) in the chip-wide order:
+// macro blocks of 16 bi x 32 bj (4096 x 4096), sub-blocks of 4 bi x 8 bj (1024 x 1024, 32 tiles)
+static std::vector<int2> order_rect(int N) {
+    const int T = (N + 127) / 128, T2 = (N + 255) / 256;
+    constexpr int MBI = 16, MBJ = 32, SI = 4, SJ = 8;
+    std::vector<std::vector<int2>> q(8);
+    int rr = 0;
+    for (int I0 = 0; I0 < T2; I0 += MBI)
+        for (int J0 = 0; J0 <= std::min(T - 1, 2 * (I0 + MBI - 1) + 1); J0 += MBJ) {
+            std::vector<int2> blk;
+            for (int si = I0; si < std::min(T2, I0 + MBI); si += SI)
+                for (int sj = J0; sj < std::min(T, J0 + MBJ); sj += SJ)
+                    for (int i = si; i < std::min(T2, si + SI); ++i)
+                        for (int j = sj; j < std::min(std::min(T, sj + SJ), 2 * i + 2); ++j) blk.push_back(int2{i, j});
+            const int cnt = (int)blk.size(), base = cnt / 8, extra = cnt % 8;
+            int p = 0;
+            for (int x = 0; x < 8; ++x) {
+                const int len = base + ((x - rr + 8) % 8 < extra ? 1 : 0);
+                for (int e = 0; e < len; ++e) q[x].push_back(blk[p++]);
+            }
+            rr = (rr + extra) % 8;
+        }
+    size_t tot = 0, mx = 0;
+    for (auto &v : q) tot += v.size(), mx = std::max(mx, v.size());
+    std::vector<int2> out;
+    for (size_t j = 0; j < mx; ++j)
+        for (int x = 0; x < 8; ++x)
+            if (j < q[x].size()) out.push_back(q[x][j]);
+    return out;
+}
+
 int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 50000;
     const int reps = argc > 2 ? atoi(argv[2]) : 2;
@@ -122,12 +153,15 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&G, (size_t)n * n * 4));
     const int T = (n + SY_T - 1) / SY_T;
     const int64_t ntiles = (int64_t)T * (T + 1) / 2;
-    std::vector<int2> o0 = order_super(n), o1 = order_chip(n);
-    int2 *d0, *d1;
+    std::vector<int2> o0 = order_super(n), o1 = order_chip(n), o2 = order_rect(n);
+    const int64_t ntiles_r = (int64_t)o2.size();
+    int2 *d0, *d1, *d2;
     CK(hipMalloc(&d0, ntiles * 8));
     CK(hipMalloc(&d1, ntiles * 8));
+    CK(hipMalloc(&d2, ntiles_r * 8));
     CK(hipMemcpy(d0, o0.data(), ntiles * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d1, o1.data(), ntiles * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d2, o2.data(), ntiles_r * 8, hipMemcpyHostToDevice));
     uint64_t *st;
     CK(hipMalloc(&st, ntiles * 32));
     hipEvent_t e0, e1;
@@ -142,7 +176,14 @@ int main(int argc, char **argv) {
                      {"super8x4 sb1 nb3", 0, 1, 0, 3},          {"chip16x16 sb1 nb3", 1, 1, 0, 3},
                      {"super8x4 sb1 nb5", 0, 1, 0, 5},          {"chip16x16 sb1 nb5", 1, 1, 0, 5},
                      {"chip16x16 nb4 no-MFMA", 1, 1, 1, 4},     {"chip16x16 nb4 no-DMA", 1, 1, 2, 4},
-                     {"chip16x16 nb4 half-DMA (B once)", 1, 1, 3, 4}};
+                     {"chip16x16 nb4 half-DMA (B once)", 1, 1, 3, 4},
+                     {"h3r 256x128 nb3 rect-chip", 2, 1, 0, 3}, {"h3r 256x128 nb3 no-MFMA", 2, 1, 1, 3},
+                     {"h3r 256x128 nb3 no-DMA", 2, 1, 2, 3},
+                     {"h3r 256x128 nb3 4 waves", 2, 4, 0, 3}, {"h3r 256x128 nb3 4 waves no-MFMA", 2, 4, 1, 3},
+                     {"h3r 256x128 nb3 4 waves no-DMA", 2, 4, 2, 3},
+                     {"h3r 256x128 nb3 8w fp32-only", 2, 1, 4, 3}, {"h3r 256x128 nb3 4w fp32-only", 2, 4, 4, 3},
+
+                     {"h3r 8w fp32-only global_load_lds", 2, 1, 14, 3}};
     const int nall = sizeof(all) / sizeof(all[0]);
     const int sel = argc > 3 ? (int)strtol(argv[3], nullptr, 0) : 0x3F;   // bit v: run variant v
     std::vector<V> vv;
@@ -150,8 +191,8 @@ int main(int argc, char **argv) {
         if (sel >> v & 1) vv.push_back(all[v]);
     const V *vs = vv.data();
     const int nv = (int)vv.size();
-    const double flop = (double)n * (n + 1) * K;
-    std::vector<float> ref;
+    const double flop = (double)n * (n + 1) * K;   // the lower triangle's FLOP (h3r's diagonal waste not counted)
+    std::vector<float> ref, diag;
     const int nrow = 8;
     std::vector<int> rows(nrow);
     for (int k = 0; k < nrow; ++k) rows[k] = (int)((int64_t)(k * 2 + 1) * n / (2 * nrow));
@@ -159,9 +200,10 @@ int main(int argc, char **argv) {
         for (int v = 0; v < nv; ++v) {
             SyrkArgs a{};
             a.N = n;
-            a.ntiles = ntiles;
+            const bool rect = vs[v].order == 2;
+            a.ntiles = rect ? ntiles_r : ntiles;
             a.t0 = 0;
-            a.tiles = vs[v].order ? d1 : d0;
+            a.tiles = rect ? d2 : vs[v].order ? d1 : d0;
             a.direct = vs[v].order;
             a.g32 = G;
             a.ldg = n;
@@ -174,7 +216,25 @@ int main(int argc, char **argv) {
             a.stamps = st;
             CK(hipMemset(G, 0, (size_t)n * n * 4));
             CK(hipEventRecord(e0));
-            if (vs[v].var == 1)
+            if (rect && vs[v].sb == 4 && vs[v].var == 0)   // sb field = waves for h3r
+                syrk_h3r_kernel<0, 3, 4><<<(unsigned)ntiles_r, 256>>>(a);
+            else if (rect && vs[v].sb == 4 && vs[v].var == 1)
+                syrk_h3r_kernel<1, 3, 4><<<(unsigned)ntiles_r, 256>>>(a);
+            else if (rect && vs[v].sb == 4 && vs[v].var == 2)
+                syrk_h3r_kernel<2, 3, 4><<<(unsigned)ntiles_r, 256>>>(a);
+            else if (rect && vs[v].sb == 4 && vs[v].var == 4)
+                syrk_h3r_kernel<4, 3, 4><<<(unsigned)ntiles_r, 256>>>(a);
+            else if (rect && vs[v].var == 4)
+                syrk_h3r_kernel<4, 3><<<(unsigned)ntiles_r, 512>>>(a);
+            else if (rect && vs[v].var == 14)
+                syrk_h3r_kernel<4, 3, 8, 1><<<(unsigned)ntiles_r, 512>>>(a);
+            else if (rect && vs[v].var == 0)
+                syrk_h3r_kernel<0, 3><<<(unsigned)ntiles_r, 512>>>(a);
+            else if (rect && vs[v].var == 1)
+                syrk_h3r_kernel<1, 3><<<(unsigned)ntiles_r, 512>>>(a);
+            else if (rect && vs[v].var == 2)
+                syrk_h3r_kernel<2, 3><<<(unsigned)ntiles_r, 512>>>(a);
+            else if (vs[v].var == 1)
                 syrk_h3q_kernel<1, 4, false, 1><<<(unsigned)ntiles, 512>>>(a);
             else if (vs[v].var == 2)
                 syrk_h3q_kernel<2, 4, false, 1><<<(unsigned)ntiles, 512>>>(a);
@@ -193,11 +253,11 @@ int main(int argc, char **argv) {
             CK(hipGetLastError());
             float ms;
             CK(hipEventElapsedTime(&ms, e0, e1));
-            std::vector<uint64_t> h(ntiles * 4);
-            CK(hipMemcpy(h.data(), st, ntiles * 32, hipMemcpyDeviceToHost));
+            std::vector<uint64_t> h(a.ntiles * 4);
+            CK(hipMemcpy(h.data(), st, a.ntiles * 32, hipMemcpyDeviceToHost));
             std::vector<double> clk;
             double cyc = 0;
-            for (int64_t w = 0; w < ntiles; w += 7) {
+            for (int64_t w = 0; w < a.ntiles; w += 7) {
                 const double dt = (double)(h[4 * w + 2] - h[4 * w]), dr = (double)(h[4 * w + 3] - h[4 * w + 1]);
                 if (dr > 0) clk.push_back(dt / dr * 100.0), cyc += dt;
             }
@@ -206,17 +266,26 @@ int main(int argc, char **argv) {
             std::vector<float> got((size_t)nrow * n);
             for (int k = 0; k < nrow; ++k) CK(hipMemcpy(&got[(size_t)k * n], G + (int64_t)rows[k] * n, (size_t)n * 4, hipMemcpyDeviceToHost));
             int64_t bad = -1;
+            double rel = -1.0;
             if (rep == 0 && v == 0) {
                 ref = got;
-            } else if (vs[v].var == 0) {
+                diag.resize(n);
+                CK(hipMemcpy2D(diag.data(), 4, G, (size_t)(n + 1) * 4, 4, n, hipMemcpyDeviceToHost));
+            } else if (vs[v].var == 0 || vs[v].var == 4 || vs[v].var == 10 || vs[v].var == 14) {
                 bad = 0;
+                rel = 0.0;
                 for (int k = 0; k < nrow; ++k)
-                    for (int j = 0; j <= rows[k]; ++j) bad += got[(size_t)k * n + j] != ref[(size_t)k * n + j];
+                    for (int j = 0; j <= rows[k]; ++j) {
+                        const float x = got[(size_t)k * n + j], y = ref[(size_t)k * n + j];
+                        bad += x != y;
+                        rel = std::max(rel, fabs((double)x - y) / sqrt((double)diag[rows[k]] * diag[j]));
+                    }
             }
             printf("{\"rep\": %d, \"variant\": \"%s\", \"n\": %d, \"ms\": %.2f, \"tflops_fp32eq\": %.1f, \"frac_h3_peak\": %.4f, "
-                   "\"clock_mhz_median\": %.0f, \"clock_mhz_p10\": %.0f, \"clock_mhz_p90\": %.0f, \"mismatch_vs_first\": %lld}\n",
+                   "\"clock_mhz_median\": %.0f, \"clock_mhz_p10\": %.0f, \"clock_mhz_p90\": %.0f, \"mismatch_vs_first\": %lld, "
+                   "\"max_abs_diff_over_sqrt_gii_gjj\": %.3g}\n",
                    rep, vs[v].name, n, ms, flop / (ms * 1e-3) * 1e-12, flop / (ms * 1e-3) * 1e-12 / (2516.0 / 3),
-                   clk[clk.size() / 2], clk[clk.size() / 10], clk[clk.size() * 9 / 10], (long long)bad);
+                   clk[clk.size() / 2], clk[clk.size() / 10], clk[clk.size() * 9 / 10], (long long)bad, rel);
             fflush(stdout);
         }
     return 0;
