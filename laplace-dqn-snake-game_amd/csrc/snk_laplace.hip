@@ -179,50 +179,24 @@ __global__ void jac_permute_kernel(const float *__restrict__ Jp, int64_t ldp, co
     }
 }
 
-// Lower-triangle tiles in the chip-wide order (round 5). Workgroup w runs on XCD w % 8,
-// so entry j * 8 + x of the table is XCD x's j-th tile, and one dispatch round (256
-// workgroups, one per CU) is table entries [256 r, 256 r + 256). The lower triangle is
-// walked in macro blocks of 16 x 16 tiles; a block's tiles, in sub-block-major order
-// (sub-blocks of 8 block rows x 4 block columns), are dealt to the 8 XCD queues in
-// contiguous chunks: a full block gives each XCD one 8 x 4 sub-block (its ~32 concurrent
-// workgroups share 8 + 4 row panels in its L2, as the round-3 supertile order did), and
-// the 8 XCDs of a round now work ONE block, so they share its 32 row panels in the 256 MB
-// Infinity Cache instead of streaming 8 disjoint sets from HBM (tools/syrk_lab.hip:
-// 507 -> 493-500 ms at n = 50,000, the held clock 1.64 -> 1.67-1.70 GHz, bit-identical G).
-// Partial blocks (the diagonal, the bottom edge) deal floor / ceil chunks, the extra tiles
-// rotating over the XCDs, so the queue lengths differ by at most one and the table is dense.
-// One device table per N, kept.
+// Lower-triangle tiles in supertile order: groups of 8 block rows x 4 block
+// columns, so the ~32 workgroups an XCD runs at once (syrk_xcd_remap hands
+// each XCD a contiguous run of this list) share 8 + 4 row blocks in its L2
+// instead of 1 + 32 in plain row-major order. One device table per N, kept.
+// Round 5 measured a chip-wide order (the 8 XCDs of a dispatch round on one 16 x 16 block,
+// sharing its panels in the Infinity Cache; tools/syrk_lab.hip order 1): 7 % faster on rows
+// with 40 % zeros (505 -> 473 ms, the clock 1.73 -> 1.80 GHz), but 3 % slower on dense rows
+// like the D(50k) Jacobian's (525 -> 541 ms at 1.5 GHz, gpurun_out r05j): with dense operands
+// the matrix cores' own power holds the clock down, not the HBM stream. Not kept.
 static std::vector<int2> syrk_tile_order_host(int N) {
     const int T = (int)ceil_div(N, SY_T);
-    constexpr int MB = 16, SI = 8, SJ = 4;
-    std::vector<std::vector<int2>> q(8);
-    int rr = 0;
-    std::vector<int2> blk;
-    for (int I0 = 0; I0 < T; I0 += MB)
-        for (int J0 = 0; J0 <= I0; J0 += MB) {
-            blk.clear();
-            for (int si = I0; si < std::min(T, I0 + MB); si += SI)
-                for (int sj = J0; sj < std::min(T, J0 + MB); sj += SJ)
-                    for (int i = si; i < std::min(T, si + SI); ++i)
-                        for (int j = sj; j < std::min(sj + SJ, i + 1); ++j) blk.push_back(int2{i, j});
-            const int cnt = (int)blk.size(), base = cnt / 8, extra = cnt % 8;
-            int p = 0;
-            for (int x = 0; x < 8; ++x) {
-                const int len = base + ((x - rr + 8) % 8 < extra ? 1 : 0);
-                for (int e = 0; e < len; ++e) q[x].push_back(blk[p++]);
-            }
-            rr = (rr + extra) % 8;
-        }
-    size_t mx = 0;
-    for (auto &v : q) mx = std::max(mx, v.size());
     std::vector<int2> t;
     t.reserve((size_t)T * (T + 1) / 2);
-    for (size_t j = 0; j < mx; ++j)
-        for (int x = 0; x < 8; ++x)
-            if (j < q[x].size()) {
-                SNK_CHECK(t.size() % 8 == (size_t)x, SNK_ERR_INTERNAL, "syrk tile order: XCD queues unbalanced");
-                t.push_back(q[x][j]);
-            }
+    constexpr int SI = 8, SJ = 4;
+    for (int i0 = 0; i0 < T; i0 += SI)
+        for (int j0 = 0; j0 <= std::min(T - 1, i0 + SI - 1); j0 += SJ)
+            for (int i = i0; i < std::min(T, i0 + SI); ++i)
+                for (int j = j0; j < std::min(j0 + SJ, i + 1); ++j) t.push_back(int2{i, j});
     SNK_CHECK((int64_t)t.size() == (int64_t)T * (T + 1) / 2, SNK_ERR_INTERNAL, "syrk tile order");
     return t;
 }
@@ -244,8 +218,7 @@ static const int2 *syrk_tile_order(int N) {
 
 // lower-triangle tiles [t0, t1) of syrk_tile_order(N) for shard `rank` of `nranks`
 // (contiguous runs of the supertile order: each shard keeps its L2 locality)
-// (run boundaries on multiples of 8: the table's XCD interleave then matches each shard's
-// own workgroup numbering)
+// (run boundaries on multiples of 8)
 static void gram_tile_range(int64_t N, int rank, int nranks, int64_t &t0, int64_t &t1) {
     const int64_t T = ceil_div(N, SY_T), tot = T * (T + 1) / 2;
     auto cut = [&](int r) { return r >= nranks ? tot : std::min(tot, (tot * r / nranks) & ~int64_t(7)); };
@@ -258,8 +231,7 @@ static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s, int r
     int64_t t1 = 0;
     gram_tile_range(a.N, rank, nranks, a.t0, t1);
     a.ntiles = t1 - a.t0;
-    a.tiles = syrk_tile_order(a.N);   // chip-wide order, XCDs interleaved in the table
-    a.direct = 1;
+    a.tiles = syrk_tile_order(a.N);   // XCD-aware supertile order (through syrk_xcd_remap)
     if (a.ntiles == 0) return;
     SNK_CHECK(a.K % 4 == 0 && a.ld % 4 == 0 && a.kchunk % 4 == 0, SNK_ERR_INTERNAL, "syrk: K/ld not multiples of 4");
     SNK_CHECK(a.ntiles < (int64_t)1 << 31 && z <= 65535, SNK_ERR_INVALID, "syrk: problem too large");
@@ -308,7 +280,6 @@ static void syrk_dense_launch(const SyrkArgs &a0, hipStream_t s, int rank, int n
     gram_tile_range(a.N, rank, nranks, a.t0, t1);
     a.ntiles = t1 - a.t0;
     a.tiles = syrk_tile_order(a.N);
-    a.direct = 1;
     if (a.ntiles == 0) return;
     SNK_CHECK(a.xh && a.xe && a.act && a.g32 && a.ldh % SY_KS == 0 && 0 < a.s1 && a.s1 < a.s2 &&
                   a.s2 < a.ldh / SY_KS && a.xes >= a.N,

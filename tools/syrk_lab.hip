@@ -11,7 +11,7 @@
 // variants only reorder tiles and barriers: identical per-tile arithmetic).
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 -DSNK_SYRK_MEASURE -I include \
 //   -I laplace-dqn-snake-game_amd/csrc tools/syrk_lab.hip -o tools/syrk_lab.bin
-// ./tools/syrk_lab.bin [n=50000] [reps=2] [variant mask=0x3F]
+// ./tools/syrk_lab.bin [n=50000] [reps=2] [variant mask=0x3F] [zero %=0]
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -37,8 +37,8 @@ using namespace snk;
     } while (0)
 
 // rows of roughly Jacobian-like statistics: normal values, a per-row binade spread and
-// ~40 % exact zeros (dead relu channels), from a counter hash
-__global__ void fill_rows(float *x, int64_t n, int64_t K, uint64_t seed) {
+// zero_pct % exact zeros (dead relu channels), from a counter hash
+__global__ void fill_rows(float *x, int64_t n, int64_t K, uint64_t seed, int zero256) {
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * K; t += (int64_t)gridDim.x * blockDim.x) {
         uint64_t z = (uint64_t)t * 0x9E3779B97F4A7C15ull + seed;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -47,7 +47,7 @@ __global__ void fill_rows(float *x, int64_t n, int64_t K, uint64_t seed) {
         const float u1 = ((z >> 40) + 0.5f) * (1.0f / 16777216.0f), u2 = ((z & 0xFFFFFF) + 0.5f) * (1.0f / 16777216.0f);
         const float g = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853f * u2);
         const int64_t row = t / K;
-        const bool dead = ((z >> 24) & 0xFF) < 100;
+        const bool dead = (int)((z >> 24) & 0xFF) < zero256;
         x[t] = dead ? 0.0f : ldexpf(g, (int)(row % 9) - 4);
     }
 }
@@ -146,7 +146,8 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&xe, (size_t)npad * 4));
     CK(hipMemset(xhl, 0, (size_t)npad * 2 * ldh * 2));
     CK(hipMemset(xe, 0, (size_t)npad * 4));
-    fill_rows<<<4096, 256>>>(x, n, K, 12345);
+    const int zero_pct = argc > 4 ? atoi(argv[4]) : 0;   // 0: dense rows (the library's D(50k) rows are)
+    fill_rows<<<4096, 256>>>(x, n, K, 12345, zero_pct * 256 / 100);
     h3_rows_kernel<<<n, 256>>>(x, K, K, xhl, xe, ldh);
     CK(hipDeviceSynchronize());
     CK(hipFree(x));
