@@ -581,7 +581,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
             const int o4 = tid & 15, c = tid >> 4;   // outputs 4 o4 .. +3, channel c of this half
             const f32x4 *w1 = reinterpret_cast<const f32x4 *>(n.th + L.off_d1w + (int64_t)(32 * half + c) * 64 + 4 * o4);
             double z0 = 0.0, z1 = 0.0, z2 = 0.0, z3 = 0.0;
-            constexpr int PB = 7;   // W1 rows in flight per thread
+            constexpr int PB = (NO + 1) / 2;   // W1 rows in flight per thread: two batches (L2 round trips)
             for (int p0 = 0; p0 < NO; p0 += PB) {
                 f32x4 wv[PB];
 #pragma unroll
