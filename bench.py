@@ -706,8 +706,10 @@ def main():
             rr["update_roofline"] = {"bound": "mfma", "flop_per_update": ufl, "achieved": utf,
                                      "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s (fp32)",
                                      "frac": utf / PEAK_FP32_TFLOPS,
-                                     "note": "4 B F (B = 64) over the marginal update time; the update is a "
-                                             "chain of 7 dependent launches, latency-bound at B = 64"}
+                                     "note": "4 B F (B = 64, F = the 3136->64 reference net's forward FLOP) over "
+                                             "the marginal update time; the update is a chain of 5 dependent "
+                                             "launches (upd_fwd with Dense1 and both heads, d1_bwd, conv3_bwd, "
+                                             "conv2_bwd, grad_update), latency-bound at B = 64"}
         except Exception as e:   # report, do not fail the headline line
             out["reference_ratio"] = {"error": str(e)}
         out["updates_per_s"] = args.updates_per_iter * args.steps / elapsed
