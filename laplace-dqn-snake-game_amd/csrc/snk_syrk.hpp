@@ -855,8 +855,12 @@ constexpr int SR_A = 256, SR_B = 128;
 // a quarter fewer fragment reads per MFMA again)
 // GL: the stage pieces by global_load_lds with one 64-bit source per job (as syrk_h3q_kernel)
 // instead of the buffer descriptors
-template <int VAR = 0, int NB = 3, int NW = 8, int GL = 0>
+// LEAN (NW = 8): the B fragments single-buffered in two column-tile halves (each refilled
+// with the next stage's right after its last MFMA of this stage), 64 fragment registers
+// instead of 96, which leaves room for the second-level sum
+template <int VAR = 0, int NB = 3, int NW = 8, int GL = 0, int LEAN = 0>
 __global__ __launch_bounds__(64 * NW) void syrk_h3r_kernel(SyrkArgs a) {
+    static_assert(!LEAN || NW == 8, "lean B fragments: 8 waves");
     constexpr int NJ = 48 / NW;                         // DMA jobs per wave and stage (48 KB / NW waves / 1 KB)
     constexpr int NTA = 2 * SR_A / NW / 16;             // A row tiles per wave (4 or 8)
     constexpr int NG = NTA / 2;                         // groups of two row tiles
@@ -1007,7 +1011,7 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3r_kernel(SyrkArgs a) {
     FA f0, f1;   // row-tile groups alternate: group gi in f(gi & 1)
     FB b0, b1;
     frag_a(0, 0, f0);
-    frag_b(0, b0);
+    if constexpr (!LEAN) frag_b(0, b0);
     // step st (buffer B = st % NB; f0 / bc hold stage st's row-tile group 0 and B): the first
     // MFMA, group 1's fragments, the rest of group 0; each further group's MFMAs with the next
     // group's fragments read under them; the DMA of stage st+NB-1 (into the buffer of stage
@@ -1043,11 +1047,80 @@ __global__ __launch_bounds__(64 * NW) void syrk_h3r_kernel(SyrkArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         if (st % SY_FLUSH == SY_FLUSH - 1) flush();
     };
-    constexpr int U = NB % 2 ? 2 * NB : NB;
+    typedef f16x8 FB2[2][2];   // two column tiles x plane
+    auto frag_b2 = [&](int buf, int j0, FB2 &f) __attribute__((always_inline)) {
+        const uint16_t *base = lds + buf * STG;
+#pragma unroll
+        for (int pn = 0; pn < 2; ++pn)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = wc + 16 * (j0 + j) + r;
+                f[j][pn] = as_h(*reinterpret_cast<const u32x4 *>(base + (2 * SR_A + pn * SR_B + row) * SH_ROW +
+                                                                 8 * (g ^ syrk_swz16(row))));
+            }
+    };
+    // 2 row tiles x 2 column tiles (12 MFMAs); part as mfma_half
+    auto mfma_q = [&](const FA &fa, const FB2 &fb, int t0, int j0, int part) __attribute__((always_inline)) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                const int i = t0 + ii, j = j0 + jj;
+                const bool first = ii == 0 && jj == 0;
+                if (VAR == 1) {
+                    if (part != 0 && (part == 2 || !first))
+                        acc[i][j][0] += (float)(fa[ii][0][0] * fb[jj][0][0]) + (float)(fa[ii][1][1] * fb[jj][1][1]);
+                    continue;
+                }
+                if (part == 2 || (part == 0) == first)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][1], fb[jj][0], acc[i][j], 0, 0, 0);
+                if (part != 0) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][0], fb[jj][1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[ii][0], fb[jj][0], acc[i][j], 0, 0, 0);
+                }
+            }
+    };
+    FB2 q01, q23;
+    if constexpr (LEAN) {
+        frag_b2(0, 0, q01);
+        frag_b2(0, 2, q23);
+    }
+    auto step_lean = [&](int st, auto bc_) __attribute__((always_inline)) {
+        constexpr int B = decltype(bc_)::value;
+        mfma_q(f0, q01, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_a(B, 2, f1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_q(f0, q01, 0, 0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_q(f0, q23, 0, 2, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        dma(st + NB - 1, (B + NB - 1) % NB);
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm((NB - 2) * NJ));   // my part of stage st+1 landed
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        frag_a((B + 1) % NB, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_q(f1, q01, 2, 0, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_b2((B + 1) % NB, 0, q01);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_q(f1, q23, 2, 2, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_b2((B + 1) % NB, 2, q23);
+        __builtin_amdgcn_sched_barrier(0);
+        if (st % SY_FLUSH == SY_FLUSH - 1) flush();
+    };
+    constexpr int U = LEAN ? NB : NB % 2 ? 2 * NB : NB;
     auto one = [&](int st0, bool tail, auto ic) __attribute__((always_inline)) {
         constexpr int I = decltype(ic)::value;
-        if (!tail || st0 + I < nst)
-            step(st0 + I, std::integral_constant<int, I % NB>{}, I % 2 ? b1 : b0, I % 2 ? b0 : b1);
+        if (!tail || st0 + I < nst) {
+            if constexpr (LEAN)
+                step_lean(st0 + I, std::integral_constant<int, I % NB>{});
+            else
+                step(st0 + I, std::integral_constant<int, I % NB>{}, I % 2 ? b1 : b0, I % 2 ? b0 : b1);
+        }
     };
     auto trip = [&](int st0, bool tail) __attribute__((always_inline)) {
         static_assert(U <= 6, "unrolled trip");

@@ -184,7 +184,8 @@ int main(int argc, char **argv) {
                      {"h3r 256x128 nb3 4 waves no-DMA", 2, 4, 2, 3},
                      {"h3r 256x128 nb3 8w fp32-only", 2, 1, 4, 3}, {"h3r 256x128 nb3 4w fp32-only", 2, 4, 4, 3},
 
-                     {"h3r 8w fp32-only global_load_lds", 2, 1, 14, 3}};
+                     {"h3r 8w fp32-only global_load_lds", 2, 1, 14, 3},
+                     {"h3r 8w lean two-level", 2, 1, 20, 3}};
     const int nall = sizeof(all) / sizeof(all[0]);
     const int sel = argc > 3 ? (int)strtol(argv[3], nullptr, 0) : 0x3F;   // bit v: run variant v
     std::vector<V> vv;
@@ -227,6 +228,8 @@ int main(int argc, char **argv) {
                 syrk_h3r_kernel<4, 3, 4><<<(unsigned)ntiles_r, 256>>>(a);
             else if (rect && vs[v].var == 4)
                 syrk_h3r_kernel<4, 3><<<(unsigned)ntiles_r, 512>>>(a);
+            else if (rect && vs[v].var == 20)
+                syrk_h3r_kernel<0, 3, 8, 0, 1><<<(unsigned)ntiles_r, 512>>>(a);
             else if (rect && vs[v].var == 14)
                 syrk_h3r_kernel<4, 3, 8, 1><<<(unsigned)ntiles_r, 512>>>(a);
             else if (rect && vs[v].var == 0)
@@ -272,7 +275,7 @@ int main(int argc, char **argv) {
                 ref = got;
                 diag.resize(n);
                 CK(hipMemcpy2D(diag.data(), 4, G, (size_t)(n + 1) * 4, 4, n, hipMemcpyDeviceToHost));
-            } else if (vs[v].var == 0 || vs[v].var == 4 || vs[v].var == 10 || vs[v].var == 14) {
+            } else if (vs[v].var == 0 || vs[v].var == 4 || vs[v].var == 14 || vs[v].var == 20) {
                 bad = 0;
                 rel = 0.0;
                 for (int k = 0; k < nrow; ++k)
