@@ -48,6 +48,11 @@ struct H3FArgs {
 // conv2's split weight image in LDS: [5 offset pairs][h | l][32 co][48 halves] (k = 16 (kk & 1)
 // + ci in the first 32 halves of a row; kk = 9 is zero), 1,920 16-byte chunks, padded to 2,048
 constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
+// conv3 LDS-DMA lookahead (NBUF 8): offset kk + H3F_LA is issued while kk runs
+#ifndef H3F_LA
+#define H3F_LA 4
+#endif
+static_assert(H3F_LA >= 4 && H3F_LA <= 7, "lookahead: 4..7 (buffer 7 holds conv1's boards in the prologue)");
 
 // conv3's weight image [36 kk][64 co][32 ci] (fp32) -> fp16 h / l parts of w * 2^ew, ew from the
 // partial maxima, laid out exactly as conv_h3f_kernel's register path stores one offset into a B
@@ -236,10 +241,8 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
                 __builtin_amdgcn_global_load_lds((const void *)(a.w2h + ((int64_t)q * 512 + tid) * 8),
                                                  (__attribute__((address_space(3))) void *)(B2 + (q * 512 + wave * 64) * 8),
                                                  16, 0, 0);
-            dma(0);   // conv1 stages its boards in buffer 7
-            dma(1);
-            dma(2);
-            dma(3);
+#pragma unroll
+            for (int k = 0; k < H3F_LA; ++k) dma(k);   // conv1 stages its boards in buffer 7
         }
     };
     // LDS-only barrier (no vmcnt drain) while the prologue DMAs are in flight
@@ -439,7 +442,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
             A1v[(((sr * 2 + 1) * NPB + pb) * XR + c0) / 4] = ll;
         }
     }
-    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(4));   // conv2's weights landed (offsets 0..3 may not)
+    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(H3F_LA));   // conv2's weights landed (the offsets may not)
     lds_barrier();
     H3F_CLK(2);
 
@@ -561,7 +564,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     }
     b_store(0, 0);
     b_store(1, 1);
-    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // offsets 0..3 landed (published below)
+    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // offsets 0..H3F_LA-1 landed (published below)
 
     constexpr int T = (NSG * ho2 + 15) / 16;
     const int rg = wave >> 1, cg = wave & 1;
@@ -628,14 +631,15 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         // read at kk+2 and last read at kk-2, so a barrier always separates the two
         auto step = [&](int kk, const Frag &cur, Frag &nxt, int set) {
             if constexpr (DMA) {
-                // offset kk + 4 into buffer (kk + 4) & 7, last read at step kk - 5 (a barrier
-                // since); after odd offsets: everything but the newest DMA landed (offsets
-                // <= kk + 3, read at steps <= kk + 2), the barrier publishes it
-                dma(kk + 4);
+                // offset kk + LA into buffer (kk + LA) & 7, last read at step kk + LA - 9 (an odd
+                // step, so a barrier, lies between for LA <= 7); after odd offsets: everything
+                // but the newest LA - 3 DMAs landed (offsets <= kk + 3, read at steps <= kk + 2),
+                // the barrier publishes them
+                dma(kk + H3F_LA);
                 frag_read(kk + 1, nxt);
                 mfma_block(cur);
                 if (kk & 1) {
-                    __builtin_amdgcn_s_waitcnt(waitcnt_vm(1));
+                    __builtin_amdgcn_s_waitcnt(waitcnt_vm(H3F_LA - 3));
                     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
                     __builtin_amdgcn_s_barrier();
                 }
