@@ -65,6 +65,9 @@ int guard(F &&f) {
 // device, raised to at least `bytes` (set once per kernel, device and size)
 void set_lds_limit(const void *kernel, size_t bytes);
 
+// compute units of the current device (persistent launches: one workgroup per CU)
+int cu_count();
+
 template <class T>
 T *dalloc(size_t n) {
     void *p = nullptr;

@@ -44,6 +44,8 @@ struct H3FArgs {
     const int *w3e;      // w3h's exponent (ew), then w2h's (ew2)
     const uint16_t *w2h;
     float *a3max;        // optional: max of each sample's a3 (>= 0: post-relu), for Dense1's h3 scale
+    uint32_t *ticket;    // optional (NBUF 8, boards from the env frame ring or floats): persistent
+                         // launch, one workgroup per CU; the group counter, zero between launches
 };
 // conv2's split weight image in LDS: [5 offset pairs][h | l][32 co][48 halves] (k = 16 (kk & 1)
 // + ci in the first 32 halves of a row; kk = 9 is zero), 1,920 16-byte chunks, padded to 2,048
@@ -51,6 +53,10 @@ constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 // conv3 LDS-DMA lookahead (NBUF 8): offset kk + H3F_LA is issued while kk runs
 #ifndef H3F_LA
 #define H3F_LA 4
+#endif
+// persistent conv_h3f_kernel launches (H3FArgs::ticket) for the act forward
+#ifndef H3F_PERSIST
+#define H3F_PERSIST 0
 #endif
 static_assert(H3F_LA >= 4 && H3F_LA <= 7, "lookahead: 4..7 (buffer 7 holds conv1's boards in the prologue)");
 
@@ -145,7 +151,7 @@ static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__res
 __device__ uint64_t *g_h3f_clk;
 #define H3F_CLK(slot)                                                                                 \
     do {                                                                                              \
-        if (threadIdx.x == 0 && g_h3f_clk) g_h3f_clk[((int64_t)blockIdx.x - rb) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0 && g_h3f_clk) g_h3f_clk[(int64_t)grp * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define H3F_CLK(slot) do { } while (0)
@@ -165,7 +171,7 @@ constexpr int h3f_lds_bytes() {
 // NBUF conv3 B buffers: 2 = one barrier per kernel offset (B(kk+2) staged while kk
 // runs); 4 = one barrier per offset PAIR (B(kk+3) staged, read two offsets later)
 template <int HIN, int NBUF = 4, int CF = 2>
-__global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
+__global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
     static_assert(NBUF == 2 || NBUF == 4 || NBUF == 8, "B buffers");
     // NBUF 8: the B buffers are filled by LDS-DMA from the pre-split image a.w3h (no
     // register staging, no split): offset kk + 4 is issued while kk runs
@@ -183,9 +189,9 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     static_assert(XR % 8 == 0 && BR % 8 == 0, "16-byte pieces");
     // the rider's workgroup is workgroup 0 (dispatched first: its serial draw overlaps the
     // sample groups instead of trailing them); it touches no LDS and no barrier
-    const int rb = a.rider.out ? 1 : 0;
+    const int rb = a_.rider.out ? 1 : 0;
     if (rb && blockIdx.x == 0) {
-        if (threadIdx.x < 64) sample_wave(a.rider);
+        if (threadIdx.x < 64) sample_wave(a_.rider);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) u32x4 h3f_lds[];
@@ -196,11 +202,40 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     u32x2 *Bs2 = reinterpret_cast<u32x2 *>(Bs);
     uint16_t *A1 = reinterpret_cast<uint16_t *>(As), *B2 = A1 + A1_H;
     u32x2 *A1v = reinterpret_cast<u32x2 *>(A1), *B2v = reinterpret_cast<u32x2 *>(B2);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // persistent mode (a.ticket; H3F_PERSIST builds, env frame ring boards): the grid is at most one workgroup per CU; each runs group
+    // blockIdx - rb first, then group nwg + t for each ticket t it draws (one draw per group,
+    // at the group's start; the draw that returns ngroups - 1 is the launch's last and resets
+    // the counter). The next group's board cells are loaded into registers between the
+    // current group's conv3 offsets and its epilogue, so their latency hides behind it.
+    const bool persist = H3F_PERSIST && DMA && a_.ticket != nullptr;
+    const int ngroups = (S + NSG - 1) / NSG, nwg = (int)gridDim.x - rb;
+    int grp = (int)blockIdx.x - rb;
+    constexpr int NX = NSG * CF * NPB, LB = (NX + 511) / 512;
+    int bv[LB];                // this thread's board cells of the group ([sample][channel][bordered cell])
+    bool have_boards = false;  // bv holds the group's cells already (persistent passes after the first)
+    const int8_t *cbase[CF];   // persistent, env frame ring: plane(s, c) = cbase[c] + s * pitch
+    __shared__ int s_next;     // persistent: the group this workgroup runs next
+#if H3F_PERSIST
+    for (;;) {
+    // the weights' pointers and the thread index through an empty asm per pass: their loads
+    // and the address arithmetic on tid stay in the pass (hoisted out of the group loop they
+    // held ~100 VGPRs through conv3 and spilled); & 511 restores tid's range
+    H3FArgs a = a_;
+    asm volatile("" : "+s"(a.w1), "+s"(a.b1), "+s"(a.b2), "+s"(a.b3), "+s"(a.w3e), "+s"(a.w2), "+s"(a.w3), "+s"(a.wmax));
+    int z_ = 0;
+    asm volatile("" : "+s"(z_));
+    const int tid = ((int)threadIdx.x + z_) & 511;
+#else
+    const H3FArgs &a = a_;
+    const int tid = threadIdx.x;
+#endif
+    const int lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
-    const int s0 = ((int)blockIdx.x - rb) * NSG;
+    const int s0 = grp * NSG;
     const int ns = min(NSG, S - s0);
     H3F_CLK(0);
+    uint32_t tk = 0;
+    if (persist && tid == 0) tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // conv3 B register sets (as conv_h3s_kernel)
     const f32x4 *__restrict__ wsrc = reinterpret_cast<const f32x4 *>(a.w3);
@@ -301,40 +336,45 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         float *xin = reinterpret_cast<float *>(Bs + (DMA ? 7 * NB : 0));
         static_assert(NSG * C * NPB <= (DMA ? NB : NBUF * NB) * 4, "conv1 staging fits the B buffers");
         __shared__ const int8_t *pbase[NSG * C];
-        if (tid < NSG * C) pbase[tid] = tid / C < ns ? a.src.plane(s0 + tid / C, tid % C) : nullptr;
+        if (!have_boards && tid < NSG * C) pbase[tid] = tid / C < ns ? a.src.plane(s0 + tid / C, tid % C) : nullptr;
         const int cq = tid & 3;
         f32x4 w1r[9 * C], b1r;
 #pragma unroll
         for (int q = 0; q < 9 * C; ++q) w1r[q] = reinterpret_cast<const f32x4 *>(a.w1)[q * 4 + cq];
         b1r = reinterpret_cast<const f32x4 *>(a.b1)[cq];
-        __syncthreads();
-        // every cell load of the thread goes out before the first is used (a loop of
-        // load-then-store waited out one round trip per cell), through global (not flat)
-        // pointers: the plane pointers come from LDS as generic ones
-        typedef const __attribute__((address_space(1))) int8_t gi8;
-        constexpr int NX = NSG * C * NPB, LB = (NX + 511) / 512;
         const bool fl = a.src.fbase != nullptr;
-        int bv[LB], bsc[LB], bcell[LB];
-        bool bin[LB];
+        if (!have_boards) {
+            __syncthreads();
+            // every cell load of the thread goes out before the first is used (a loop of
+            // load-then-store waited out one round trip per cell), through global (not flat)
+            // pointers: the plane pointers come from LDS as generic ones
+            typedef const __attribute__((address_space(1))) int8_t gi8;
+            int bsc[LB], bcell[LB];
+            bool bin[LB];
 #pragma unroll
-        for (int u = 0; u < LB; ++u) {
-            const int q = u * 512 + tid;
-            const int sc = min(q / NPB, NSG * C - 1), b = q - sc * NPB;
-            const int bj = b / BP, bi = b - bj * BP;
-            bsc[u] = sc;
-            bcell[u] = (bi - 1) + (bj - 1) * hin;
-            bin[u] = q < NX && sc / C < ns && bi >= 1 && bi <= hin && bj >= 1 && bj <= hin;
-        }
-        if (fl) {
+            for (int u = 0; u < LB; ++u) {
+                const int q = u * 512 + tid;
+                const int sc = min(q / NPB, NSG * C - 1), b = q - sc * NPB;
+                const int bj = b / BP, bi = b - bj * BP;
+                bsc[u] = sc;
+                bcell[u] = (bi - 1) + (bj - 1) * hin;
+                bin[u] = q < NX && sc / C < ns && bi >= 1 && bi <= hin && bj >= 1 && bj <= hin;
+            }
+            if (fl) {
 #pragma unroll
-            for (int u = 0; u < LB; ++u)
-                bv[u] = bin[u] ? __float_as_int(a.src.fbase[((int64_t)(s0 + bsc[u] / C) * C + bsc[u] % C) * hin2 + bcell[u]]) : 0;
-        } else {
-            gi8 *pl[LB];
+                for (int u = 0; u < LB; ++u)
+                    bv[u] = bin[u] ? __float_as_int(a.src.fbase[((int64_t)(s0 + bsc[u] / C) * C + bsc[u] % C) * hin2 + bcell[u]]) : 0;
+            } else {
+                gi8 *pl[LB];
 #pragma unroll
-            for (int u = 0; u < LB; ++u) pl[u] = (gi8 *)pbase[bsc[u]];
+                for (int u = 0; u < LB; ++u) pl[u] = (gi8 *)pbase[bsc[u]];
 #pragma unroll
-            for (int u = 0; u < LB; ++u) bv[u] = bin[u] ? (int)pl[u][bcell[u]] : 0;
+                for (int u = 0; u < LB; ++u) bv[u] = bin[u] ? (int)pl[u][bcell[u]] : 0;
+            }
+            // the ring's slot of each channel is the launch's (one step counter): the first
+            // group's sample-0 planes give every later group's
+#pragma unroll
+            for (int c = 0; c < C; ++c) cbase[c] = persist ? pbase[c] - (int64_t)s0 * a.src.pitch : nullptr;
         }
 #pragma unroll
         for (int u = 0; u < LB; ++u) {
@@ -570,7 +610,30 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     const int rg = wave >> 1, cg = wave & 1;
     const int nt = __builtin_amdgcn_readfirstlane(T > rg ? (T - rg + 3) / 4 : 0);
     const int bslot = (cg * 32 + r) * 4 + (g ^ ((4 - ((r >> 2) & 3)) & 3));
+    if (persist && tid == 0) {   // (the ticket returned long ago: the DMA waits above are in order)
+        s_next = nwg + (int)tk;
+        if (tk == (uint32_t)(ngroups - 1)) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
+    // persistent: the next group's board cells into bv (after the conv3 offsets: no LDS-DMA in
+    // flight, so the compiler's own vmcnt waits stay exact), as the first pass loads them
+    auto prefetch = [&]() __attribute__((always_inline)) {
+        const int gn = s_next;
+        if (!persist || gn >= ngroups) return;
+        const int s1 = gn * NSG, ns1 = min(NSG, S - s1);
+        typedef const __attribute__((address_space(1))) int8_t gi8;
+#pragma unroll
+        for (int u = 0; u < LB; ++u) {
+            const int q = u * 512 + tid;
+            const int sc = min(q / NPB, NSG * CF - 1), b = q - sc * NPB;
+            const int bj = b / BP, bi = b - bj * BP;
+            const int sr = sc / CF, c = sc - sr * CF;
+            const int cell = (bi - 1) + (bj - 1) * hin;
+            const bool in = q < NX && sr < ns1 && bi >= 1 && bi <= hin && bj >= 1 && bj <= hin;
+            const int8_t *cb = (CF > 1 && c) ? cbase[CF - 1] : cbase[0];
+            bv[u] = in ? (int)((gi8 *)(cb + (int64_t)(s1 + sr) * a.src.pitch))[cell] : 0;
+        }
+    };
 
     // ---- conv3: conv_h3s_kernel's pipeline
     auto run = [&](auto ntc) {
@@ -673,6 +736,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
         }
         H3F_CLK(5);
         if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // the tail reloads landed
+        prefetch();
         // output through LDS as conv_h3s_kernel
         constexpr int CS = 80;
         static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN, NBUF>() - NBUF * NB * 16, "output staging fits");
@@ -729,6 +793,14 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a, int S) {
     else if (nt == 3) run(std::integral_constant<int, 3>{});
     else if (nt == 2) run(std::integral_constant<int, 2>{});
     else run(std::integral_constant<int, 1>{});
+#if H3F_PERSIST
+    if (!persist) return;
+    __syncthreads();   // the epilogue's reads of the A region are done before the next group stages there
+    grp = s_next;
+    if (grp >= ngroups) return;
+    have_boards = true;
+    }
+#endif
 }
 
 }  // namespace snk

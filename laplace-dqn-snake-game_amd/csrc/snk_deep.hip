@@ -166,17 +166,6 @@ static void work_ensure(DeepNet &N, DeepWork &w, int64_t S, bool train) {
 }
 
 // ---------------------------------------------------------------- forward
-// compute units of the current device (persistent launches: one workgroup per CU)
-static int cu_count() {
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        SNK_HIP(hipGetDevice(&dev));
-        SNK_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-        return std::max(n, 1);
-    }();
-    return cus;
-}
-
 template <int CIN, int COUT, int KS, int PAD, int H>
 static void conv_layer(const uint16_t *x, const uint16_t *img, const float *bias, uint16_t *y, int64_t S,
                        hipStream_t s) {

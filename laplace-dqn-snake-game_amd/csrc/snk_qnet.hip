@@ -799,7 +799,7 @@ void qwork_free(QWork &w) {
     for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a2b, (void *)w.a1b, (void *)w.a3, (void *)w.slab, (void *)w.cslab,
                     (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.x0, (void *)w.target,
-                    (void *)w.loss, (void *)w.upd_ticket, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e,
+                    (void *)w.loss, (void *)w.upd_ticket, (void *)w.h3f_ticket, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e,
                     (void *)w.w2h, (void *)w.w1h, (void *)w.w1e, (void *)w.a3max})
         dfree(p);
     w = QWork{};
@@ -864,6 +864,8 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     w.w1h = dalloc<uint16_t>((size_t)L.Wo * L.Wo * 2 * 4096);
     w.w1e = dalloc<int>((size_t)L.Wo * L.Wo * 64);
     w.a3max = dalloc<float>((size_t)cap);
+    w.h3f_ticket = dalloc<uint32_t>(1);
+    SNK_HIP(hipMemsetAsync(w.h3f_ticket, 0, 4, stream()));
     SNK_HIP(hipMemsetAsync(w.w2h, 0, (size_t)H3F_B2_CHUNKS * 16, stream()));   // pads stay zero
     if (tr) {
         w.has_train = 1;
@@ -906,13 +908,18 @@ static void h3c2_launch_bs(const float *a1, const float *wimg, const float *b2, 
 // One barrier per offset pair either way.
 template <int HIN, int CF>
 static void h3f_launch_t(const H3FArgs &fa, int64_t S, hipStream_t s) {
-    const unsigned grid = (unsigned)(ceil_div(S, 4) + (fa.rider.out ? 1 : 0));
+    const int64_t ngroups = ceil_div(S, 4);
+    const unsigned rb = fa.rider.out ? 1 : 0;
     if constexpr (h3f_lds_bytes<HIN, 8>() <= 160 * 1024) {
+        // persistent (fa.ticket): one workgroup per CU (the LDS admits one), the groups by ticket
+        const unsigned grid = (unsigned)((fa.ticket ? std::min<int64_t>(ngroups, cu_count()) : ngroups) + rb);
         constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, 8>();
         SNK_CHECK(fa.w3h && fa.w3e, SNK_ERR_INTERNAL, "conv_h3f: no pre-split conv3 weights");
         set_lds_limit((const void *)conv_h3f_kernel<HIN, 8, CF>, lds);
         conv_h3f_kernel<HIN, 8, CF><<<grid, 512, lds, s>>>(fa, (int)S);
     } else {
+        const unsigned grid = (unsigned)(ngroups + rb);
+        SNK_CHECK(!fa.ticket, SNK_ERR_INTERNAL, "conv_h3f: persistent mode needs the LDS-DMA path");
         constexpr size_t lds = (size_t)h3f_lds_bytes<HIN, 4>();
         static_assert(lds <= 160 * 1024, "conv_h3f LDS");
         set_lds_limit((const void *)conv_h3f_kernel<HIN, 4, CF>, lds);
@@ -1056,6 +1063,9 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
                 fa.w2 = n.wt + L.off_t2; fa.b2 = n.th + L.off_b2; fa.w3 = img; fa.wmax = w.wmax_part;
                 fa.nwmax = w.wmax_n; fa.b3 = n.th + L.off_b3; fa.out = w.a3;
                 fa.a3max = dh3prep ? w.a3max : nullptr;
+                // persistent launch: boards from the env frame ring (replay slots would need a
+                // per-sample index load for every next group)
+                if (H3F_PERSIST && h3f_dma(L.bs) && !n.src.idx && !n.src.fbase) fa.ticket = w.h3f_ticket;
                 conv_h3f_launch(L.bs, L.C, fa, S, s);
             }
         }

@@ -39,6 +39,20 @@ void set_lds_limit(const void *kernel, size_t bytes) {
     have = bytes;
 }
 
+int cu_count() {
+    static std::mutex mu;
+    static std::map<int, int> cus;
+    int dev = 0;
+    SNK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    int &n = cus[dev];
+    if (n == 0) {
+        SNK_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+        n = n > 0 ? n : 1;
+    }
+    return n;
+}
+
 int arith(int knob) { return g_arith[knob]; }
 
 hipStream_t stream() {
