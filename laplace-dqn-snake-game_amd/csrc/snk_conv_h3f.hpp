@@ -54,6 +54,10 @@ constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 #ifndef H3F_LA
 #define H3F_LA 4
 #endif
+// conv3's output stored from the accumulators instead of through LDS
+#ifndef H3F_DIRECT
+#define H3F_DIRECT 0
+#endif
 // persistent conv_h3f_kernel launches (H3FArgs::ticket) for the act forward
 #ifndef H3F_PERSIST
 #define H3F_PERSIST 0
@@ -737,10 +741,11 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
         H3F_CLK(5);
         if constexpr (DMA) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // the tail reloads landed
         prefetch();
-        // output through LDS as conv_h3s_kernel
+        // output through LDS as conv_h3s_kernel (H3F_DIRECT builds: straight from the
+        // accumulators, each store 4 positions x 64 contiguous bytes)
         constexpr int CS = 80;
         static_assert(NSG * ho2 * CS * 4 <= h3f_lds_bytes<HIN, NBUF>() - NBUF * NB * 16, "output staging fits");
-        float *Cs = reinterpret_cast<float *>(As);
+        [[maybe_unused]] float *Cs = reinterpret_cast<float *>(As);
         float vm[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // this lane's max per sample (post-relu: >= 0)
 #pragma unroll
         for (int k = 0; k < NT; ++k) {
@@ -754,7 +759,11 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
                 for (int e = 0; e < 4; ++e) {
                     const float v = __builtin_ldexpf(acc[k][ct][e], -(ea[e] + ew)) + bv;
                     const float rv = v > 0.0f ? v : 0.0f;
+#if H3F_DIRECT
+                    if (e < ns) a.out[((int64_t)(s0 + e) * ho2 + p) * CN + col] = rv;
+#else
                     Cs[(e * ho2 + p) * CS + col] = rv;
+#endif
                     vm[e] = fmaxf(vm[e], rv);
                 }
             }
@@ -783,10 +792,12 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
                 for (int q = 0; q < 4; ++q) m = fmaxf(m, a3red[w][q][tid]);
             a.a3max[s0 + tid] = m;
         }
+#if !H3F_DIRECT
         const int n4o = ns * ho2 * 16;
         f32x4 *o4 = reinterpret_cast<f32x4 *>(a.out + (int64_t)s0 * ho2 * CN);
         const f32x4 *c4 = reinterpret_cast<const f32x4 *>(Cs);
         for (int q = tid; q < n4o; q += 512) o4[q] = c4[(q >> 4) * (CS / 4) + (q & 15)];
+#endif
         H3F_CLK(6);
     };
     if (nt == 4) run(std::integral_constant<int, 4>{});
