@@ -28,7 +28,8 @@
 //            dense1_upd_kernel (8.8 us) and its launch boundary in round 5: the 64 samples'
 //            W1 re-reads (401 KB per workgroup at 12x12) stay in L2.
 //   phase 5  (head) the last of the sample's four workgroups (its two halves in both nets,
-//            an agent-scope ticket per sample) runs both heads for it (head_pair_one: the
+//            a relaxed agent-scope ticket per sample, slabs handed over by sc1 stores and
+//            loads) runs both heads for it (head_pair_one: the
 //            t_net TD target, the q_net Huber loss, dq and dz1), which replaced the
 //            head_pair_kernel launch.
 // conv1 and conv2 run in both halves of a sample (they are ~20 % of the work);
@@ -59,6 +60,11 @@ __device__ uint64_t *g_upd_clk;
 // head_kernel<HEAD_TARGET> / <HEAD_LOSS> (snk_qnet.hip), the ks Dense1 slabs added to the
 // bias in slab order. Run by head_pair_kernel (one wave per sample) and by the last of a
 // sample's four update-forward workgroups (upd_fwd_kernel phase 5).
+// phase 5's slab hand-off by sc1 stores / loads and a relaxed ticket (0: an acq_rel ticket,
+// measurement builds only)
+#ifndef UPD_SC1
+#define UPD_SC1 1
+#endif
 struct HeadNet {
     const float *slab, *theta;
     float *h1, *q;
@@ -75,11 +81,13 @@ __device__ __forceinline__ void head_pair_one(const HeadNet &tn, const HeadNet &
     // q_net half used to start its loads only after the t_net half's reductions)
     constexpr int KMAX = 16;
     float zt[KMAX], zq[KMAX];
+    // slab loads sc1 (relaxed agent-scope, L1 bypassed): upd_fwd_kernel's phase 5 reads slabs
+    // other workgroups stored sc1 moments ago, with no acquire
 #pragma unroll
     for (int z = 0; z < KMAX; ++z) {
         if (z < ks) {
-            zt[z] = tn.slab[((int64_t)z * S + s) * 64 + lane];
-            zq[z] = qn.slab[((int64_t)z * S + s) * 64 + lane];
+            zt[z] = __hip_atomic_load(tn.slab + ((int64_t)z * S + s) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            zq[z] = __hip_atomic_load(qn.slab + ((int64_t)z * S + s) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     float wt2[3], wq2[3], bt2[3], bq2[3];
@@ -101,7 +109,8 @@ __device__ __forceinline__ void head_pair_one(const HeadNet &tn, const HeadNet &
         for (int z = 0; z < KMAX; ++z)
             if (z < ks) h += zt[z];
     } else {
-        for (int z = 0; z < ks; ++z) h += tn.slab[((int64_t)z * S + s) * 64 + lane];
+        for (int z = 0; z < ks; ++z)
+            h += __hip_atomic_load(tn.slab + ((int64_t)z * S + s) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     h = h > 0.0f ? h : 0.0f;
     tn.h1[s * 64 + lane] = h;
@@ -128,7 +137,8 @@ __device__ __forceinline__ void head_pair_one(const HeadNet &tn, const HeadNet &
         for (int z = 0; z < KMAX; ++z)
             if (z < ks) h += zq[z];
     } else {
-        for (int z = 0; z < ks; ++z) h += qn.slab[((int64_t)z * S + s) * 64 + lane];
+        for (int z = 0; z < ks; ++z)
+            h += __hip_atomic_load(qn.slab + ((int64_t)z * S + s) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     h = h > 0.0f ? h : 0.0f;
     qn.h1[s * 64 + lane] = h;
@@ -607,16 +617,29 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
         double z = 0.0;
 #pragma unroll 8
         for (int c = 0; c < 32; ++c) z += red[c * 64 + tid];
+#if UPD_SC1
+        // sc1 store (relaxed agent-scope): the line leaves the XCD's L2 for memory
+        __hip_atomic_store(n.slab + ((int64_t)half * args.S + s) * 64 + tid, (float)z, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+#else
         n.slab[((int64_t)half * args.S + s) * 64 + tid] = (float)z;
+#endif
         if (!args.head) return;
         // ---- phase 5: the last of the sample's four workgroups (2 halves x 2 nets) runs the
-        // heads. Release: the agent-scope atomic writes back this wave's slab stores (the only
-        // ones the heads read from this workgroup) before it counts; the last arriver's acquire
-        // (same atomic) invalidates its caches, so the other three workgroups' slabs, written
-        // on any XCD, are read fresh.
+        // heads. The hand-off without fences (an agent release / acquire pair is a write-back of
+        // the XCD's L2 and an L1 invalidate, ~3.5 us per workgroup): this wave stores its
+        // slab with sc1 stores and waits for them, then one lane counts with a relaxed agent
+        // atomic; the last arriver, told by the value its add returned, reads every slab with
+        // sc1 loads (head_pair_one), which bypass the stale L1 and find the data in memory.
         uint32_t last = 0;
+#if UPD_SC1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0)
+            last = __hip_atomic_fetch_add(args.ticket + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3u;
+#else   // (A/B builds) the release / acquire pair
         if (tid == 0)
             last = __hip_atomic_fetch_add(args.ticket + s, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 3u;
+#endif
         last = __shfl(last, 0, 64);
         if (!last) return;
         if (tid == 0) __hip_atomic_store(args.ticket + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
