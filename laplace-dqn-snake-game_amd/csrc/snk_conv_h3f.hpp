@@ -58,9 +58,11 @@ constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 #ifndef H3F_DIRECT
 #define H3F_DIRECT 0
 #endif
-// persistent conv_h3f_kernel launches (H3FArgs::ticket) for the act forward
+// persistent conv_h3f_kernel launches (H3FArgs::ticket) for the act forward: +0.3-0.6 % on the
+// headline loop in three interleaved A/B rounds (profiles/r05o_h3f_ab.txt); 0 = one workgroup
+// per group of four samples (measurement builds)
 #ifndef H3F_PERSIST
-#define H3F_PERSIST 0
+#define H3F_PERSIST 1
 #endif
 static_assert(H3F_LA >= 4 && H3F_LA <= 7, "lookahead: 4..7 (buffer 7 holds conv1's boards in the prologue)");
 
@@ -217,7 +219,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
     constexpr int NX = NSG * CF * NPB, LB = (NX + 511) / 512;
     int bv[LB];                // this thread's board cells of the group ([sample][channel][bordered cell])
     bool have_boards = false;  // bv holds the group's cells already (persistent passes after the first)
-    const int8_t *cbase[CF];   // persistent, env frame ring: plane(s, c) = cbase[c] + s * pitch
+    const int8_t *cbase0 = nullptr, *cbase1 = nullptr;   // persistent, env frame ring: plane(s, c) = cbase_c + s * pitch
     __shared__ int s_next;     // persistent: the group this workgroup runs next
 #if H3F_PERSIST
     for (;;) {
@@ -377,8 +379,11 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
             }
             // the ring's slot of each channel is the launch's (one step counter): the first
             // group's sample-0 planes give every later group's
-#pragma unroll
-            for (int c = 0; c < C; ++c) cbase[c] = persist ? pbase[c] - (int64_t)s0 * a.src.pitch : nullptr;
+            // (two scalars, not an array: a selected array element went to scratch)
+            if (persist) {
+                cbase0 = pbase[0] - (int64_t)s0 * a.src.pitch;
+                cbase1 = pbase[C - 1] - (int64_t)s0 * a.src.pitch;
+            }
         }
 #pragma unroll
         for (int u = 0; u < LB; ++u) {
@@ -634,7 +639,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
             const int sr = sc / CF, c = sc - sr * CF;
             const int cell = (bi - 1) + (bj - 1) * hin;
             const bool in = q < NX && sr < ns1 && bi >= 1 && bi <= hin && bj >= 1 && bj <= hin;
-            const int8_t *cb = (CF > 1 && c) ? cbase[CF - 1] : cbase[0];
+            const int8_t *cb = (CF > 1 && c) ? cbase1 : cbase0;
             bv[u] = in ? (int)((gi8 *)(cb + (int64_t)(s1 + sr) * a.src.pitch))[cell] : 0;
         }
     };
