@@ -120,6 +120,8 @@ def parse():
     p.add_argument("--no-configs3", action="store_true", help="skip the configs[3] per-rank shard line")
     p.add_argument("--d-samples", type=int, default=0, help="Jacobian Gram rows (0 = the whole replay buffer)")
     p.add_argument("--d-snapshots", type=int, default=1000, help="K of the snapshot D (compute_D.jl:51)")
+    p.add_argument("--arith", action="append", default=[], metavar="NAME=0|1",
+                   help="A/B measurement: a non-default snk.set_arith knob (repeatable); the line's config records it")
     a = p.parse_args()
     if a.n_envs <= 0:
         a.n_envs = CONFIGS3_ENVS_PER_GPU if a.workload == "configs3" else 4096
@@ -536,6 +538,11 @@ def main():
     from snake_amd import _lib
     lib = snk.load()
     _lib.call("snk_set_device", local)
+    arith_set = {}
+    for kv in args.arith:
+        k, v = kv.split("=")
+        snk.set_arith(k, bool(int(v)))
+        arith_set[k] = int(v)
 
     n, bs, C = args.n_envs, args.board_size, args.n_frames
     tr = snk.Trainer(n_envs=n, board_size=bs, n_frames=C, capacity=args.capacity, batch_size=64,
@@ -615,7 +622,8 @@ def main():
                    "hipgraph": graph,
                    "gemm_arithmetic": ("act-forward conv2 + conv3: f32 operands as fp16 hi/lo parts of power-of-two-scaled "
                                        "values, 3 f16 MFMA products; other GEMMs: 3-way bf16 split, 6 bf16 MFMA "
-                                       "products; f32 accumulation throughout")},
+                                       "products; f32 accumulation throughout"),
+                   **({"arith_ab": arith_set} if arith_set else {})},
         "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
                         "food_faults": faults},
         "roofline": None,
