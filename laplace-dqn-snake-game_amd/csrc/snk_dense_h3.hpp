@@ -19,17 +19,8 @@
 // template constant and the position loop unrolled: straight-line code keeps the compiler's
 // vmcnt waits on the A registers exact (a loop back edge merged them to waits on the newest
 // loads, which also count the DMAs).
-//
-// HEAD (the act forward): the act head (head_kernel<HEAD_ACT>) runs in the kernel's tail. The
-// slabs go out as sc1 stores; after every wave's stores completed, one lane per workgroup counts
-// on a relaxed agent-scope ticket per 128-row block, and the last of the block's gridDim.y
-// workgroups (told by the value its add returned) reads the block's slabs with sc1 loads and
-// runs the heads of its 128 samples, four threads per sample (no fences: see
-// upd_fwd_kernel's phase 5). The head's arithmetic is head_kernel's to the bit: h = bias +
-// slabs in slab order, relu, and Dense2's sums in wave_sum's butterfly order (below).
 #pragma once
 #include "snk_conv_h3.hpp"
-#include "snk_qnet.hpp"
 
 namespace snk {
 
@@ -40,94 +31,11 @@ struct DenseH3Args {
     const int *w1e;        // [nkk][64]
     float *slab;           // [nkk / KPZ][S][64]
     int S, nkk;
-    // HEAD: the fused act head (head_kernel<HEAD_ACT>'s operands), ticket[S / 128] zero between launches
-    uint32_t *ticket = nullptr;
-    const float *theta = nullptr;
-    QLayout L{};
-    float *h1 = nullptr, *q = nullptr;
-    HeadArgs ha{};
 };
-
-// The act head of sample s from its Dense1 slabs, thread t = 0..3 of the sample's quad (adjacent
-// lanes): the thread owns outputs o = 4t + i + 16m (i, m = 0..3; f32x4 loads of each slab row).
-// Dense2's sum sum_o w2[a][o] h[o] in wave_sum's order (xor butterfly 32, 16, 8, 4, 2, 1 over
-// o): the 32 and 16 steps pair outputs the thread owns, 8 and 4 pair thread t with t ^ 2 and
-// t ^ 1 (DPP quad permutes; both partners compute the same commutative sums), 2 and 1 are
-// local again. Slab loads sc1 (the fused tail's hand-off).
-__device__ __forceinline__ float quad_xchg(float v, int ctrl_xor) {
-    const int o = ctrl_xor == 1 ? __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xf, 0xf, false)
-                                : __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xf, 0xf, false);
-    return __builtin_bit_cast(float, o);
-}
-__device__ __forceinline__ void act_head_quad(const float *slab, int ks, int64_t S, const float *theta, const QLayout &L,
-                                              float *h1o, float *qo, const HeadArgs &ha, int64_t s, int t, bool valid) {
-    constexpr int KMAX = 8;
-    const int64_t sl = valid ? s : 0;
-    f32x4 z[KMAX][4];
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k)
-        if (k < ks)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {   // two 8-byte sc1 loads (16-byte atomics are not lock-free)
-                const uint64_t *p = reinterpret_cast<const uint64_t *>(slab + ((int64_t)k * S + sl) * 64 + 16 * m + 4 * t);
-                const uint64_t lo = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t hi = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                z[k][m] = f32x4{__builtin_bit_cast(float, (uint32_t)lo), __builtin_bit_cast(float, (uint32_t)(lo >> 32)),
-                                __builtin_bit_cast(float, (uint32_t)hi), __builtin_bit_cast(float, (uint32_t)(hi >> 32))};
-            }
-    f32x4 h[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        h[m] = *reinterpret_cast<const f32x4 *>(theta + L.off_d1b + 16 * m + 4 * t);
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k)
-            if (k < ks) h[m] += z[k][m];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) h[m][i] = h[m][i] > 0.0f ? h[m][i] : 0.0f;
-    }
-    float q[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        float v[4];   // a2[4t + i] = (p[o] + p[o + 32]) + (p[o + 16] + p[o + 48]), o = 4t + i
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float p[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) p[m] = theta[L.off_d2w + a * 64 + 16 * m + 4 * t + i] * h[m][i];
-            v[i] = (p[0] + p[2]) + (p[1] + p[3]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] + quad_xchg(v[i], 2);   // o ^ 8: thread t ^ 2
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] + quad_xchg(v[i], 1);   // o ^ 4: thread t ^ 1
-        const float r = (v[0] + v[2]) + (v[1] + v[3]);                      // o ^ 2, o ^ 1
-        q[a] = theta[L.off_d2b + a] + r;
-    }
-    if (!valid) return;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) *reinterpret_cast<f32x4 *>(h1o + s * 64 + 16 * m + 4 * t) = h[m];
-    if (t != 0) return;
-    qo[s * 3 + 0] = q[0];
-    qo[s * 3 + 1] = q[1];
-    qo[s * 3 + 2] = q[2];
-    // head_kernel<HEAD_ACT> (utils.jl:161-169)
-    const uint64_t tt = *ha.tptr;
-    const float eps = ha.eps_dev ? *ha.eps_dev : ha.epsilon;
-    const float u = rng_uniform(rng_hash(ha.seed, (uint64_t)s, tt));
-    int act;
-    if (u < eps) {
-        act = (int)((rng_hash(ha.seed ^ 0xA5A5A5A5A5A5A5A5ULL, (uint64_t)s, tt) >> 32) % 3);
-    } else {
-        act = 0;   // argmax: first maximum
-        if (q[1] > q[act]) act = 1;
-        if (q[2] > q[act]) act = 2;
-    }
-    ha.act[s] = (uint8_t)act;
-}
 constexpr int DH3_RING = 4, DH3_SLOT = 2 * 64 * 64 * 2;   // bytes per slot: both planes of one position
 constexpr int DH3_NT = 512;                                  // 8 waves x 16 rows
 
-template <int KPZ, bool HEAD = false>   // positions per slab; the launch guarantees nkk % KPZ == 0
+template <int KPZ>   // positions per slab; the launch guarantees nkk % KPZ == 0
 __global__ __launch_bounds__(DH3_NT) void dense_h3_kernel(DenseH3Args a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t dh3_lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -237,26 +145,7 @@ __global__ __launch_bounds__(DH3_NT) void dense_h3_kernel(DenseH3Args a) {
         if (row >= a.S) continue;
         const int ex = h3_exp(cm[e]);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-            float *o = out + (int64_t)row * 64 + ct * 16 + r;
-            const float v = __builtin_ldexpf(acc[ct][e], -ex);
-            if constexpr (HEAD) __hip_atomic_store(o, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
-            else *o = v;
-        }
-    }
-    if constexpr (HEAD) {
-        __shared__ int s_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab stores completed
-        __syncthreads();                                    // ... and every other wave's
-        if (tid == 0) {
-            const uint32_t old = __hip_atomic_fetch_add(a.ticket + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = old == gridDim.y - 1;
-            if (s_last) __hip_atomic_store(a.ticket + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (!s_last) return;
-        const int64_t sm = (int64_t)blockIdx.x * 128 + (tid >> 2);
-        act_head_quad(a.slab, (int)gridDim.y, a.S, a.theta, a.L, a.h1, a.q, a.ha, sm, tid & 3, sm < a.S);
+        for (int ct = 0; ct < 4; ++ct) out[(int64_t)row * 64 + ct * 16 + r] = __builtin_ldexpf(acc[ct][e], -ex);
     }
 }
 

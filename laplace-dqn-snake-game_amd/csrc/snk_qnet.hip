@@ -799,7 +799,7 @@ void qwork_free(QWork &w) {
     for (void *p : {(void *)w.a1, (void *)w.a2, (void *)w.a2b, (void *)w.a1b, (void *)w.a3, (void *)w.slab, (void *)w.cslab,
                     (void *)w.h1, (void *)w.q,
                     (void *)w.dq, (void *)w.dz1, (void *)w.dz3, (void *)w.dz2, (void *)w.dzc1, (void *)w.x0, (void *)w.target,
-                    (void *)w.loss, (void *)w.upd_ticket, (void *)w.h3f_ticket, (void *)w.dh3_ticket, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e,
+                    (void *)w.loss, (void *)w.upd_ticket, (void *)w.h3f_ticket, (void *)w.wmax_part, (void *)w.w3h, (void *)w.w3e,
                     (void *)w.w2h, (void *)w.w1h, (void *)w.w1e, (void *)w.a3max})
         dfree(p);
     w = QWork{};
@@ -866,8 +866,6 @@ void qwork_ensure(QWork &w, const QLayout &L, int64_t S, bool train) {
     w.a3max = dalloc<float>((size_t)cap);
     w.h3f_ticket = dalloc<uint32_t>(1);
     SNK_HIP(hipMemsetAsync(w.h3f_ticket, 0, 4, stream()));
-    w.dh3_ticket = dalloc<uint32_t>((size_t)ceil_div(cap, 128));
-    SNK_HIP(hipMemsetAsync(w.dh3_ticket, 0, (size_t)ceil_div(cap, 128) * 4, stream()));
     SNK_HIP(hipMemsetAsync(w.w2h, 0, (size_t)H3F_B2_CHUNKS * 16, stream()));   // pads stay zero
     if (tr) {
         w.has_train = 1;
@@ -939,16 +937,8 @@ static bool dh3_ok(const QLayout &L, int ks, int kpz) {
 static void dh3_launch(const DenseH3Args &a, int ks, int kpz, hipStream_t s) {
     SNK_CHECK(kpz == 7 && ks * kpz == a.nkk && a.S > 0, SNK_ERR_INTERNAL, "dense_h3: slab split");
     constexpr size_t lds = (size_t)DH3_RING * DH3_SLOT;
-    const dim3 grid((unsigned)ceil_div(a.S, 128), (unsigned)ks);
-    if (a.ticket) {   // the act head fused into the tail
-        SNK_CHECK(ks <= 8 && a.theta && a.h1 && a.q && a.ha.act && a.ha.tptr && !a.ha.rider.out, SNK_ERR_INTERNAL,
-                  "dense_h3: fused act head");
-        set_lds_limit((const void *)dense_h3_kernel<7, true>, lds);
-        dense_h3_kernel<7, true><<<grid, DH3_NT, lds, s>>>(a);
-    } else {
-        set_lds_limit((const void *)dense_h3_kernel<7>, lds);
-        dense_h3_kernel<7><<<grid, DH3_NT, lds, s>>>(a);
-    }
+    set_lds_limit((const void *)dense_h3_kernel<7>, lds);
+    dense_h3_kernel<7><<<dim3((unsigned)ceil_div(a.S, 128), (unsigned)ks), DH3_NT, lds, s>>>(a);
     launch_check("dense_h3_kernel");
 }
 template <int HIN>
@@ -1007,10 +997,8 @@ bool qnet_fused23(const QLayout &L, const float *th, const float *wt, const uint
     return h3s_ok(L, &net, 1, S) && h3c2_on() && !w.has_train;
 }
 
-// act_head (one net, full forward to Dense1): run the act head in dense_h3_kernel's tail when
-// Dense1 takes that kernel; returns whether it did (the caller then skips qnet_head)
-static bool forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi,
-                           const SampleRider *rider = nullptr, const HeadArgs *act_head = nullptr) {
+static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t S, hipStream_t s, int lo, int hi,
+                           const SampleRider *rider = nullptr) {
     const int lo0 = lo;   // lo as called (the fused act forward advances lo past conv3)
     const int bs = L.bs, nc = L.ncell;
     bool fresh_in[2] = {false, false};   // QWork::wmax_fresh holds for this forward only
@@ -1159,21 +1147,12 @@ static bool forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
     if (lo <= 3 && hi >= 3 && dh3) {   // Dense1 on the h3 split, the same slab layout
         int kc;
         const int ks = d1_split(L, S, kc);
-        const bool fuse = act_head && ng == 1 && !act_head->rider.out && ks <= 8 && arith(SNK_ARITH_ACT_HEAD);
         for (int g = 0; g < ng; ++g) {
             const FwdNet &n = net[g];
-            DenseH3Args da{n.w->a3, n.w->a3max, n.w->w1h, n.w->w1e, n.w->slab, (int)S, L.Wo * L.Wo};
-            if (fuse) {
-                da.ticket = n.w->dh3_ticket;
-                da.theta = n.th;
-                da.L = L;
-                da.h1 = n.w->h1;
-                da.q = n.w->q;
-                da.ha = *act_head;
-            }
+            const DenseH3Args da{n.w->a3, n.w->a3max, n.w->w1h, n.w->w1e, n.w->slab, (int)S, L.Wo * L.Wo};
             dh3_launch(da, ks, kc, s);
         }
-        return fuse;
+        return;
     }
     if (lo <= 3 && hi >= 3) {   // Dense1 (split over the Wo^2 positions into partial slabs; bias + relu in the head)
         int kc;
@@ -1190,7 +1169,6 @@ static bool forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
         }
         conv_launch<64, 64, 0, 0, MODE_DENSE, EPI_SLAB>(ga, ng, ks, s, wb);
     }
-    return false;
 }
 
 void qnet_forward(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, int64_t S, QWork &w,
@@ -1198,14 +1176,13 @@ void qnet_forward(const QLayout &L, const float *th, const float *wt, const Boar
                   const SampleRider *rider) {
     const FwdNet net{th, wt, wtb, src, &w};
     SNK_CHECK(!rider || (only < 0 && rider->batch <= 64), SNK_ERR_INTERNAL, "sample rider: full forward, batch <= 64");
-    bool head_done = false;
     if (only < 0)
-        head_done = forward_layers(L, &net, 1, S, s, 0, 3, rider, mode == HEAD_ACT ? &ha : nullptr);
+        forward_layers(L, &net, 1, S, s, 0, 3, rider);
     else if (only == QNET_ONLY_CONV23)
         forward_layers(L, &net, 1, S, s, 1, 2);
     else if (only < 4)
         forward_layers(L, &net, 1, S, s, only, only);
-    if ((only >= 0 && only != 4) || head_done) return;
+    if (only >= 0 && only != 4) return;
     qnet_head(L, th, S, w, mode, ha, s);
 }
 

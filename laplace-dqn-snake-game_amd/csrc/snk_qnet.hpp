@@ -81,7 +81,6 @@ struct QWork {
     int dh3_ready = 0;               // a3, a3max, w1h / w1e are those of the last conv_h3f + w3_split forward
                                      //   (a Dense1-only call, e.g. the per-layer timing, may then use dense_h3)
     double *target = nullptr, *loss = nullptr;
-    uint32_t *dh3_ticket = nullptr;  // dense_h3_kernel's fused act head: arrivals per 128-row block
     uint32_t *h3f_ticket = nullptr;  // persistent conv_h3f_kernel's group counter (zero between launches)
     uint32_t *upd_ticket = nullptr;  // training: per-sample arrivals of the update forward's four workgroups
                                      //   (upd_fwd_kernel phase 5), 0 between launches

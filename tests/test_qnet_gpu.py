@@ -425,33 +425,3 @@ def test_dense_h3_act_forward(snk):
     for q in (qh, qx):
         err = np.abs(q[sel] - qref) / np.maximum(1.0, np.abs(qref))
         assert err.max() <= 1e-5, float(err.max())
-
-
-def test_fused_act_head_bitexact(snk):
-    """The act head in dense_h3_kernel's tail (the 4096-state act forward: sc1 slab hand-off,
-    four threads per sample, Dense2 in wave_sum's butterfly order) against head_kernel<HEAD_ACT>
-    (snk.arith(act_head=False)): Q-values and actions bit-identical, greedy and at epsilon 0.3."""
-    from snake_amd import _lib
-    bs, C, n = 12, 2, 4096
-    g = snk.SnakeGame(bs, C, n_envs=n, autoreset=True)
-    m = snk.DQNModel(bs, 3, n_frames=C, seed=31)
-    act = snk.DeviceArray(n, np.uint8)
-    for _ in range(6):
-        snk.synth_actions_dev(g, 13, act)
-        snk.step_indices_dev(g, act.ptr)
-    out = {}
-    for fused in (True, False):
-        res = []
-        with snk.arith(act_head=fused):
-            for eps, seed in ((0.0, 0), (0.3, 9)):
-                a = np.array(snk.epsilon_greedy(g, m, eps, seed=seed))
-                q = np.zeros((n, 3), np.float32)
-                _lib.call("snk_dqn_last_q", m.handle, q.ctypes.data_as(_lib.vp), n)
-                res.append((a, q))
-        out[fused] = res
-    for (af, qf), (au, qu) in zip(out[True], out[False]):
-        assert np.array_equal(qf, qu), float(np.abs(qf - qu).max())
-        assert np.array_equal(af, au)
-    a0, q0 = out[True][0]
-    assert np.array_equal(a0, q0.argmax(1))
-    assert (out[True][1][0] != a0).sum() > 0.05 * n
