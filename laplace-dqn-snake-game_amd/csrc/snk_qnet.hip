@@ -1291,7 +1291,7 @@ int qnet_forward_update_pair(const QLayout &L, const FwdNet *net, int64_t S, hip
                                  w.a3, train ? w.x0 : nullptr, w.slab};
             a.hn[g] = HeadNet{w.slab, net[g].th, w.h1, w.q};
         }
-        a.head = a.d1 && head && net[1].w->upd_ticket && net[1].w->cap >= S;
+        a.head = a.d1 && head && net[1].w->upd_ticket && net[1].w->cap >= S && arith(SNK_ARITH_UPD_HEAD);
         if (a.head) {
             a.ha = *head;
             a.ticket = net[1].w->upd_ticket;

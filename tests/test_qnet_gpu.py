@@ -425,3 +425,22 @@ def test_dense_h3_act_forward(snk):
     for q in (qh, qx):
         err = np.abs(q[sel] - qref) / np.maximum(1.0, np.abs(qref))
         assert err.max() <= 1e-5, float(err.max())
+
+
+@pytest.mark.parametrize("B", [64, 37])
+def test_update_heads_fused_bitexact(snk, B):
+    """The update's two heads (t_net TD target, q_net Huber loss / dq / dz1) in upd_fwd_kernel's
+    tail (sc1 slab hand-off, per-sample ticket) against head_pair_kernel
+    (snk.arith(upd_head=False)): loss and gradient bit-identical."""
+    g, rb = _random_replay(snk, 12, 2)
+    m = snk.DQNModel(12, 3, n_frames=2, seed=21)
+    rng = np.random.default_rng(1)
+    m.set_params(m.get_params() + rng.standard_normal(m.P).astype(np.float32) * 0.01, snk.SNK_NET_TARGET)
+    idx, _ = snk.sample(rb, seed=4)
+    res = {}
+    for fused in (True, False):
+        with snk.arith(upd_head=fused):
+            loss = m.loss_grad(rb, idx, B)
+            res[fused] = (loss, m.grad.copy())
+    assert res[True][0] == res[False][0]
+    assert np.array_equal(res[True][1], res[False][1])
