@@ -54,6 +54,14 @@ constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 #ifndef H3F_LA
 #define H3F_LA 4
 #endif
+// measurement builds (-DSNK_H3F_VAR=n with SNK_ENV_CLOCKS, phase clocks): the conv3 offset
+// loop without its LDS-DMA (1), its barriers (2), its MFMAs (3) or its fragment reads (4)
+#ifndef SNK_H3F_VAR
+#define SNK_H3F_VAR 0
+#endif
+#if SNK_H3F_VAR && !defined(SNK_ENV_CLOCKS)
+#error "SNK_H3F_VAR: measurement (clocks) builds only"
+#endif
 // conv3's output stored from the accumulators instead of through LDS
 #ifndef H3F_DIRECT
 #define H3F_DIRECT 0
@@ -707,6 +715,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
                 // step, so a barrier, lies between for LA <= 7); after odd offsets: everything
                 // but the newest LA - 3 DMAs landed (offsets <= kk + 3, read at steps <= kk + 2),
                 // the barrier publishes them
+#if SNK_H3F_VAR == 0
                 dma(kk + H3F_LA);
                 frag_read(kk + 1, nxt);
                 mfma_block(cur);
@@ -715,6 +724,28 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
                     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
                     __builtin_amdgcn_s_barrier();
                 }
+#else   // measurement builds only (wrong results by design): one part of the step left out
+                if (SNK_H3F_VAR != 1) dma(kk + H3F_LA);
+                if (SNK_H3F_VAR != 4) {
+                    frag_read(kk + 1, nxt);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < NT; ++k) asm volatile("" : "+v"(nxt.a[k][0]), "+v"(nxt.a[k][1]));
+                    asm volatile("" : "+v"(nxt.b[0][0]), "+v"(nxt.b[0][1]), "+v"(nxt.b[1][0]), "+v"(nxt.b[1][1]));
+                }
+                if (SNK_H3F_VAR != 3) {
+                    mfma_block(cur);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < NT; ++k) asm volatile("" :: "v"(cur.a[k][0]), "v"(cur.a[k][1]));
+                    asm volatile("" :: "v"(cur.b[0][0]), "v"(cur.b[0][1]), "v"(cur.b[1][0]), "v"(cur.b[1][1]));
+                }
+                if (kk & 1) {
+                    __builtin_amdgcn_s_waitcnt(waitcnt_vm(H3F_LA - 3));
+                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                    if (SNK_H3F_VAR != 2) __builtin_amdgcn_s_barrier();
+                }
+#endif
             } else if (NBUF == 2) {
                 b_load(kk + 3, set ^ 1);
                 frag_read(kk + 1, nxt);
