@@ -62,10 +62,6 @@ constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 #if SNK_H3F_VAR && !defined(SNK_ENV_CLOCKS)
 #error "SNK_H3F_VAR: measurement (clocks) builds only"
 #endif
-// conv3's row tiles balanced over the SIMDs (the partial last tile split by column tiles)
-#ifndef H3F_BAL
-#define H3F_BAL 0
-#endif
 // conv3's output stored from the accumulators instead of through LDS
 #ifndef H3F_DIRECT
 #define H3F_DIRECT 0
@@ -629,14 +625,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
 
     constexpr int T = (NSG * ho2 + 15) / 16;
     const int rg = wave >> 1, cg = wave & 1;
-    // H3F_BAL: the full row tiles (TF) round-robin over the row groups, and the partial last tile
-    // (4 rows when 4 ho^2 % 16 = 4: 196 rows at 12x12) split by 16-column tiles over the waves
-    // of row groups 0 and 1 (column tile cg * 2 + rg of it): 13 tile products per SIMD instead
-    // of 14 / 14 / 12 / 12 (the waves of row group 0 carried the whole partial tile)
-    constexpr int TF = H3F_BAL ? NSG * ho2 / 16 : T;
-    constexpr bool PRT = H3F_BAL && (NSG * ho2) % 16 != 0;
-    const bool hp = PRT && rg < 2;
-    const int nt = __builtin_amdgcn_readfirstlane(TF > rg ? (TF - rg + 3) / 4 : 0);
+    const int nt = __builtin_amdgcn_readfirstlane(T > rg ? (T - rg + 3) / 4 : 0);
     const int bslot = (cg * 32 + r) * 4 + (g ^ ((4 - ((r >> 2) & 3)) & 3));
     if (persist && tid == 0) {   // (the ticket returned long ago: the DMA waits above are in order)
         s_next = nwg + (int)tk;
@@ -674,14 +663,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
             const int j = p / ho, i = p - j * ho;
             abase[k] = sr * XS + g * GG + j * XW + i;
         }
-        f32x4v acc[NT][2], accp = {0.f, 0.f, 0.f, 0.f};
-        int abp = 0;   // the partial tile (hp)
-        {
-            const int q = 16 * TF + r;
-            const int p = min(q >> 2, ho2 - 1), sr = q & 3;
-            const int j = p / ho, i = p - j * ho;
-            abp = sr * XS + g * GG + j * XW + i;
-        }
+        f32x4v acc[NT][2];
 #pragma unroll
         for (int k = 0; k < NT; ++k)
 #pragma unroll
@@ -690,7 +672,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
         // compiler re-loaded and waited on them per row tile: three serial round trips)
         const float bv2[2] = {a.b3[cg * 32 + r], a.b3[cg * 32 + 16 + r]};
         struct Frag {
-            u32x4 a[NT][2], b[2][2], p[2];
+            u32x4 a[NT][2], b[2][2];
         };
         auto frag_read = [&](int kk, Frag &f) {
             kk = min(kk, NKK - 1);
@@ -707,10 +689,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
 #pragma unroll
                 for (int pl = 0; pl < 2; ++pl) f.a[k][pl] = pa[pl * PL];
             }
-            if (hp) {
-#pragma unroll
-                for (int pl = 0; pl < 2; ++pl) f.p[pl] = As[abp + off + pl * PL];
-            }
         };
         auto mfma_block = [&](const Frag &f) {
 #pragma unroll
@@ -725,17 +703,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
                     c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
                     acc[k][ct] = c;
                 }
-            }
-            if (hp) {   // the partial tile's column tile rg of this wave's two (uniform branches)
-                const f16x8 ah = as_h(f.p[0]), al = as_h(f.p[1]);
-                auto part = [&](const u32x4 (&b)[2]) __attribute__((always_inline)) {
-                    const f16x8 bh = as_h(b[0]), bl = as_h(b[1]);
-                    accp = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, accp, 0, 0, 0);
-                    accp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, accp, 0, 0, 0);
-                    accp = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, accp, 0, 0, 0);
-                };
-                if (rg == 0) part(f.b[0]);
-                else part(f.b[1]);
             }
         };
         // NBUF 2: B(kk+3) -> registers, B(kk+2) -> LDS buffer kk & 1, barrier every offset.
@@ -835,21 +802,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
 #endif
                     vm[e] = fmaxf(vm[e], rv);
                 }
-            }
-        }
-        if (hp && 4 * TF + g < ho2) {   // the partial tile: column tile rg of this wave's pair
-            const int p = 4 * TF + g, col = cg * 32 + rg * 16 + r;
-            const float bv = rg == 0 ? bv2[0] : bv2[1];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float v = __builtin_ldexpf(accp[e], -(ea[e] + ew)) + bv;
-                const float rv = v > 0.0f ? v : 0.0f;
-#if H3F_DIRECT
-                if (e < ns) a.out[((int64_t)(s0 + e) * ho2 + p) * CN + col] = rv;
-#else
-                Cs[(e * ho2 + p) * CS + col] = rv;
-#endif
-                vm[e] = fmaxf(vm[e], rv);
             }
         }
         // per-sample maxima for Dense1's h3 scale: DPP within each 16-lane row (no readlane
