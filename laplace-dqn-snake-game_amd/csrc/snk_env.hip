@@ -129,16 +129,91 @@ __device__ __forceinline__ uint32_t pack16(const i32x4 v) {
     return out;
 }
 
+// The act head of env e (head_kernel<HEAD_ACT>'s arithmetic to the bit), thread t = 0..3 of
+// the env's quad of adjacent lanes: the thread owns Dense1 outputs o = 4t + i + 16m (i, m =
+// 0..3; float4 loads of each slab row); h = bias + slabs in slab order, relu; Dense2's sum in
+// wave_sum's butterfly order over o (xor 32, 16, 8, 4, 2, 1): 32 and 16 pair outputs the thread
+// owns, 8 and 4 pair thread t with t ^ 2 and t ^ 1 (DPP quad permutes; both partners form the
+// same commutative sums), 2 and 1 are local again. Writes h1, q, the action (act_out and the
+// workgroup's LDS slot).
+typedef float envf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float quad_xor(float v, int x) {
+    const int o = x == 1 ? __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xf, 0xf, false)    // [1,0,3,2]
+                         : __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xf, 0xf, false);   // [2,3,0,1]
+    return __builtin_bit_cast(float, o);
+}
+__device__ __forceinline__ void env_act_head(const EnvActHead &H, int64_t n, int64_t e, int t, bool valid, int64_t step,
+                                             uint8_t *s_slot) {
+    constexpr int KMAX = 8;
+    const int64_t es = valid ? e : 0;
+    envf4 z[KMAX][4];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+        if (k < H.ks)
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                z[k][m] = *reinterpret_cast<const envf4 *>(H.slab + ((int64_t)k * n + es) * 64 + 16 * m + 4 * t);
+    envf4 h[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        h[m] = *reinterpret_cast<const envf4 *>(H.b1 + 16 * m + 4 * t);
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k)
+            if (k < H.ks) h[m] += z[k][m];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[m][i] = h[m][i] > 0.0f ? h[m][i] : 0.0f;
+    }
+    float q[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        float v[4];   // (p[o] + p[o + 32]) + (p[o + 16] + p[o + 48]), o = 4t + i
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float p[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) p[m] = H.w2[a * 64 + 16 * m + 4 * t + i] * h[m][i];
+            v[i] = (p[0] + p[2]) + (p[1] + p[3]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] + quad_xor(v[i], 2);   // o ^ 8: thread t ^ 2
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] + quad_xor(v[i], 1);   // o ^ 4: thread t ^ 1
+        q[a] = H.b2[a] + ((v[0] + v[2]) + (v[1] + v[3]));                 // o ^ 2, o ^ 1
+    }
+    if (!valid) return;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) *reinterpret_cast<envf4 *>(H.h1 + e * 64 + 16 * m + 4 * t) = h[m];
+    if (t != 0) return;
+    H.q[e * 3 + 0] = q[0];
+    H.q[e * 3 + 1] = q[1];
+    H.q[e * 3 + 2] = q[2];
+    // utils.jl:161-169: Float32(rand()) < epsilon ? rand(av) : av[argmax(Q)] (head_kernel's draw)
+    const float eps = H.eps_dev ? *H.eps_dev : H.epsilon;
+    const float u = rng_uniform(rng_hash(H.seed, (uint64_t)e, (uint64_t)step));
+    int act;
+    if (u < eps) {
+        act = (int)((rng_hash(H.seed ^ 0xA5A5A5A5A5A5A5A5ULL, (uint64_t)e, (uint64_t)step) >> 32) % 3);
+    } else {
+        act = 0;   // argmax: first maximum
+        if (q[1] > q[act]) act = 1;
+        if (q[2] > q[act]) act = 2;
+    }
+    H.act_out[e] = (uint8_t)act;
+    *s_slot = (uint8_t)act;
+}
+
 // Boards stay in the registers of the thread that loaded them (NPT 16-byte pieces per
 // thread, 13 at 20x20); LDS holds only a 2-bit copy for the logic lanes (100 B per env at
 // 20x20), so LDS no longer caps the envs in flight: 2-wave workgroups, 5 per SIMD.
 template <int PITCH>
 constexpr int env_waves_per_simd() { return PITCH > 304 ? 4 : 5; }   // the register budget of NPT pieces
 
-template <int PITCH, int NE = ENV_NE>
-__global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_kernel(EnvDev E, const uint8_t *__restrict__ act,
-                                                             int act_mode, ReplayDev R, int store, EpisodeAcc acc,
-                                                             int with_acc) {
+// HEAD: the act head runs here first (EnvActHead; four threads per env: NE * 4 == ENV_NT);
+// the occupancy bound is dropped (these grids fill a quarter of the SIMDs at most)
+template <int PITCH, int NE = ENV_NE, bool HEAD = false>
+__global__ __launch_bounds__(ENV_NT, HEAD ? 1 : env_waves_per_simd<PITCH>()) void env_step_kernel(
+    EnvDev E, const uint8_t *__restrict__ act, int act_mode, ReplayDev R, int store, EpisodeAcc acc, int with_acc,
+    EnvActHead H) {
     constexpr int NCH = PITCH / 16, NPT = (NE * NCH + ENV_NT - 1) / ENV_NT;
     __shared__ uint32_t sbp[NE * NCH];                              // packed boards
     __shared__ __attribute__((aligned(8))) int16_t s_pc[NE * 4];   // patch cells (tail, head, food), -1 = none
@@ -146,6 +221,7 @@ __global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_
     __shared__ int16_t s_food[64];
     __shared__ float s_epr[NE];   // finished episodes: reward (NaN = not finished), score
     __shared__ uint8_t s_score[NE];
+    __shared__ uint8_t s_act[NE];   // HEAD: the actions
     ENV_CLK(0);
     const int tid = threadIdx.x;
     const bool w0 = tid < 64;
@@ -165,7 +241,7 @@ __global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_
     float epr0 = 0.0f;
     if (live) {
         st = E.state[e];
-        a = act[e];
+        if (!HEAD) a = act[e];
         epr0 = E.ep_reward[e];
         head_cell = (int)st.head_cell;
         tail_cell = (int)st.tail_cell;
@@ -185,6 +261,11 @@ __global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_
         const int idx = tid + k * ENV_NT;
         if (idx < ne * NCH) vcur[k] = *reinterpret_cast<const i32x4 *>(fcur + idx * 16);
     }
+    if constexpr (HEAD) {   // with the board loads in flight; the barrier below publishes s_act
+        static_assert(NE * 4 == ENV_NT, "four threads per env");
+        const int el = tid >> 2;
+        env_act_head(H, E.n, e0 + el, tid & 3, el < ne, t, s_act + el);
+    }
 #pragma clang loop unroll(full)
     for (int k = 0; k < NPT; ++k) {
         const int idx = tid + k * ENV_NT;
@@ -198,6 +279,7 @@ __global__ __launch_bounds__(ENV_NT, env_waves_per_simd<PITCH>()) void env_step_
     float epr_out = 0.0f;
     int score_out = 0;
     if (live) {
+        if (HEAD) a = s_act[lane];
         uint8_t flag = 0;
         int16_t pc[3] = {-1, -1, -1};
         const uint32_t *bp = sbp + lane * NCH;
@@ -513,8 +595,29 @@ __global__ void env_synth_kernel(EnvDev E, uint64_t seed, uint8_t *__restrict__ 
     act[e] = (uint8_t)((rng_hash(seed, (uint64_t)e, (uint64_t)E.ctl->t) >> 32) % 3);
 }
 
+template <int P>
+static void env_step_launch_p(bool small, bool head, int grid, hipStream_t s, const EnvDev &E, const uint8_t *act,
+                              int act_mode, const ReplayDev &r, int store, const EpisodeAcc &ea, int wa,
+                              const EnvActHead &H) {
+    if constexpr (P <= 256) {
+        if (small && head) {
+            env_step_kernel<P, ENV_NE_SMALL, true><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, store, ea, wa, H);
+            return;
+        }
+        if (small) {
+            env_step_kernel<P, ENV_NE_SMALL><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, store, ea, wa, H);
+            return;
+        }
+    }
+    env_step_kernel<P, ENV_NE><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, store, ea, wa, H);
+}
+
+bool env_act_head_ok(const EnvDev &E, int ks) {
+    return E.n <= ENV_NE_SMALL_MAX && E.pitch <= 256 && ks >= 1 && ks <= 8;
+}
+
 void env_launch_step(const EnvDev &E, const uint8_t *act, int act_mode, const ReplayDev *R, hipStream_t s,
-                     const EpisodeAcc *acc) {
+                     const EpisodeAcc *acc, const EnvActHead *head) {
     ReplayDev r{};
     if (R) r = *R;
     EpisodeAcc ea{};
@@ -523,14 +626,15 @@ void env_launch_step(const EnvDev &E, const uint8_t *act, int act_mode, const Re
     const bool small = E.n <= ENV_NE_SMALL_MAX && E.pitch <= 256;
     const int grid = (int)ceil_div(E.n, small ? ENV_NE_SMALL : ENV_NE);
     const int store = R ? 1 : 0;
-#define SNK_ENV_CASE(P)                                                                                      \
-    case P:                                                                                                  \
-        if (P <= 256 && small)                                                                               \
-            env_step_kernel<P, (P <= 256 ? ENV_NE_SMALL : ENV_NE)><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, \
-                                                                                      store, ea, wa);        \
-        else                                                                                                 \
-            env_step_kernel<P, ENV_NE><<<grid, ENV_NT, 0, s>>>(E, act, act_mode, r, store, ea, wa);        \
-        break;
+    EnvActHead H{};
+    if (head) {
+        SNK_CHECK(env_act_head_ok(E, head->ks) && act_mode == SNK_ACT_INDEX && head->act_out == act && head->slab &&
+                      head->b1 && head->w2 && head->b2 && head->h1 && head->q,
+                  SNK_ERR_INTERNAL, "env step: fused act head");
+        H = *head;
+    }
+#define SNK_ENV_CASE(P) \
+    case P: env_step_launch_p<P>(small, head != nullptr, grid, s, E, act, act_mode, r, store, ea, wa, H); break;
     switch (E.pitch) {
         SNK_ENV_CASE(48) SNK_ENV_CASE(64) SNK_ENV_CASE(96) SNK_ENV_CASE(112) SNK_ENV_CASE(128)
         SNK_ENV_CASE(144) SNK_ENV_CASE(176) SNK_ENV_CASE(208) SNK_ENV_CASE(240) SNK_ENV_CASE(256)

@@ -143,7 +143,21 @@ __device__ inline void sample_wave(const SampleRider &r) {
 // Launch helpers implemented in the .hip files. One launch is a whole lockstep
 // step: its last workgroup also advances ctl->t (and the replay count when
 // storing) and, with acc, folds the finished episodes into the trainer stats.
+// head (the trainer's act step, small lockstep batches): the act head of the act forward runs
+// in the step kernel (head_kernel<HEAD_ACT>'s arithmetic to the bit) and writes act itself
+struct EnvActHead {
+    const float *slab = nullptr;   // the act forward's Dense1 slabs [ks][n][64]
+    int ks = 0;
+    const float *b1 = nullptr, *w2 = nullptr, *b2 = nullptr;   // Dense1 bias, Dense2 weights [3][64], bias
+    float *h1 = nullptr, *q = nullptr;                        // outputs [n][64], [n][3]
+    uint8_t *act_out = nullptr;                               // the actions (the step's act argument)
+    uint64_t seed = 0;
+    const float *eps_dev = nullptr;
+    float epsilon = 0.0f;
+};
+// whether env_launch_step can run the act head for this env batch (and ks slabs)
+bool env_act_head_ok(const EnvDev &E, int ks);
 void env_launch_step(const EnvDev &E, const uint8_t *act, int act_mode, const ReplayDev *R,
-                     hipStream_t s, const EpisodeAcc *acc = nullptr);
+                     hipStream_t s, const EpisodeAcc *acc = nullptr, const EnvActHead *head = nullptr);
 
 }  // namespace snk

@@ -1186,6 +1186,19 @@ void qnet_forward(const QLayout &L, const float *th, const float *wt, const Boar
     qnet_head(L, th, S, w, mode, ha, s);
 }
 
+int qnet_forward_act_slabs(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, int64_t S,
+                           QWork &w, hipStream_t s, const uint16_t *wtb, const SampleRider *rider) {
+    const FwdNet net{th, wt, wtb, src, &w};
+    SNK_CHECK(!rider || rider->batch <= 64, SNK_ERR_INTERNAL, "sample rider: batch <= 64");
+    forward_layers(L, &net, 1, S, s, 0, 3, rider);
+    return qnet_act_slab_count(L, S);
+}
+
+int qnet_act_slab_count(const QLayout &L, int64_t S) {
+    int kc;
+    return d1_split(L, S, kc);
+}
+
 void qnet_forward_pair(const QLayout &L, const FwdNet *net, int64_t S, hipStream_t s) {
     forward_layers(L, net, 2, S, s, 0, 3);
 }

@@ -147,6 +147,12 @@ void qnet_head(const QLayout &L, const float *theta, int64_t S, QWork &w, HeadMo
                hipStream_t s);
 // only: -1 all layers + head; 0..3 one layer; 4 the head; QNET_ONLY_CONV23 conv2 and conv3
 constexpr int QNET_ONLY_CONV23 = 12;
+// the act forward up to Dense1's partial slabs (w.slab) without the head; returns the slab
+// count (the trainer runs the act head inside env_step_kernel)
+int qnet_forward_act_slabs(const QLayout &L, const float *th, const float *wt, const BoardSrc &src, int64_t S,
+                           QWork &w, hipStream_t s, const uint16_t *wtb, const SampleRider *rider);
+// the number of Dense1 slabs an act forward of S samples writes
+int qnet_act_slab_count(const QLayout &L, int64_t S);
 // whether an act forward of S samples runs conv2 + conv3 fused (conv_h3f_kernel)
 bool qnet_fused23(const QLayout &L, const float *theta, const float *wt, const uint16_t *wtb, int64_t S, QWork &w);
 // wtb (optional): bf16 split planes of the image -> conv2/conv3/Dense1 on the x6 kernels.

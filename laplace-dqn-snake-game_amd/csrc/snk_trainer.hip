@@ -122,22 +122,43 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     ha.tptr = &E.ctl->t;
     ha.eps_dev = &h->stats->epsilon;
     const float *qact = q->act.q;
-    if (q->deep)
+    // the act head inside env_step_kernel (small lockstep batches): the act forward stops at
+    // Dense1's slabs and the step computes each env's Q-values and action first (bit-identical
+    // to head_kernel<HEAD_ACT>; SNK_ARITH_ENV_HEAD = 0: the separate head launch)
+    const bool env_head = !q->deep && arith(SNK_ARITH_ENV_HEAD) && env_act_head_ok(E, qnet_act_slab_count(q->L, E.n));
+    EnvActHead eh;
+    if (q->deep) {
         qact = deep_forward(q, SNK_NET_Q, src_env(E), E.n, HEAD_ACT, ha, s);
-    else
+    } else if (env_head) {
+        eh.ks = qnet_forward_act_slabs(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, s, q->wtb_q,
+                                       ride ? &rider : nullptr);
+        eh.slab = q->act.slab;
+        eh.b1 = q->theta_q + q->L.off_d1b;
+        eh.w2 = q->theta_q + q->L.off_d2w;
+        eh.b2 = q->theta_q + q->L.off_d2b;
+        eh.h1 = q->act.h1;
+        eh.q = q->act.q;
+        eh.act_out = h->act;
+        eh.seed = ha.seed;
+        eh.eps_dev = ha.eps_dev;
+    } else {
         qnet_forward(q->L, q->theta_q, q->wt_q, src_env(E), E.n, q->act, HEAD_ACT, ha, s, -1, q->wtb_q,
                      ride ? &rider : nullptr);
+    }
     // step! + virtual_step + store! + the episode statistics, one launch
     const EpisodeAcc acc{&h->stats->episodes, &h->stats->score_sum, &h->stats->env_steps, &h->stats->reward_sum,
                          &h->stats->reward_max, &h->stats->score_max};
-    if (h->act_trace) {
+    auto trace = [&]() {
+        if (!h->act_trace) return;
         const int64_t slot = (int64_t)it % h->act_trace_slots;
         SNK_HIP(hipMemcpyAsync(h->act_trace + slot * E.n, h->act, (size_t)E.n, hipMemcpyDeviceToDevice, s));
         if (h->q_trace)
             SNK_HIP(hipMemcpyAsync(h->q_trace + slot * E.n * 3, qact, (size_t)E.n * 3 * sizeof(float),
                                    hipMemcpyDeviceToDevice, s));
-    }
-    env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s, &acc);
+    };
+    if (!env_head) trace();
+    env_launch_step(E, h->act, SNK_ACT_INDEX, &R, s, &acc, env_head ? &eh : nullptr);
+    if (env_head) trace();   // the actions and Q-values the step computed
     if (!upd) return;
     for (int u = 0; u < n_upd; ++u) {
         // update u > 0 of the non-deep net: drawn by update u-1's grad_update_kernel (PostUpdate::next)

@@ -444,3 +444,28 @@ def test_update_heads_fused_bitexact(snk, B):
             res[fused] = (loss, m.grad.copy())
     assert res[True][0] == res[False][0]
     assert np.array_equal(res[True][1], res[False][1])
+
+
+def test_env_fused_act_head_bitexact(snk):
+    """The trainer's act head inside env_step_kernel (4096 envs: the act forward stops at
+    Dense1's slabs; the step computes each env's Q-values and epsilon-greedy action first,
+    four threads per env, Dense2 in wave_sum's butterfly order) against head_kernel<HEAD_ACT>
+    (snk.arith(env_head=False)): 16 captured iterations with learning after the fill, every
+    iteration's actions and Q-values, the losses and both nets bit-identical."""
+    n, U = 4096, 8
+    res = {}
+    for fused in (True, False):
+        with snk.arith(env_head=fused):
+            tr = snk.Trainer(n_envs=n, board_size=12, n_frames=2, capacity=20_000, batch_size=64, n_batches=10_000,
+                             epsilon=0.3, epsilon_end=0.3, decay=0.0, seed=0xE4, graph_unroll=U)
+            snk.fill_buffer_(tr, graph=True)
+            acts = snk.DeviceArray((2 * U, n), np.uint8)
+            qs = snk.DeviceArray((2 * U, n, 3), np.float32)
+            tr.set_act_trace(acts, qs)
+            tr.run(2 * U, learn=True, graph=True)
+            res[fused] = (acts.numpy(), qs.numpy(), np.array(tr.losses), tr.model.get_params(),
+                          tr.model.get_params(snk.SNK_NET_TARGET))
+    for x, y in zip(res[True], res[False]):
+        assert np.array_equal(x, y)
+    a, q = res[True][0], res[True][1]
+    assert 0.1 < (a != q.argmax(2)).mean() < 0.4   # the epsilon draws took effect, greedy elsewhere
