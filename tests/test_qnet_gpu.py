@@ -468,4 +468,4 @@ def test_env_fused_act_head_bitexact(snk):
     for x, y in zip(res[True], res[False]):
         assert np.array_equal(x, y)
     a, q = res[True][0], res[True][1]
-    assert 0.1 < (a != q.argmax(2)).mean() < 0.4   # the epsilon draws took effect, greedy elsewhere
+    assert 0.05 < (a != q.argmax(2)).mean() < 0.3   # the epsilon draws took effect (0.3 x 2/3 at most)
