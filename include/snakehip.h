@@ -60,7 +60,8 @@ int snk_synchronize(void);
 #define SNK_ARITH_SYRK_H3_32 5   /* 1: Jacobian Gram on the round-2 32x32x16 kernel; 0: syrk_h3q */
 #define SNK_ARITH_UPD_HEAD 6     /* 1: the update's heads run in upd_fwd_kernel's tail; 0: head_pair_kernel (same bits) */
 #define SNK_ARITH_ENV_HEAD 7     /* 1: the trainer's act head runs in env_step_kernel; 0: head_kernel (same bits) */
-#define SNK_ARITH_COUNT 8
+#define SNK_ARITH_SPLIT_CHAIN 8  /* 1: the trainer's grad_update writes the next act forward's split weights; 0: w3_split every act */
+#define SNK_ARITH_COUNT 9
 int snk_set_arith(int32_t knob, int32_t value);
 int snk_get_arith(int32_t knob, int32_t *value_out);
 int snk_malloc(void **dev_out, int64_t bytes);

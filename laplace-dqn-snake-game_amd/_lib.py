@@ -228,12 +228,12 @@ def ptr(a: np.ndarray | None):
 
 
 # snk_set_arith knobs (include/snakehip.h SNK_ARITH_*): name -> knob
-ARITH = {"x6s": 0, "h3s": 1, "dh3": 2, "h3c2": 3, "conv_fp32": 4, "syrk_h3_32": 5, "upd_head": 6, "env_head": 7}
+ARITH = {"x6s": 0, "h3s": 1, "dh3": 2, "h3c2": 3, "conv_fp32": 4, "syrk_h3_32": 5, "upd_head": 6, "env_head": 7, "split_chain": 8}
 
 
 def set_arith(name: str, value: bool) -> bool:
     """Select a GEMM arithmetic path process-wide (SNK_ARITH_*); returns the previous
-    value. Production defaults: x6s, h3s, dh3, h3c2, upd_head, env_head on; conv_fp32, syrk_h3_32 off."""
+    value. Production defaults: x6s, h3s, dh3, h3c2, upd_head, env_head, split_chain on; conv_fp32, syrk_h3_32 off."""
     old = get_arith(name)
     call("snk_set_arith", ARITH[name], int(bool(value)))
     return old

@@ -89,6 +89,15 @@ static_assert(H3F_LA >= 4 && H3F_LA <= 7, "lookahead: 4..7 (buffer 7 holds conv1
 // fragment reads: distinct bank quads). A per-(position, output) scale factors out of the
 // position's partial sum, so each is scaled back on its own.
 constexpr int W3S_BLOCKS = 36 * 512 / 256, W2S_BLOCKS = (9 * 32 * 16 / 4 + 255) / 256;
+// The weight splits' exponents leave H3_W_HEADROOM bits of fp16 range above the maximum (scaled
+// maximum in [2^10, 2^11) instead of h3_exp's [2^14, 2^15)): the training loop's grad_update_kernel
+// re-splits the updated weights with the exponents of the last w3_split_kernel (a chained act
+// forward skips the split launch), which stays exact while no weight has grown 32-fold since;
+// the trainer runs w3_split_kernel again at the start of every captured graph. The cost is
+// nil: each element keeps its 22-bit h + l form, only values below 2^-14 of the maximum (whose l
+// part falls into the fp16 subnormals) carry an absolute error <= 2^-36 of the maximum
+constexpr int H3_W_HEADROOM = 4;
+__device__ __forceinline__ int h3_exp_w(float m) { return h3_exp(m) - H3_W_HEADROOM; }
 __host__ __device__ constexpr int w1s_blocks(int nkk) { return nkk * 64 * 16 / 256; }
 static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__restrict__ img, const float *__restrict__ wmax,
                                                        int nwmax, uint16_t *__restrict__ out, int *__restrict__ eout,
@@ -105,7 +114,7 @@ static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__res
         m = dpp_max<0x4E>(m);
         m = dpp_max<0x141>(m);
         m = dpp_max<0x140>(m);
-        const int ex = h3_exp(m);
+        const int ex = h3_exp_w(m);
         if (q4 == 0) e1[row] = ex;
         u32x2 hh, ll;
         h3_split4(v, ex, hh, ll);
@@ -127,7 +136,7 @@ static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__res
         m = wave_max(m);
         if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
         __syncthreads();
-        const int ew2 = h3_exp(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
+        const int ew2 = h3_exp_w(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
         if (blockIdx.x == W3S_BLOCKS && threadIdx.x == 0) eout[1] = ew2;
         if (e < NW4) {
             const int kk = e >> 7, co = (e >> 2) & 31, ci0 = 4 * (e & 3);
@@ -148,7 +157,7 @@ static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__res
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
     __syncthreads();
-    const int ew = h3_exp(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
+    const int ew = h3_exp_w(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
     if (blockIdx.x == 0 && threadIdx.x == 0) *eout = ew;
     const int bch = (tt >> 3) * 4 + ((tt & 7) >> 1), bhalf = tt & 1;
     u32x2 h, l;

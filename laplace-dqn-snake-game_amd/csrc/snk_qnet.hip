@@ -1002,9 +1002,12 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
     const int lo0 = lo;   // lo as called (the fused act forward advances lo past conv3)
     const int bs = L.bs, nc = L.ncell;
     bool fresh_in[2] = {false, false};   // QWork::wmax_fresh holds for this forward only
+    bool split_in[2] = {false, false};   // QWork::split_fresh likewise
     for (int g = 0; g < ng; ++g) {
         fresh_in[g] = net[g].w->wmax_fresh != 0;
         net[g].w->wmax_fresh = 0;
+        split_in[g] = net[g].w->split_fresh != 0;
+        net[g].w->split_fresh = 0;
     }
     const bool h3 = h3s_ok(L, net, ng, S);
     // h3 also for conv2 (conv_h3c2_kernel): conv1 then writes fp32 a1 only. SNK_H3C2=0: x6 conv2.
@@ -1044,7 +1047,9 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
                 rd = SampleRider{};
             }
             SNK_CHECK(!rd.out || (lo <= 2 && hi >= 1), SNK_ERR_INTERNAL, "sample rider without a launch");
-            if (lo <= 2 && hi >= 1 && h3f_dma(L.bs)) {   // the conv3 weights pre-split once for every workgroup
+            // the conv3 weights pre-split once for every workgroup, unless the grad_update that last
+            // changed them wrote the split (the trainer's chained iterations)
+            if (lo <= 2 && hi >= 1 && h3f_dma(L.bs) && !(split_in[g] && fresh)) {
                 const int nkk = L.Wo * L.Wo;
                 w3_split_kernel<<<W3S_BLOCKS + W2S_BLOCKS + (dh3prep ? w1s_blocks(nkk) : 0), 256, 0, s>>>(
                     img, w.wmax_part, w.wmax_n, w.w3h, w.w3e, n.wt + L.off_t2, w.w2h, dh3prep ? n.wt + L.off_td : nullptr,
@@ -1685,7 +1690,8 @@ __host__ __device__ inline int gu_blocks(int CK, int nkk) { return nkk * (CK / G
 static_assert(GU_WMAX_BLOCKS == 36 * (32 / GU_ROWS), "conv3 image blocks");
 
 // wmax: where this block's max |new theta| goes (the conv3 section, UpdateTarget::wmax_out)
-__device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb, bool due, float omr,
+// sec: 0 conv2, 1 conv3, 2 Dense1 (the split images of UpdateTarget::s_*)
+__device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int sec, int kk, int cb, bool due, float omr,
                                float *wmax = nullptr) {
     // rows of CN + 4 floats: the image pass below reads column n of rows c4 .. c4 + 3 with
     // lane groups spanning four c4 values, which a CN-float pitch put on one bank (4-way)
@@ -1758,6 +1764,31 @@ __device__ void gu_image_block(const UpdArgs &a, const GuSec &S, int kk, int cb,
         const f32x4 w4 = {v0, v1, v2, v3};
         *reinterpret_cast<f32x4 *>(a.u.wt + t) = w4;
         if (due) *reinterpret_cast<f32x4 *>(a.u.wt_t + t) = w4;
+        // the next act forward's split images (w3_split_kernel's layouts and exponents)
+        const int ci0 = cb * GU_ROWS + c4;
+        if (sec == 1 && a.u.s_w3h) {   // conv3: [kk][512 chunks], chunk (co, ci / 8), 8-byte half (ci / 4) & 1
+            const int bch = n * 4 + (ci0 >> 3), bhalf = (ci0 >> 2) & 1;
+            u32x2 h, l;
+            h3_split4(w4, a.u.s_w3e[0], h, l);
+            u32x2 *o = reinterpret_cast<u32x2 *>(a.u.s_w3h) + (int64_t)kk * 512 * 2;
+            o[x6s_bswz(bch) * 2 + bhalf] = h;
+            o[x6s_bswz(256 + bch) * 2 + bhalf] = l;
+        } else if (sec == 0 && a.u.s_w2h) {   // conv2: the B2 image, offset pair kk / 2
+            const int p = kk >> 1, k0 = 16 * (kk & 1) + ci0;
+            u32x2 h, l;
+            h3_split4(w4, a.u.s_w3e[1], h, l);
+            u32x2 *o2 = reinterpret_cast<u32x2 *>(a.u.s_w2h);
+            o2[(((p * 2 + 0) * 32 + n) * H3F_B2_BR + k0) / 4] = h;
+            o2[(((p * 2 + 1) * 32 + n) * H3F_B2_BR + k0) / 4] = l;
+        } else if (sec == 2 && a.u.s_w1h) {   // Dense1: row (kk, out n), its own exponent
+            const int q4 = ci0 >> 2;
+            u32x2 h, l;
+            h3_split4(w4, a.u.s_w1e[kk * 64 + n], h, l);
+            const int off = (n * 64 + (((q4 >> 1) ^ (n & 7)) << 3) + ((q4 & 1) << 2)) / 4;
+            u32x2 *o1 = reinterpret_cast<u32x2 *>(a.u.s_w1h + (int64_t)kk * 2 * 4096);
+            o1[off] = h;
+            o1[1024 + off] = l;
+        }
         if (a.u.wtb) {
             const int64_t x6 = 3 * S.base + (int64_t)kk * 3 * S.CK * CN + (int64_t)n * S.CK + cb * GU_ROWS + c4;
 #pragma unroll
@@ -1835,7 +1866,7 @@ __global__ __launch_bounds__(256) void grad_update_kernel(UpdArgs a) {
         const int bl = b - (sec == 0 ? 0 : sec == 1 ? nb2 : nb2 + nb3);
         const GuSec S = gu_sec(L, sec);
         const int per = S.CK / GU_ROWS;
-        gu_image_block(a, S, bl / per, bl % per, due, omr, sec == 1 && a.u.wmax_out ? a.u.wmax_out + bl : nullptr);
+        gu_image_block(a, S, sec, bl / per, bl % per, due, omr, sec == 1 && a.u.wmax_out ? a.u.wmax_out + bl : nullptr);
     } else {
         // conv1 [off_w1, off_w2), conv2 bias [off_b2, off_w3), conv3 bias [off_b3, off_d1w),
         // Dense1 bias [off_d1b, off_d2w): one index space over the four runs. These finish from

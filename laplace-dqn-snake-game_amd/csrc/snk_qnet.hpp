@@ -72,6 +72,9 @@ struct QWork {
     const float *wmax_img = nullptr; //   of this image
     int wmax_fresh = 0;              //   set by the trainer: the partials were written by the grad_update that
                                      //   last changed the image (the next full forward skips its scan; reset there)
+    int split_fresh = 0;             // set by the trainer: w3h / w2h / w1h were written by the grad_update that
+                                     //   last changed the image (UpdateTarget::s_*): the next act forward skips
+                                     //   w3_split_kernel (reset there)
     uint16_t *w3h = nullptr;         // h3 conv3 weights pre-split for conv_h3f_kernel's LDS-DMA staging:
     int *w3e = nullptr;              //   [36 kk][512 16-byte chunks] in the B buffers' swizzled order, and their exponent
     uint16_t *w2h = nullptr;         //   (w3e[1]: conv2's) and conv2's weights pre-split into the B2 image bytes
@@ -189,6 +192,11 @@ struct UpdateTarget {
     // optional: per-block partial max |w| of the new conv3 image (one per conv3 image
     // block of grad_update_kernel, gu_blocks(32, 36) of them) for the next h3 act forward
     float *wmax_out = nullptr;
+    // optional: the new conv2 / conv3 / Dense1 images split for the next act forward
+    // (w3_split_kernel's layouts, with the exponents of its last launch): that forward skips
+    // w3_split_kernel (QWork::split_fresh)
+    uint16_t *s_w3h = nullptr, *s_w2h = nullptr, *s_w1h = nullptr;
+    const int *s_w3e = nullptr, *s_w1e = nullptr;
 };
 constexpr int GU_WMAX_BLOCKS = 36 * (32 / 16);   // conv3 image blocks of grad_update_kernel (gu_blocks(32, 36))
 // the trainer's bookkeeping after an update (utils.jl:456-481: track_loss!, epsilon decay,

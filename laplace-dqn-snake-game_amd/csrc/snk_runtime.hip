@@ -15,7 +15,7 @@ static thread_local std::string g_err;
 static thread_local hipStream_t g_user_stream = nullptr;
 static thread_local bool g_user_stream_set = false;
 // snk_set_arith knobs, production defaults (SNK_ARITH_* in include/snakehip.h)
-static int g_arith[SNK_ARITH_COUNT] = {1, 1, 1, 1, 0, 0, 1, 1};
+static int g_arith[SNK_ARITH_COUNT] = {1, 1, 1, 1, 0, 0, 1, 1, 1};
 static hipStream_t g_own_stream[64] = {};
 
 void set_error(const char *fmt, ...) {

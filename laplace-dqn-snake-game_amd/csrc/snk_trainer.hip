@@ -94,8 +94,12 @@ struct snk_trainer_s {
 // chain: the previous iteration of this launch sequence (same learn / n_upd) ran
 // just before, so its last grad_update wrote the conv3 weight-max partials of
 // the image the act forward reads (no scan); next_chain: the next one will.
+// split / next_split: as chain / next_chain for the split weight images of the act forward
+// (grad_update writes them, the act forward skips w3_split_kernel); a captured graph's first
+// iteration and every unroll-th eager iteration re-split with fresh exponents, so eager runs and
+// graph replays compute the same bits
 static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream_t s, int it = 0, bool chain = false,
-                              bool next_chain = false) {
+                              bool next_chain = false, bool split = false, bool next_split = false) {
     const EnvDev &E = env_dev(h->env);
     const ReplayDev &R = replay_dev(h->rb);
     snk_dqn_s *q = h->dqn;
@@ -103,11 +107,14 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     const uint64_t sseed = h->cfg.seed ^ 0x5A4D504C45ULL;
     chain = chain && upd && !q->deep;
     next_chain = next_chain && upd && !q->deep;
+    split = split && chain && arith(SNK_ARITH_SPLIT_CHAIN);
+    next_split = next_split && next_chain && arith(SNK_ARITH_SPLIT_CHAIN);
     // the first update's sample (counting the n transitions this step stores) rides in a
     // spare workgroup of a launch of the act forward (batch <= 64): the weight-max scan or the
     // fused conv kernel (small net), the head (deep net)
     const bool ride = upd && h->B <= 64;
     if (chain) q->act.wmax_fresh = 1;
+    if (split) q->act.split_fresh = 1;
     HeadArgs ha;
     SampleRider rider;
     if (ride) {
@@ -192,6 +199,13 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
             // nb % rate == 0, and (last block to arrive) the post-update bookkeeping
             UpdateTarget ut = dqn_update_target(q, &h->stats->nb, h->cfg.target_update_rate);
             if (last && next_chain) ut.wmax_out = q->act.wmax_part;   // for the next iteration's act forward
+            if (last && next_split) {   // ... and its split images (w3_split_kernel's exponents)
+                ut.s_w3h = q->act.w3h;
+                ut.s_w2h = q->act.w2h;
+                ut.s_w1h = q->act.w1h;
+                ut.s_w3e = q->act.w3e;
+                ut.s_w1e = q->act.w1e;
+            }
             if (h->comm) {   // data-parallel replicas: mean gradient before the step
                 grad_update_launch(q->L, &pend, q->grad, nullptr, s);
                 comm_allreduce_mean(h->comm, q->grad, q->L.P, s);
@@ -348,7 +362,7 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
             }
             SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             try {
-                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s, i, i > 0, i + 1 < n);
+                for (int i = 0; i < n; ++i) trainer_iteration(h, learn != 0, upi, s, i, i > 0, i + 1 < n, i > 0, i + 1 < n);
             } catch (...) {
                 hipGraph_t dummy;
                 (void)hipStreamEndCapture(s, &dummy);
@@ -360,7 +374,8 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
         };
         if (!use_graph) {
             for (int64_t i = 0; i < iters; ++i)
-                trainer_iteration(h, learn != 0, upi, s, (int)(i % (1 << 20)), i > 0, i + 1 < iters);
+                trainer_iteration(h, learn != 0, upi, s, (int)(i % (1 << 20)), i > 0, i + 1 < iters, i % U != 0,
+                                  i + 1 < iters && (i + 1) % U != 0);
             return;
         }
         if (U <= 1) {

@@ -471,3 +471,26 @@ def test_env_fused_act_head_bitexact(snk):
         assert np.array_equal(x, y)
     a, q = res[True][0][:U], res[True][1][:U]
     assert 0.05 < (a != q.argmax(2)).mean() < 0.3   # the epsilon draws took effect (0.3 x 2/3 at most)
+
+
+def test_split_chain_matches_fresh_splits(snk):
+    """The trainer's chained act forwards (grad_update writes conv2 / conv3 / Dense1's split images
+    with the exponents of the graph's first w3_split_kernel; the act forward skips the split launch)
+    against a w3_split_kernel launch every iteration (snk.arith(split_chain=False)): while no
+    weight maximum crosses a power of two inside a graph the exponents agree and so do the bits;
+    16 captured iterations with learning at 4096 envs: actions, Q-values, losses, both nets."""
+    n, U = 4096, 8
+    res = {}
+    for chained in (True, False):
+        with snk.arith(split_chain=chained):
+            tr = snk.Trainer(n_envs=n, board_size=12, n_frames=2, capacity=20_000, batch_size=64, n_batches=10_000,
+                             epsilon=0.05, epsilon_end=0.05, decay=0.0, seed=0x5C, graph_unroll=U)
+            snk.fill_buffer_(tr, graph=True)
+            acts = snk.DeviceArray.from_host(np.zeros((U, n), np.uint8))
+            qs = snk.DeviceArray.from_host(np.zeros((U, n, 3), np.float32))
+            tr.set_act_trace(acts, qs)
+            tr.run(2 * U, learn=True, graph=True)
+            res[chained] = (acts.numpy(), qs.numpy(), np.array(tr.losses), tr.model.get_params(),
+                            tr.model.get_params(snk.SNK_NET_TARGET))
+    for x, y in zip(res[True], res[False]):
+        assert np.array_equal(x, y)
