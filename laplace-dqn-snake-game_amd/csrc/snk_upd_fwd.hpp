@@ -43,7 +43,8 @@
 namespace snk {
 
 // Profiling builds only (make clocks): per-workgroup phase timestamps, read back by
-// snk_upd_debug_clocks (slots: start, phase 0, 1, 2 done, phase 3 done)
+// snk_upd_debug_clocks (slots: start, phase 0, 1, 2 done, phase 3 done, phase 4 done (slab stored),
+// phase 5 done (the last arriver's heads))
 #ifdef SNK_ENV_CLOCKS
 __device__ uint64_t *g_upd_clk;
 #define UPD_CLK(slot)                                                                                  \
@@ -624,6 +625,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
 #else
         n.slab[((int64_t)half * args.S + s) * 64 + tid] = (float)z;
 #endif
+        UPD_CLK(5);
         if (!args.head) return;
         // ---- phase 5: the last of the sample's four workgroups (2 halves x 2 nets) runs the
         // heads. The hand-off without fences (an agent release / acquire pair is a write-back of
@@ -644,6 +646,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
         if (!last) return;
         if (tid == 0) __hip_atomic_store(args.ticket + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         head_pair_one(args.hn[0], args.hn[1], 2, args.S, L, args.ha, s, tid);
+        UPD_CLK(6);
     }
 }
 

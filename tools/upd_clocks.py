@@ -25,7 +25,11 @@ assert lib.snk_upd_debug_clocks(nwg, buf.ctypes.data, 0) == 0
 c = buf.astype(np.float64) / 100.0
 t0 = c[:, 0].min()
 ph = {"phase0_loads": c[:, 1] - c[:, 0], "phase1_conv1": c[:, 2] - c[:, 1], "phase2_conv2": c[:, 3] - c[:, 2],
-      "phase3_conv3": c[:, 4] - c[:, 3], "start_offset": c[:, 0] - t0, "lifetime": c[:, 4] - c[:, 0]}
+      "phase3_conv3": c[:, 4] - c[:, 3], "phase4_dense1": c[:, 5] - c[:, 4], "start_offset": c[:, 0] - t0,
+      "lifetime": c[:, 5] - c[:, 0]}
+last = buf[:, 6] > 0
+if last.any():
+    ph["phase5_heads_last"] = c[last, 6] - c[last, 5]
 out = {k: {"median": float(np.median(v)), "max": float(v.max())} for k, v in ph.items()}
-out["grid_end_us"] = float(c[:, 4].max() - t0)
+out["grid_end_us"] = float(np.max(np.where(buf[:, 6] > 0, c[:, 6], c[:, 5])) - t0)
 print(json.dumps(out))
