@@ -62,6 +62,10 @@ constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 #if SNK_H3F_VAR && !defined(SNK_ENV_CLOCKS)
 #error "SNK_H3F_VAR: measurement (clocks) builds only"
 #endif
+// persistent passes after the first read conv1's weights from LDS (0: from L2, A/B builds)
+#ifndef H3F_W1LDS
+#define H3F_W1LDS 1
+#endif
 // conv3's output stored from the accumulators instead of through LDS
 #ifndef H3F_DIRECT
 #define H3F_DIRECT 0
@@ -362,9 +366,21 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
         if (!have_boards && tid < NSG * C) pbase[tid] = tid / C < ns ? a.src.plane(s0 + tid / C, tid % C) : nullptr;
         const int cq = tid & 3;
         f32x4 w1r[9 * C], b1r;
+        // the conv1 weights and bias: from L2 in the first pass, which also parks them in LDS; the
+        // persistent passes after it read them there (an L2 round trip in front of conv1 each)
+        __shared__ f32x4 w1s[9 * C * 4 + 4];
+        if (!have_boards || !H3F_W1LDS) {
 #pragma unroll
-        for (int q = 0; q < 9 * C; ++q) w1r[q] = reinterpret_cast<const f32x4 *>(a.w1)[q * 4 + cq];
-        b1r = reinterpret_cast<const f32x4 *>(a.b1)[cq];
+            for (int q = 0; q < 9 * C; ++q) w1r[q] = reinterpret_cast<const f32x4 *>(a.w1)[q * 4 + cq];
+            b1r = reinterpret_cast<const f32x4 *>(a.b1)[cq];
+            if (persist && H3F_W1LDS && tid < 9 * C * 4 + 4)
+                w1s[tid] = tid < 9 * C * 4 ? reinterpret_cast<const f32x4 *>(a.w1)[tid]
+                                           : reinterpret_cast<const f32x4 *>(a.b1)[tid - 9 * C * 4];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 9 * C; ++q) w1r[q] = w1s[q * 4 + cq];
+            b1r = w1s[9 * C * 4 + cq];
+        }
         const bool fl = a.src.fbase != nullptr;
         if (!have_boards) {
             __syncthreads();
