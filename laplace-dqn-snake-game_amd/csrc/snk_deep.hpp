@@ -657,6 +657,11 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         f32x4 acc[TPS][2];
 #pragma unroll
         for (int i = 0; i < TPS; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // the epilogue's bias quads, loaded before the offsets (the epilogue re-loaded them per
+        // row tile; L1 hits, the same time: `profiles/r05j2_l3_bias.txt`)
+        f32x4 bb[2];
+#pragma unroll
+        for (int c2 = 0; c2 < 2; ++c2) bb[c2] = *reinterpret_cast<const f32x4 *>(bias + (2 * half + c2) * 16 + 4 * g);
         // one barrier per offset: wait for this wave's DMAs of offsets kk and kk + 1 (kk + 2 stays
         // in flight), barrier (every wave's pieces landed; every wave is past offset kk - 1, so
         // its slot is free), refill that slot with offset kk + 3. The weight fragments of kk + 1
@@ -706,11 +711,9 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
             if (sg >= S) continue;
             const int o = r + (t % WO) * WO;
 #pragma unroll
-            for (int c2 = 0; c2 < 2; ++c2) {
-                const f32x4 bb = *reinterpret_cast<const f32x4 *>(bias + (2 * half + c2) * 16 + 4 * g);
+            for (int c2 = 0; c2 < 2; ++c2)
                 *reinterpret_cast<u32x2 *>(y + (sg * WO * WO + o) * 64 + (2 * half + c2) * 16 + 4 * g) =
-                    relu_bf16x4(acc[i][c2], bb);
-            }
+                    relu_bf16x4(acc[i][c2], bb[c2]);
         }
         __syncthreads();   // every wave is done reading this pair's inputs
         if (more) {   // the next pair's inputs
