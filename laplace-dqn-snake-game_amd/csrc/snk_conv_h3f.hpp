@@ -349,6 +349,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
         }
     }
     f32x4 wv[LW], av[LA];
+    float a1b = 0.0f;   // the group's bound on conv1's output (below)
     const f32x4 *w4 = reinterpret_cast<const f32x4 *>(a.w2);
     const int na4 = ns * hin2 * 4;
 #pragma unroll
@@ -418,11 +419,16 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
                 cbase1 = pbase[C - 1] - (int64_t)s0 * a.src.pitch;
             }
         }
+        float xm = 0.0f;   // max |x| over the thread's cells (absent cells are 0)
 #pragma unroll
         for (int u = 0; u < LB; ++u) {
             const int q = u * 512 + tid;
-            if (q < NX) xin[q] = fl ? __int_as_float(bv[u]) : (float)bv[u];
+            const float xv = fl ? __int_as_float(bv[u]) : (float)bv[u];
+            if (q < NX) xin[q] = xv;
+            xm = fmaxf(xm, fabsf(xv));
         }
+        xm = wave_max(xm);
+        if (lane == 0) red[wave][6] = xm;
         // after the boards are consumed: the compiler does not count LDS-DMAs in its vmcnt
         // waits, so a wait for a load issued before them comes out as vmcnt(0)
         __builtin_amdgcn_sched_barrier(0);
@@ -451,51 +457,55 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
             }
             av[u] = f32x4{fmaxf(acc01[0], 0.f), fmaxf(acc01[1], 0.f), fmaxf(acc23[0], 0.f), fmaxf(acc23[1], 0.f)};
         }
+        // conv1's output bound: a1[c] <= |b1[c]| + max|x| * sum over taps |w1[tap][c]| for every
+        // sample of the group; the thread's four channels, then the quad's sixteen by DPP
+        float xg = red[0][6];
+#pragma unroll
+        for (int w8 = 1; w8 < 8; ++w8) xg = fmaxf(xg, red[w8][6]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float sw = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 9 * C; ++q) sw += fabsf(w1r[q][e]);
+            a1b = fmaxf(a1b, fabsf(b1r[e]) + xg * sw);
+        }
+        a1b = dpp_max<0x4E>(dpp_max<0xB1>(a1b));
     }
     H3F_CLK(1);
     float wm3 = wmx;
     if (!DMA)
         for (int i = tid + 512; i < a.nwmax; i += 512) wm3 = fmaxf(wm3, a.wmax[i]);
-    float mw2 = 0.0f, ms[NSG] = {0.0f, 0.0f, 0.0f, 0.0f};
+    // A1's exponent is the group's bound's, not each sample's max |a1| (a reduction and a
+    // barrier fewer): the h3 split is scale-free, so this changes nothing but where an
+    // element's l part meets the fp16 subnormals (values below ~2^-27 of the bound)
+    int ea1[NSG], ew2 = ew2_dma;
 #pragma unroll
-    for (int u = 0; u < LW; ++u) {
-        const f32x4 v = wv[u];
-        if (!DMA && u * 512 + tid < NW4)
-            mw2 = fmaxf(mw2, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-    }
+    for (int q = 0; q < NSG; ++q) ea1[q] = h3_exp(a1b);
+    if constexpr (!DMA) {   // conv2 / conv3 weight exponents from the data
+        float mw2 = 0.0f;
 #pragma unroll
-    for (int u = 0; u < LA; ++u) {
-        const int e = u * 512 + tid;
-        const int sr = e < na4 ? e / (hin2 * 4) : NSG;
-        const f32x4 v = av[u];
-        const float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
-#pragma unroll
-        for (int q = 0; q < NSG; ++q) ms[q] = sr == q ? fmaxf(ms[q], m) : ms[q];
-    }
-#pragma unroll
-    for (int q = 0; q < NSG; ++q) ms[q] = wave_max(ms[q]);
-    mw2 = wave_max(mw2);
-    wm3 = wave_max(wm3);
-    if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < NSG; ++q) red[wave][q] = ms[q];
-        red[wave][4] = mw2;
-        red[wave][5] = wm3;
-    }
-    lds_barrier();   // also: the border fill is complete
-    int ea1[NSG], ew2;
-    {
-        float m[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            m[q] = red[0][q];
-#pragma unroll
-            for (int w8 = 1; w8 < 8; ++w8) m[q] = fmaxf(m[q], red[w8][q]);
+        for (int u = 0; u < LW; ++u) {
+            const f32x4 v = wv[u];
+            if (u * 512 + tid < NW4)
+                mw2 = fmaxf(mw2, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
         }
+        mw2 = wave_max(mw2);
+        wm3 = wave_max(wm3);
+        if (lane == 0) {
+            red[wave][4] = mw2;
+            red[wave][5] = wm3;
+        }
+        lds_barrier();
+        float m4 = red[0][4], m5 = red[0][5];
 #pragma unroll
-        for (int q = 0; q < NSG; ++q) ea1[q] = h3_exp(m[q]);
-        ew2 = DMA ? ew2_dma : h3_exp(m[4]);
-        ew = DMA ? ew_dma : h3_exp(m[5]);
+        for (int w8 = 1; w8 < 8; ++w8) {
+            m4 = fmaxf(m4, red[w8][4]);
+            m5 = fmaxf(m5, red[w8][5]);
+        }
+        ew2 = h3_exp(m4);
+        ew = h3_exp(m5);
+    } else {
+        ew = ew_dma;
     }
 #pragma unroll
     for (int u = 0; u < LW; ++u) {   // image [kk][co][ci]: k = 16 * (kk - 2p) + ci in offset pair p
