@@ -204,6 +204,11 @@ __host__ __device__ constexpr int updf_base_bytes(int hin, int C) {
 // in the LDS beyond the images, filled by LDS-DMA NR - 1 offsets ahead; boards whose images
 // leave room for fewer than UPDF_RING_MIN slots keep the register-staged path
 constexpr int UPDF_SLOT = 3 * 32 * 32 * 2, UPDF_RING_MAX = 12, UPDF_RING_MIN = 6;
+// conv3 ring offsets per barrier step (1, 2, 3 or 4: 36, 18, 12 or 9 barriers): 3 took the
+// B = 64 update from 0.0720 to 0.0711 ms (profiles/r05bb_upd_ring_ab.txt)
+#ifndef UPDF_KS
+#define UPDF_KS 3
+#endif
 __host__ __device__ constexpr int updf_ring(int hin, int C) {
     return (160 * 1024 - updf_base_bytes(hin, C)) / UPDF_SLOT >= UPDF_RING_MAX
                ? UPDF_RING_MAX
@@ -235,6 +240,16 @@ __device__ __forceinline__ f32x4v mfma_x6(const u32x4 *a, const u32x4 *b, f32x4v
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
     return c;
+}
+
+// s_waitcnt vmcnt(n) for a value n that is constant only after unrolling (the builtin needs a
+// literal): n > 12 waits for vmcnt(12), n < 0 for vmcnt(0)
+__device__ __forceinline__ void vm_wait_le12(int n) {
+#define VMW(k) else if (n == k) __builtin_amdgcn_s_waitcnt(waitcnt_vm(k));
+    if (n >= 12) __builtin_amdgcn_s_waitcnt(waitcnt_vm(12));
+    VMW(11) VMW(10) VMW(9) VMW(8) VMW(7) VMW(6) VMW(5) VMW(4) VMW(3) VMW(2) VMW(1)
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+#undef VMW
 }
 
 template <int HIN, int C>
@@ -363,7 +378,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     // enough to cover the weights' trip from L2 / MALL, conv1 is not)
     if constexpr (RING) {
 #pragma unroll
-        for (int k = 0; k < NR - 1; ++k) dma3(k);
+        for (int k = 0; k < NR - UPDF_KS; ++k) dma3(k);
     }
 
     // ---- phase 2: conv2 on x6 MFMA: rows = the HIN^2 positions, 32 columns -------------
@@ -500,16 +515,18 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
         };
         static_assert(NSTG % 2 == 0, "stages come in pairs");
         if constexpr (RING) {
-            // one barrier per offset: wait for this wave's DMA of offset kk (the newer ones,
-            // up to NR - 2, may stay in flight), publish with the barrier (every wave has also
-            // read slot (kk - 1) % NR into registers), refill that slot with offset kk + NR - 1.
-            // Chains as the staged path: offset kk into acc[.][(kk % 3) & 1]
-            // software-pipelined: step kk reads offset kk's fragments (B from slot kk % NR, A from
-            // the image) into registers right after the barrier, then issues offset kk - 1's MFMAs
-            // from the previous step's registers, so the LDS latency hides under the MFMAs
+            // UPDF_KS offsets per step, one barrier each: wait for this wave's DMAs of the
+            // step's offsets (newer ones may stay in flight), publish with the barrier (every wave
+            // has also read step st - 1's slots into registers), refill those slots with offsets
+            // st KS + NR - KS .. + KS - 1. Chains as the staged path: offset kk into
+            // acc[.][(kk % 3) & 1], in kk order. Software-pipelined: step st reads its offsets'
+            // fragments (B from slot kk % NR, A from the image) right after the barrier, then
+            // issues step st - 1's MFMAs from registers, so the LDS latency hides under them
             static_assert(NTW == 1, "ring path: one row tile per wave");
+            constexpr int KS = UPDF_KS, NS = 36 / KS;
+            static_assert(36 % KS == 0 && NR >= 2 * KS + 1, "ring steps");
             const bool live = rt0 < T3;   // wave-uniform
-            u32x4 fa[2][3], fb[2][3];
+            u32x4 fa[2][KS][3], fb[2][KS][3];
             auto frag = [&](int kk, u32x4 (&xa)[3], u32x4 (&xb)[3]) __attribute__((always_inline)) {
                 const int du = kk % 6, dv = kk / 6;
                 const uint16_t *bb = R3 + (kk % NR) * (UPDF_SLOT / 2) + (ct * 16 + r) * LDB + 8 * (g ^ ((r >> 2) & 3));
@@ -521,23 +538,30 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
                 for (int pl = 0; pl < 3; ++pl) xa[pl] = *reinterpret_cast<const u32x4 *>(pa + pl * A2P);
             };
 #pragma unroll
-            for (int kk = 0; kk <= 36; ++kk) {
-                if (kk < 36) {
-                    if (kk + NR - 2 <= 35)
-                        __builtin_amdgcn_s_waitcnt(waitcnt_vm(NR - 2));
-                    else
-                        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of slot (kk - 1) % NR done
+            for (int st = 0; st <= NS; ++st) {
+                if (st < NS) {
+                    // this wave's DMAs of the step's offsets landed: the ones issued after them
+                    // (offsets up to min(35, st KS + NR - KS - 1)) may stay in flight
+                    vm_wait_le12(min(35, st * KS + NR - KS - 1) - (st * KS + KS - 1));
+                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of step st - 1 done
                     __builtin_amdgcn_s_barrier();
-                    if (kk + NR - 1 < 36) dma3(kk + NR - 1);
-                    if (live) frag(kk, fa[kk & 1], fb[kk & 1]);
+#pragma unroll
+                    for (int k = 0; k < KS; ++k)
+                        if (st * KS + NR - KS + k < 36) dma3(st * KS + NR - KS + k);
+                    if (live) {
+#pragma unroll
+                        for (int k = 0; k < KS; ++k) frag(st * KS + k, fa[st & 1][k], fb[st & 1][k]);
+                    }
                 }
-                if (kk > 0 && live) {
-                    const int k1 = kk - 1;
-                    if (((k1 % 3) & 1) == 0)
-                        acc[0][0] = mfma_x6(fa[k1 & 1], fb[k1 & 1], acc[0][0]);
-                    else
-                        acc[0][1] = mfma_x6(fa[k1 & 1], fb[k1 & 1], acc[0][1]);
+                if (st > 0 && live) {
+#pragma unroll
+                    for (int k = 0; k < KS; ++k) {
+                        const int k1 = (st - 1) * KS + k;
+                        if (((k1 % 3) & 1) == 0)
+                            acc[0][0] = mfma_x6(fa[(st - 1) & 1][k], fb[(st - 1) & 1][k], acc[0][0]);
+                        else
+                            acc[0][1] = mfma_x6(fa[(st - 1) & 1][k], fb[(st - 1) & 1][k], acc[0][1]);
+                    }
                 }
             }
         } else {
