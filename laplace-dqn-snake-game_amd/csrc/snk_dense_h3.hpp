@@ -20,6 +20,7 @@
 // vmcnt waits on the A registers exact (a loop back edge merged them to waits on the newest
 // loads, which also count the DMAs).
 #pragma once
+#include <utility>
 #include "snk_conv_h3.hpp"
 
 namespace snk {
@@ -34,6 +35,29 @@ struct DenseH3Args {
 };
 constexpr int DH3_RING = 4, DH3_SLOT = 2 * 64 * 64 * 2;   // bytes per slot: both planes of one position
 constexpr int DH3_NT = 512;                                  // 8 waves x 16 rows
+// A (a3) loaded DH3_AD positions ahead (D + 1 register sets)
+#ifndef DH3_AD
+#define DH3_AD 2
+#endif
+
+// vector-memory ops a lane has issued after the later of A(j) (4 loads) and B(j) (2 LDS-DMA
+// pieces) when position j's wait comes: prologue B0 B1 B2 (the row maxima and exponents) A0 ..
+// A(D-1), then after the barrier of each step s: B(s + 3), A(s + D)
+__host__ __device__ constexpr int dh3_newer(int j, int D, int KPZ) {
+    int t = 0, pa[64] = {}, pb[64] = {};
+    for (int p = 0; p < 3 && p < KPZ; ++p) { t += 2; pb[p] = t; }
+    for (int p = 0; p < D && p < KPZ; ++p) { t += 4; pa[p] = t; }
+    for (int q = 0; q < j; ++q) {
+        if (q + 3 < KPZ) { t += 2; pb[q + 3] = t; }
+        if (q + D < KPZ) { t += 4; pa[q + D] = t; }
+    }
+    return t - (pa[j] > pb[j] ? pa[j] : pb[j]);
+}
+
+template <typename F, int... J>
+__device__ __forceinline__ void dh3_for(F &&f, std::integer_sequence<int, J...>) {
+    (f(std::integral_constant<int, J>{}), ...);
+}
 
 template <int KPZ>   // positions per slab; the launch guarantees nkk % KPZ == 0
 __global__ __launch_bounds__(DH3_NT) void dense_h3_kernel(DenseH3Args a) {
@@ -63,6 +87,11 @@ __global__ __launch_bounds__(DH3_NT) void dense_h3_kernel(DenseH3Args a) {
             x[ks][1] = *reinterpret_cast<const f32x4 *>(p + 32 * ks + 4);
         }
     };
+    // B(0..2) first: the compiler does not count LDS-DMAs in its own vmcnt waits, so a register
+    // load issued before them is waited for with vmcnt(0) (which drained the A prefetches too)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+        if (p < KPZ) dma(p);
     const int ea = h3_exp(a.a3max[ar]);
     // the maxima of the C rows this lane writes (sample row0 + 4g + e), and the slab's B
     // exponents of its four columns, up front (a load inside the loop would be the newest
@@ -78,38 +107,32 @@ __global__ __launch_bounds__(DH3_NT) void dense_h3_kernel(DenseH3Args a) {
     f32x4v acc[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc[ct] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    // issue order (vmcnt retires loads and DMAs together, in order): B(0) A(0) B(1) A(1) B(2),
-    // then per position j: A(j+2) B(j+3). At j, A(j) and everything older (B(<= j)) must have
-    // landed; B(j+1), A(j+1) and B(j+2), issued after A(j), may stay in flight
-    f32x4 xa[3][2][2];   // [set][k-step][half]
-    dma(0);
-    aload(0, xa[0]);
-    if (KPZ > 1) {
-        dma(1);
-        aload(1, xa[1]);
-    }
-    if (KPZ > 2) dma(2);
+    // issue order (vmcnt retires loads and DMAs together, in order): B(0) B(1) B(2) (above)
+    // A(0) .. A(D-1), then per position j: B(j+3) A(j+D). At j, A(j) and B(j) must have landed;
+    // what was issued after the later of them may stay in flight (dh3_newer, a constant per j:
+    // the position loop is a fold over an index sequence)
+    constexpr int D = DH3_AD < KPZ - 1 ? DH3_AD : KPZ - 1, NSET = D + 1;
+    f32x4 xa[NSET][2][2];   // [set][k-step][half]
 #pragma unroll
-    for (int j = 0; j < KPZ; ++j) {
-        const int newer = (j + 1 < KPZ ? 6 : 0) + (j + 2 < KPZ ? 2 : 0);
-        if (newer == 8) __builtin_amdgcn_s_waitcnt(waitcnt_vm(8));
-        else if (newer == 6) __builtin_amdgcn_s_waitcnt(waitcnt_vm(6));
-        else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    for (int p = 0; p < D; ++p) aload(p, xa[p % NSET]);
+    auto position = [&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(dh3_newer(j, D, KPZ)));
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's reads of slot (j - 1) % 4 done
         __builtin_amdgcn_s_barrier();         // every wave's pieces of B(j) landed; slot (j + 3) % 4 free
         // pinned here: left to itself the scheduler sank the prefetches behind this
         // position's MFMAs
         __builtin_amdgcn_sched_barrier(0);
-        if (j + 2 < KPZ) aload(j + 2, xa[(j + 2) % 3]);
-        if (j + 3 < KPZ) dma(j + 3);
+        if constexpr (j + 3 < KPZ) dma(j + 3);
+        if constexpr (j + D < KPZ) aload(j + D, xa[(j + D) % NSET]);
         __builtin_amdgcn_sched_barrier(0);
         // A fragments: the position's 16 values per lane, scaled and split
         f16x8 ah[2], al[2];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             u32x2 h0, l0, h1, l1;
-            h3_split4(xa[j % 3][ks][0], ea, h0, l0);
-            h3_split4(xa[j % 3][ks][1], ea, h1, l1);
+            h3_split4(xa[j % NSET][ks][0], ea, h0, l0);
+            h3_split4(xa[j % NSET][ks][1], ea, h1, l1);
             ah[ks] = as_h(u32x4{h0[0], h0[1], h1[0], h1[1]});
             al[ks] = as_h(u32x4{l0[0], l0[1], l1[0], l1[1]});
         }
@@ -135,7 +158,8 @@ __global__ __launch_bounds__(DH3_NT) void dense_h3_kernel(DenseH3Args a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[ct][e] = __builtin_fmaf(c[e], sc, acc[ct][e]);
         }
-    }
+    };
+    dh3_for(position, std::make_integer_sequence<int, KPZ>{});
     __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
     // C row 4g + e = sample row0 + 4g + e, column ct*16 + r; the row scale back
     float *out = a.slab + (int64_t)z * a.S * 64;
