@@ -424,7 +424,10 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
         for (int u = 0; u < LB; ++u) {
             const int q = u * 512 + tid;
             const float xv = fl ? __int_as_float(bv[u]) : (float)bv[u];
-            if (q < NX) xin[q] = xv;
+            if (q < NX) {   // [sample][bordered cell][channel]: a tap's C channels in one LDS read
+                const int sc = q / NPB, b = q - sc * NPB;
+                xin[((sc / C) * NPB + b) * C + sc % C] = xv;
+            }
             xm = fmaxf(xm, fabsf(xv));
         }
         xm = wave_max(xm);
@@ -446,9 +449,19 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
 #pragma unroll
             for (int kk = 0; kk < 9; ++kk) {
                 const int du = kk % 3, dv = kk / 3;
+                const float *xp = xin + (sr * NPB + (i + du) + (j + dv) * BP) * C;
+                float xc[C];
+                if constexpr (C == 2) {
+                    const f32x2 x2 = *reinterpret_cast<const f32x2 *>(xp);
+                    xc[0] = x2[0];
+                    xc[C - 1] = x2[1];
+                } else {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) xc[c] = xp[c];
+                }
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    const float x = xin[(sr * C + c) * NPB + (i + du) + (j + dv) * BP];
+                    const float x = xc[c];
                     const f32x2 xx{x, x};
                     const f32x4 w = w1r[kk * C + c];
                     acc01 = __builtin_elementwise_fma(xx, f32x2{w[0], w[1]}, acc01);
