@@ -146,6 +146,9 @@ __device__ __forceinline__ void env_act_head(const EnvActHead &H, int64_t n, int
                                              uint8_t *s_slot) {
     constexpr int KMAX = 8;
     const int64_t es = valid ? e : 0;
+    // epsilon first: loaded behind the early returns below it was one more memory round trip
+    // after the Q values, on the step's critical path
+    const float eps = H.eps_dev ? *H.eps_dev : H.epsilon;
     envf4 z[KMAX][4];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k)
@@ -188,7 +191,6 @@ __device__ __forceinline__ void env_act_head(const EnvActHead &H, int64_t n, int
     H.q[e * 3 + 1] = q[1];
     H.q[e * 3 + 2] = q[2];
     // utils.jl:161-169: Float32(rand()) < epsilon ? rand(av) : av[argmax(Q)] (head_kernel's draw)
-    const float eps = H.eps_dev ? *H.eps_dev : H.epsilon;
     const float u = rng_uniform(rng_hash(H.seed, (uint64_t)e, (uint64_t)step));
     int act;
     if (u < eps) {

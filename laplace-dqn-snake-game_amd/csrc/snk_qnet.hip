@@ -618,7 +618,7 @@ __global__ __launch_bounds__(256) void head_pair_kernel(HeadNet tn, HeadNet qn, 
                                                         HeadArgs ha) {
     const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= S) return;
-    head_pair_one(tn, qn, ks, S, L, ha, s, threadIdx.x & 63);
+    head_pair_one(tn, qn, ks, S, L, ha, s, threadIdx.x & 63, head_pre(ha, s));
 }
 
 // backward of Dense2 + relu: dz1[s][o] = (h1 > 0) * sum_a dq[s][a] W2[a][o]

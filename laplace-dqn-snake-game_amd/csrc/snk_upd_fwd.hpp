@@ -75,9 +75,19 @@ __device__ __forceinline__ float wave_sum(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-__device__ __forceinline__ void head_pair_one(const HeadNet &tn, const HeadNet &qn, int ks, int64_t S,
-                                              const QLayout &L, const HeadArgs &ha, int64_t s, int lane) {
+// the sample's replay fields (mask, done, reward, action), two dependent loads (the slot, then
+// the fields): upd_fwd_kernel issues them at its start, long before its phase 5 needs them
+struct HeadPre {
+    uint32_t bits;   // mask | done << 8 | action << 16 (two registers held through the kernel)
+    float rw;
+};
+__device__ __forceinline__ HeadPre head_pre(const HeadArgs &ha, int64_t s) {
     const int64_t m = ha.idx ? ha.idx[s] : s;
+    return HeadPre{(uint32_t)ha.mask[m] | ((uint32_t)ha.done[m] << 8) | ((uint32_t)(ha.act_idx[m] % 3) << 16), ha.rew[m]};
+}
+__device__ __forceinline__ void head_pair_one(const HeadNet &tn, const HeadNet &qn, int ks, int64_t S,
+                                              const QLayout &L, const HeadArgs &ha, int64_t s, int lane,
+                                              const HeadPre &pre) {
     // every independent load of both nets up front (the kernel is load-latency bound: the
     // q_net half used to start its loads only after the t_net half's reductions)
     constexpr int KMAX = 16;
@@ -100,9 +110,9 @@ __device__ __forceinline__ void head_pair_one(const HeadNet &tn, const HeadNet &
         bq2[a] = qn.theta[L.off_d2b + a];
     }
     const float bt1 = tn.theta[L.off_d1b + lane], bq1 = qn.theta[L.off_d1b + lane];
-    const uint8_t mk = ha.mask[m], dn = ha.done[m];
-    const float rw = ha.rew[m];
-    const int a_taken = ha.act_idx[m] % 3;
+    const uint8_t mk = (uint8_t)(pre.bits & 0xff), dn = (uint8_t)((pre.bits >> 8) & 0xff);
+    const float rw = pre.rw;
+    const int a_taken = (int)(pre.bits >> 16);
     // t_net(s'): TD target (utils.jl:448-451)
     float h = bt1;
     if (ks <= KMAX) {
@@ -275,6 +285,9 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     const UpdFwdNet &n = args.net[blockIdx.y];
     const QLayout &L = args.L;
     const int s = blockIdx.x >> 1, half = blockIdx.x & 1;
+    // phase 5's replay fields, loaded now by wave 0 (only a sample's last workgroup uses them)
+    HeadPre hpre{};
+    if (args.head && threadIdx.x < 64) hpre = head_pre(args.ha, s);
     const bool wr = half == 0;   // half 0 writes the training activations
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
@@ -669,7 +682,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
         last = __shfl(last, 0, 64);
         if (!last) return;
         if (tid == 0) __hip_atomic_store(args.ticket + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        head_pair_one(args.hn[0], args.hn[1], 2, args.S, L, args.ha, s, tid);
+        head_pair_one(args.hn[0], args.hn[1], 2, args.S, L, args.ha, s, tid, hpre);
         UPD_CLK(6);
     }
 }
