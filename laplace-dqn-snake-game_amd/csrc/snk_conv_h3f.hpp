@@ -66,11 +66,6 @@ constexpr int H3F_B2_BR = 48, H3F_B2_CHUNKS = 2048;
 #ifndef H3F_W1LDS
 #define H3F_W1LDS 1
 #endif
-// conv1 on the matrix cores (h3 split of the weights and of the boards, 16x16x32 f16, written
-// straight into conv2's A1 image); 0: the VALU form, four channels per thread (A/B builds)
-#ifndef H3F_C1MFMA
-#define H3F_C1MFMA 0
-#endif
 // conv3's output stored from the accumulators instead of through LDS
 #ifndef H3F_DIRECT
 #define H3F_DIRECT 0
@@ -379,7 +374,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
 #pragma unroll
             for (int q = 0; q < 9 * C; ++q) w1r[q] = reinterpret_cast<const f32x4 *>(a.w1)[q * 4 + cq];
             b1r = reinterpret_cast<const f32x4 *>(a.b1)[cq];
-            if ((H3F_C1MFMA || (persist && H3F_W1LDS)) && tid < 9 * C * 4 + 4)
+            if (persist && H3F_W1LDS && tid < 9 * C * 4 + 4)
                 w1s[tid] = tid < 9 * C * 4 ? reinterpret_cast<const f32x4 *>(a.w1)[tid]
                                            : reinterpret_cast<const f32x4 *>(a.b1)[tid - 9 * C * 4];
         } else {
@@ -443,85 +438,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
         dma_prologue();
         __builtin_amdgcn_sched_barrier(0);
         lds_barrier();
-#if H3F_C1MFMA
-        {
-            // C^T[co][p] = sum_k W[co][k] X[p][k], k = tap * C + c (9C <= 32: one k step), on
-            // v_mfma_f32_16x16x32_f16 with the weights as A (row co = r, k = 8g .. 8g+7) and the
-            // board cells as B (column = position r of the tile): a lane's accumulator is
-            // channels 4g .. 4g+3 of one position, one 8-byte piece of the A1 image per part.
-            // Both operands as fp16 h / l of power-of-two-scaled values (exact for the board
-            // codes; the weights to 2^-22), three products (hl, lh, hh) per tile
-            static_assert(9 * C <= 32, "conv1 fan-in within one k step");
-            const float *w1f = reinterpret_cast<const float *>(w1s);   // [9C][16] then the bias [16]
-            float wk[8];
-            float mw = 0.0f, sp = 0.0f;
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int k = 8 * g + m;
-                wk[m] = k < 9 * C ? w1f[k * 16 + r] : 0.0f;
-                mw = fmaxf(mw, fabsf(wk[m]));
-                sp += fabsf(wk[m]);
-            }
-            const int ew1 = h3_exp(wave_max(mw));
-            f16x8 wh, wl;
-            {
-                u32x2 h0, l0, h1, l1;
-                h3_split4(f32x4{wk[0], wk[1], wk[2], wk[3]}, ew1, h0, l0);
-                h3_split4(f32x4{wk[4], wk[5], wk[6], wk[7]}, ew1, h1, l1);
-                wh = as_h(u32x4{h0[0], h0[1], h1[0], h1[1]});
-                wl = as_h(u32x4{l0[0], l0[1], l1[0], l1[1]});
-            }
-            // the group's bound on conv1's output (A1's exponent): |b1[co]| + max|x| sum_k |w1[k][co]|,
-            // channel r's sum over the lane's four k groups, then the max over the 16 channels
-            sp += __shfl_xor(sp, 16, 64);
-            sp += __shfl_xor(sp, 32, 64);
-            float xg = red[0][6];
-#pragma unroll
-            for (int w8 = 1; w8 < 8; ++w8) xg = fmaxf(xg, red[w8][6]);
-            float bnd = fabsf(w1f[9 * C * 16 + r]) + xg * sp;
-            bnd = dpp_max<0xB1>(bnd);
-            bnd = dpp_max<0x4E>(bnd);
-            bnd = dpp_max<0x141>(bnd);
-            a1b = dpp_max<0x140>(bnd);   // every lane: the max over the row's 16 channels
-            const int ea = h3_exp(a1b), ex = h3_exp(xg);
-            const f32x4 b1v = reinterpret_cast<const f32x4 *>(w1f + 9 * C * 16)[g];
-            constexpr int NT1 = (NSG * hin2 + 15) / 16;   // the last tile's rows past the group repeat its last
-#pragma unroll
-            for (int u = 0; u < (NT1 + 7) / 8; ++u) {
-                const int t = wave + 8 * u;
-                if (t >= NT1) break;   // wave-uniform
-                const int pq = min(t * 16 + r, NSG * hin2 - 1), sr = pq / hin2, pos = pq - sr * hin2;
-                const int j = pos / hin, i = pos - j * hin;
-                const float *xb = xin + (sr * NPB + i + j * BP) * C;
-                float xk[8];
-#pragma unroll
-                for (int m = 0; m < 8; ++m) {
-                    const int k = 8 * g + m, tap = k / C, c = k - tap * C;
-                    xk[m] = k < 9 * C ? xb[((tap % 3) + (tap / 3) * BP) * C + c] : 0.0f;
-                }
-                f16x8 xh, xl;
-                {
-                    u32x2 h0, l0, h1, l1;
-                    h3_split4(f32x4{xk[0], xk[1], xk[2], xk[3]}, ex, h0, l0);
-                    h3_split4(f32x4{xk[4], xk[5], xk[6], xk[7]}, ex, h1, l1);
-                    xh = as_h(u32x4{h0[0], h0[1], h1[0], h1[1]});
-                    xl = as_h(u32x4{l0[0], l0[1], l1[0], l1[1]});
-                }
-                f32x4v c1 = {0.f, 0.f, 0.f, 0.f};
-                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, c1, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, c1, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, c1, 0, 0, 0);
-                f32x4 v;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = fmaxf(__builtin_ldexpf(c1[e], -(ew1 + ex)) + b1v[e], 0.0f);
-                const int pb = (i + 1) + (j + 1) * BP;
-                u32x2 hh, ll;
-                h3_split4(v, ea, hh, ll);
-                A1v[(((sr * 2 + 0) * NPB + pb) * XR + 4 * g) / 4] = hh;
-                A1v[(((sr * 2 + 1) * NPB + pb) * XR + 4 * g) / 4] = ll;
-            }
-        }
-#else
 #pragma unroll
         for (int u = 0; u < LA; ++u) {   // output (sample, position, channels 4 cq..): a1's layout
             const int e = min(u * 512 + tid, na4 - 1);
@@ -567,7 +483,6 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
             a1b = fmaxf(a1b, fabsf(b1r[e]) + xg * sw);
         }
         a1b = dpp_max<0x4E>(dpp_max<0xB1>(a1b));
-#endif
     }
     H3F_CLK(1);
     float wm3 = wmx;
@@ -618,7 +533,7 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
         }
     }
 #pragma unroll
-    for (int u = 0; u < (H3F_C1MFMA ? 0 : LA); ++u) {   // a1 [s][pos][16] -> bordered [s][part][pos][24 halves]
+    for (int u = 0; u < LA; ++u) {   // a1 [s][pos][16] -> bordered [s][part][pos][24 halves]
         const int e = u * 512 + tid;
         if (e < na4) {
             const int sr = e / (hin2 * 4), loc = e - sr * hin2 * 4;

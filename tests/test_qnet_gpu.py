@@ -396,6 +396,23 @@ def test_trainer_episode_stats_fold(snk, n_envs):
     assert len(tr.buffer) == min(60 * n_envs, 4 * n_envs)
 
 
+@pytest.mark.parametrize("bs,C", [(9, 2), (10, 1), (11, 2), (13, 1), (13, 2)])
+def test_h3f_act_forward_boards_vs_oracle(snk, bs, C):
+    """conv_h3f_kernel (conv1 on the matrix cores, conv2 + conv3 on the h3 split; >= 1024
+    states) at the other board sides it serves: odd sides leave a partial conv1 tile per group,
+    13 runs the register-staged (non-DMA) form, 1100 states a partial last group of four.
+    Q of every 7th state and the last four within 1e-5 * max(1, |q|) of the fp64 oracle."""
+    rng = np.random.default_rng(bs * 10 + C)
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=31)
+    p = m.get_params()
+    x = rng.integers(-1, 3, size=(1100, C, bs * bs)).astype(np.float32)
+    q = m(x)
+    sel = np.concatenate([np.arange(0, 1100, 7), np.arange(1096, 1100)])
+    qref = oracle.qnet_forward(bs, C, p, x[sel])
+    err = np.abs(q[sel] - qref) / np.maximum(1.0, np.abs(qref))
+    assert err.max() <= 1e-5, float(err.max())
+
+
 def test_dense_h3_act_forward(snk):
     """Dense1 of the 4096-state act forward on dense_h3_kernel (fp16 h3 split, per-sample
     a3 scale from conv_h3f's epilogue, per-(position, output) weight scales from
