@@ -34,21 +34,26 @@ struct DenseH3Args {
     int S, nkk;
 };
 constexpr int DH3_RING = 4, DH3_SLOT = 2 * 64 * 64 * 2;   // bytes per slot: both planes of one position
-constexpr int DH3_NT = 512;                                  // 8 waves x 16 rows
+// waves per workgroup (16 rows each): 8 = 128-row blocks (224 workgroups at 4096 x 7 slabs)
+#ifndef DH3_WAVES
+#define DH3_WAVES 8
+#endif
+constexpr int DH3_NT = DH3_WAVES * 64, DH3_ROWS = DH3_WAVES * 16;
 // A (a3) loaded DH3_AD positions ahead (D + 1 register sets)
 #ifndef DH3_AD
 #define DH3_AD 2
 #endif
 
-// vector-memory ops a lane has issued after the later of A(j) (4 loads) and B(j) (2 LDS-DMA
-// pieces) when position j's wait comes: prologue B0 B1 B2 (the row maxima and exponents) A0 ..
-// A(D-1), then after the barrier of each step s: B(s + 3), A(s + D)
+// vector-memory ops a lane has issued after the later of A(j) (4 loads) and B(j) (1024 /
+// DH3_NT LDS-DMA pieces) when position j's wait comes: prologue B0 B1 B2 (the row maxima and
+// exponents) A0 .. A(D-1), then after the barrier of each step s: B(s + 3), A(s + D)
 __host__ __device__ constexpr int dh3_newer(int j, int D, int KPZ) {
+    constexpr int NBP = 1024 / DH3_NT;
     int t = 0, pa[64] = {}, pb[64] = {};
-    for (int p = 0; p < 3 && p < KPZ; ++p) { t += 2; pb[p] = t; }
+    for (int p = 0; p < 3 && p < KPZ; ++p) { t += NBP; pb[p] = t; }
     for (int p = 0; p < D && p < KPZ; ++p) { t += 4; pa[p] = t; }
     for (int q = 0; q < j; ++q) {
-        if (q + 3 < KPZ) { t += 2; pb[q + 3] = t; }
+        if (q + 3 < KPZ) { t += NBP; pb[q + 3] = t; }
         if (q + D < KPZ) { t += 4; pa[q + D] = t; }
     }
     return t - (pa[j] > pb[j] ? pa[j] : pb[j]);
@@ -66,15 +71,16 @@ __global__ __launch_bounds__(DH3_NT) void dense_h3_kernel(DenseH3Args a) {
     const int r = lane & 15, g = lane >> 4;
     const int z = blockIdx.y, kk0 = z * KPZ;
     const int K1 = a.nkk * 64;
-    const int row0 = blockIdx.x * 128 + wave * 16;
+    const int row0 = blockIdx.x * DH3_ROWS + wave * 16;
     // B ring: position j of the slab in slot j % DH3_RING; 1024 16-byte pieces, 2 per lane
     auto dma = [&](int j) __attribute__((always_inline)) {
         const uint16_t *src = a.w1h + (int64_t)(kk0 + j) * 2 * 4096;
+        static_assert(1024 % DH3_NT == 0, "whole pieces per lane");
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-            __builtin_amdgcn_global_load_lds((const void *)(src + (u * 512 + tid) * 8),
+        for (int u = 0; u < 1024 / DH3_NT; ++u)
+            __builtin_amdgcn_global_load_lds((const void *)(src + (u * DH3_NT + tid) * 8),
                                              (__attribute__((address_space(3))) void *)(dh3_lds + (j % DH3_RING) * (DH3_SLOT / 2) +
-                                                                                         (u * 512 + wave * 64) * 8),
+                                                                                         (u * DH3_NT + wave * 64) * 8),
                                              16, 0, 0);
     };
     // A: row row0 + r (clamped), channels 32ks + 8g .. +7 of position kk0 + j

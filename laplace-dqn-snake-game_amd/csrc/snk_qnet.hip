@@ -938,7 +938,7 @@ static void dh3_launch(const DenseH3Args &a, int ks, int kpz, hipStream_t s) {
     SNK_CHECK(kpz == 7 && ks * kpz == a.nkk && a.S > 0, SNK_ERR_INTERNAL, "dense_h3: slab split");
     constexpr size_t lds = (size_t)DH3_RING * DH3_SLOT;
     set_lds_limit((const void *)dense_h3_kernel<7>, lds);
-    dense_h3_kernel<7><<<dim3((unsigned)ceil_div(a.S, 128), (unsigned)ks), DH3_NT, lds, s>>>(a);
+    dense_h3_kernel<7><<<dim3((unsigned)ceil_div(a.S, DH3_ROWS), (unsigned)ks), DH3_NT, lds, s>>>(a);
     launch_check("dense_h3_kernel");
 }
 template <int HIN>
