@@ -431,32 +431,38 @@ def d_build_gram(args, snk, model, dist, rank, world) -> dict:
     speak = PEAK_BF16_TFLOPS / H3_PRODUCTS
     res = {"d_build_sec": wall + t_gather,
            "d_build": {"kind": "per-sample Jacobian Gram G = J J' (n x n, fp32-accurate fp16 h3 split MFMA, "
-                               "fp64 accumulation)" + (f", {world} shards of the lower-triangle tiles + RCCL "
-                                                        f"send/recv gather to rank 0" if world > 1 else ""),
+                               "fp32 sums over chunks of 5,120 k added in fp64)" +
+                               (f", {world} shards of the lower-triangle tiles + RCCL "
+                                f"send/recv gather to rank 0" if world > 1 else ""),
                        "n_samples": n, "n_params": model.P, "conv_columns": Kc, "ranks": world,
                        "shard_sec_max_over_ranks": wall, "gather_sec": t_gather,
                        **({"gather_check": gather_check} if gather_check else {}),
                        "phase_ms": {"forward_and_data_grads": ms[0], "per_sample_conv_jacobians": ms[1],
-                                    "conv_gram": ms[2], "dense_terms_and_mirror": ms[3]},
+                                    "conv_gram": ms[2], "dense_terms_chunk_sum_and_mirror": ms[3]},
                        "naive_flop": 2.0 * n * n * model.P, "executed_gram_flop_this_rank": flop_gram,
                        "roofline": {"bound": "mfma",
-                                    "kernel": "h3_rows_kernel + syrk_h3q_kernel (fp16 h3 split on "
-                                              "v_mfma_f32_16x16x32_f16, LDS-DMA staged), conv-column Gram",
+                                    "kernel": "h3_rows_kernel + syrk_h3k_kernel (256 x 256 tiles, the k "
+                                              "reduction split into fp32 chunks of 5,120; fp16 h3 split on "
+                                              "v_mfma_f32_16x16x32_f16, LDS-DMA staged), conv-column Gram; the "
+                                              "chunk sum (syrk_ksum_kernel, fp64) is in the next phase",
                                     "achieved": tf, "peak": speak, "unit": "TFLOP/s (fp32-equivalent)",
                                     "frac": tf / speak, "avg_launch_ms": ms[2], "flop_per_launch": flop_gram,
                                     "traffic": None, "half_mfma_tflops_executed": tf * H3_PRODUCTS,
                                     "mfma_utilization": tf * H3_PRODUCTS / PEAK_BF16_TFLOPS,
                                     "fp32_mfma_peak": PEAK_FP32_TFLOPS}}}
     if n == 50000 and world == 1:
-        res["d_build"]["roofline"].update(_latest_pmc("syrk_h3q_kernel<0, 4, false>", "*_pmc_syrk.json"))
-    tr_file = _latest_traffic("syrk_h3q_kernel", "*_syrk_traffic.json") if n == 50000 and world == 1 else None
+        res["d_build"]["roofline"].update(_latest_pmc("syrk_h3k_kernel", "*_pmc_syrk.json"))
+    tr_file = _latest_traffic("syrk_h3k_kernel", "*_syrk_traffic.json") if n == 50000 and world == 1 else None
     if tr_file:
         rf = res["d_build"]["roofline"]
         rf["traffic"] = tr_file["bytes_per_launch"]
         rf["traffic_source"] = tr_file["source"]
         rf["traffic_note"] = ("L2-miss bytes (HBM + Infinity Cache) of the Gram launch; its unique operand bytes "
-                              "are the n x Kc fp16 h/l row planes (4 B per entry) + the lower-triangle fp32 G")
-        uniq = 4.0 * n * ((Kc + 31) // 32 * 32) + 4.0 * n * (n + 1) / 2
+                              "are the n x Kc fp16 h/l row planes (4 B per entry) + the fp32 partial tiles it "
+                              "writes (one 256 x 256 tile per lower-triangle tile and chunk)")
+        nch = -(-((Kc + 31) // 32) // 160)
+        t256 = -(-n // 256)
+        uniq = 4.0 * n * ((Kc + 31) // 32 * 32) + 4.0 * nch * (t256 * (t256 + 1) // 2) * 256 * 256
         rf["unique_operand_bytes"] = uniq
         rf["traffic_over_unique"] = rf["traffic"] / uniq
     del G, rb
@@ -584,6 +590,18 @@ def main():
     elapsed = float(np.median(windows))   # median of the timed windows
     st = tr.stats()
     faults = tr.game.check_faults()
+    # RCCL's own count of the group (ncclCommCount on the trainer's communicator; a one-rank
+    # communicator at --gpus 1): a scaling run proves the ranks its gradient all-reduce spanned
+    if comm is not None:
+        rccl_nranks, rccl_rank = comm.info()
+    else:
+        c1 = snk.Comm(1, 0, snk.Comm.unique_id())
+        rccl_nranks, rccl_rank = c1.info()
+        del c1
+    if rccl_nranks != world or rccl_rank != rank:
+        print(json.dumps({"error": f"RCCL reports {rccl_nranks} ranks (this is rank {rccl_rank}); "
+                                   f"WORLD_SIZE {world}, RANK {rank}"}), flush=True)
+        sys.exit(3)
     if comm is not None:
         # every rank leaves the RCCL group together: rank 0's extras below keep
         # training locally (snapshots) and must not wait on ranks that have exited
@@ -626,6 +644,7 @@ def main():
                    **({"arith_ab": arith_set} if arith_set else {})},
         "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
                         "food_faults": faults},
+        "rccl_nranks": rccl_nranks,
         "roofline": None,
         "cpu_baseline": None,
     }

@@ -61,7 +61,8 @@ int snk_synchronize(void);
 #define SNK_ARITH_UPD_HEAD 6     /* 1: the update's heads run in upd_fwd_kernel's tail; 0: head_pair_kernel (same bits) */
 #define SNK_ARITH_ENV_HEAD 7     /* 1: the trainer's act head runs in env_step_kernel; 0: head_kernel (same bits) */
 #define SNK_ARITH_SPLIT_CHAIN 8  /* 1: the trainer's grad_update writes the next act forward's split weights; 0: w3_split every act */
-#define SNK_ARITH_COUNT 9
+#define SNK_ARITH_SYRK_KSPLIT 9  /* 1: Jacobian Gram on 256x256 tiles, K split into fp32 chunks summed in fp64; 0: SNK_ARITH_SYRK_H3_32's kernel */
+#define SNK_ARITH_COUNT 10
 int snk_set_arith(int32_t knob, int32_t value);
 int snk_get_arith(int32_t knob, int32_t *value_out);
 int snk_malloc(void **dev_out, int64_t bytes);
@@ -298,6 +299,9 @@ int snk_comm_create(snk_comm *out, int32_t nranks, int32_t rank, const uint8_t *
 int snk_comm_destroy(snk_comm c);
 int snk_comm_allreduce_mean(snk_comm c, float *buf_dev, int64_t n);
 int snk_comm_broadcast(snk_comm c, float *buf_dev, int64_t n, int32_t root);
+/* what RCCL itself reports for the communicator (ncclCommCount / ncclCommUserRank), not the
+ * arguments it was created with: the bench records it so a scaling run proves its rank count */
+int snk_comm_info(snk_comm c, int32_t *nranks_out, int32_t *rank_out);
 /* the trainer all-reduces (mean) the gradient of every update across the
  * communicator; broadcasts rank 0's q_net first. c = NULL detaches (updates
  * are local again; nothing is broadcast) */

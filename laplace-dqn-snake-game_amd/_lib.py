@@ -125,6 +125,7 @@ _PROTOS = {
     "snk_comm_destroy": [vp],
     "snk_comm_allreduce_mean": [vp, vp, i64],
     "snk_comm_broadcast": [vp, vp, i64, i32],
+    "snk_comm_info": [vp, P(i32), P(i32)],
     "snk_laplace_create": [P(vp), i64, i32],
     "snk_laplace_destroy": [vp],
     "snk_laplace_snapshot": [vp, vp, i32],
@@ -227,13 +228,22 @@ def ptr(a: np.ndarray | None):
     return a.ctypes.data_as(vp)
 
 
+def header_arith() -> dict[str, int]:
+    """snk_set_arith knobs as the header defines them: SNK_ARITH_<NAME> -> name.lower()."""
+    with open(HEADER) as f:
+        txt = f.read()
+    return {m.group(1).lower(): int(m.group(2))
+            for m in re.finditer(r"#define\s+SNK_ARITH_(\w+)\s+(\d+)", txt) if m.group(1) != "COUNT"}
+
+
 # snk_set_arith knobs (include/snakehip.h SNK_ARITH_*): name -> knob
-ARITH = {"x6s": 0, "h3s": 1, "dh3": 2, "h3c2": 3, "conv_fp32": 4, "syrk_h3_32": 5, "upd_head": 6, "env_head": 7, "split_chain": 8}
+ARITH = header_arith()
 
 
 def set_arith(name: str, value: bool) -> bool:
     """Select a GEMM arithmetic path process-wide (SNK_ARITH_*); returns the previous
-    value. Production defaults: x6s, h3s, dh3, h3c2, upd_head, env_head, split_chain on; conv_fp32, syrk_h3_32 off."""
+    value. Production defaults: x6s, h3s, dh3, h3c2, upd_head, env_head, split_chain, syrk_ksplit on;
+    conv_fp32, syrk_h3_32 off."""
     old = get_arith(name)
     call("snk_set_arith", ARITH[name], int(bool(value)))
     return old

@@ -100,6 +100,17 @@ extern "C" int snk_comm_allreduce_mean(snk_comm h, float *buf_dev, int64_t n) {
     });
 }
 
+extern "C" int snk_comm_info(snk_comm h, int32_t *nranks_out, int32_t *rank_out) {
+    return guard([&] {
+        SNK_CHECK(h && h->comm && nranks_out && rank_out, SNK_ERR_INVALID, "bad comm_info arguments");
+        int n = 0, r = 0;
+        SNK_NCCL(ncclCommCount(h->comm, &n));
+        SNK_NCCL(ncclCommUserRank(h->comm, &r));
+        *nranks_out = n;
+        *rank_out = r;
+    });
+}
+
 extern "C" int snk_comm_broadcast(snk_comm h, float *buf_dev, int64_t n, int32_t root) {
     return guard([&] {
         SNK_CHECK(h && buf_dev && n >= 0, SNK_ERR_INVALID, "bad broadcast arguments");

@@ -100,14 +100,27 @@ constexpr int W3S_BLOCKS = 36 * 512 / 256, W2S_BLOCKS = (9 * 32 * 16 / 4 + 255) 
 // the trainer runs w3_split_kernel again at the start of every captured graph. The cost is
 // nil: each element keeps its 22-bit h + l form, only values below 2^-14 of the maximum (whose l
 // part falls into the fp16 subnormals) carry an absolute error <= 2^-36 of the maximum
+// The headroom alone does not bound a tensor (or Dense1 row) whose maximum is tiny: RMSProp moves
+// a weight by up to lr / sqrt(1 - rho) per step whatever its size (|g| / sqrt(acc) <= 1 / sqrt(1 -
+// rho)), so a row with max 1e-3 can grow past 32x its max within a graph. The trainer
+// passes `grow`, a bound on that movement until the next fresh split (steps x lr / sqrt(1 - rho),
+// doubled for the fp32 rounding of the update), and the exponent is also capped so that
+// (max + grow) 2^e < 2^15: a chained split then stays below 2^15 < 65504 (the fp16 maximum) by
+// construction. The cap binds only when grow > ~15x the maximum (a maximum below ~0.007 at
+// lr 5e-4 and 64 chained steps), so the usual exponents, and the bits, are unchanged
+// (test_split_chain_exponent_cap_keeps_q_finite).
 constexpr int H3_W_HEADROOM = 4;
-__device__ __forceinline__ int h3_exp_w(float m) { return h3_exp(m) - H3_W_HEADROOM; }
+__device__ __forceinline__ int h3_exp_w(float m, float grow = 0.0f) {
+    const int e = h3_exp(m) - H3_W_HEADROOM;
+    return grow > 0.0f ? min(e, h3_exp(m + grow)) : e;
+}
 __host__ __device__ constexpr int w1s_blocks(int nkk) { return nkk * 64 * 16 / 256; }
 static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__restrict__ img, const float *__restrict__ wmax,
                                                        int nwmax, uint16_t *__restrict__ out, int *__restrict__ eout,
                                                        const float *__restrict__ img2, uint16_t *__restrict__ out2,
                                                        const float *__restrict__ img1 = nullptr,
-                                                       uint16_t *__restrict__ out1 = nullptr, int *__restrict__ e1 = nullptr) {
+                                                       uint16_t *__restrict__ out1 = nullptr, int *__restrict__ e1 = nullptr,
+                                                       float grow = 0.0f) {
     __shared__ float red4[4];
     if (blockIdx.x >= W3S_BLOCKS + W2S_BLOCKS) {   // Dense1
         const int t = (blockIdx.x - W3S_BLOCKS - W2S_BLOCKS) * 256 + threadIdx.x;
@@ -118,7 +131,7 @@ static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__res
         m = dpp_max<0x4E>(m);
         m = dpp_max<0x141>(m);
         m = dpp_max<0x140>(m);
-        const int ex = h3_exp_w(m);
+        const int ex = h3_exp_w(m, grow);
         if (q4 == 0) e1[row] = ex;
         u32x2 hh, ll;
         h3_split4(v, ex, hh, ll);
@@ -140,7 +153,7 @@ static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__res
         m = wave_max(m);
         if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
         __syncthreads();
-        const int ew2 = h3_exp_w(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
+        const int ew2 = h3_exp_w(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])), grow);
         if (blockIdx.x == W3S_BLOCKS && threadIdx.x == 0) eout[1] = ew2;
         if (e < NW4) {
             const int kk = e >> 7, co = (e >> 2) & 31, ci0 = 4 * (e & 3);
@@ -161,7 +174,7 @@ static __global__ __launch_bounds__(256) void w3_split_kernel(const float *__res
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
     __syncthreads();
-    const int ew = h3_exp_w(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
+    const int ew = h3_exp_w(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])), grow);
     if (blockIdx.x == 0 && threadIdx.x == 0) *eout = ew;
     const int bch = (tt >> 3) * 4 + ((tt & 7) >> 1), bhalf = tt & 1;
     u32x2 h, l;

@@ -234,7 +234,7 @@ extern "C" int snk_dqn_destroy(snk_dqn h) {
         qwork_free(h->tgt);
         qwork_free(h->trn);
         qwork_free(h->jw);
-        for (void *p : {(void *)h->jbuf, (void *)h->jplanes, (void *)h->jexp, (void *)h->dplanes, (void *)h->dexp, (void *)h->jidx, (void *)h->jact, (void *)h->theta_q, (void *)h->theta_t,
+        for (void *p : {(void *)h->jbuf, (void *)h->jplanes, (void *)h->jexp, (void *)h->dplanes, (void *)h->dexp, (void *)h->gpart, (void *)h->jidx, (void *)h->jact, (void *)h->theta_q, (void *)h->theta_t,
                         (void *)h->acc, (void *)h->grad, (void *)h->tmp,
                         (void *)h->perm, (void *)h->slab, (void *)h->loss_dev, (void *)h->meta, (void *)h->wt_q,
                         (void *)h->wt_t, (void *)h->wtb_q, (void *)h->wtb_t})

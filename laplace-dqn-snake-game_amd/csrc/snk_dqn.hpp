@@ -30,6 +30,8 @@ struct snk_dqn_s {
     uint16_t *dplanes = nullptr;    // the Dense-section Gram operands a3 | dz1 | h1 as h3 segments
     int32_t *dexp = nullptr;        //   (h3_seg_rows_kernel) and their exponents [3][dexp_cap]
     int64_t dplanes_halves = 0, dexp_cap = 0;
+    float *gpart = nullptr;         // the K-split Gram's fp32 partial tiles (syrk_h3k_kernel)
+    int64_t gpart_floats = 0;
     int64_t *jidx = nullptr;
     uint8_t *jact = nullptr;
     // snk_dqn_create_deep: the deeper bf16 net; L then holds its head offsets and P only

@@ -17,6 +17,7 @@
 //     the 79k conv columns of J go through the big MFMA Gram.
 #include <cstring>
 #include <algorithm>
+#include <deque>
 #include <mutex>
 #include <vector>
 
@@ -179,17 +180,21 @@ __global__ void jac_permute_kernel(const float *__restrict__ Jp, int64_t ldp, co
     }
 }
 
-// Lower-triangle tiles in supertile order: groups of 8 block rows x 4 block
-// columns, so the ~32 workgroups an XCD runs at once (syrk_xcd_remap hands
-// each XCD a contiguous run of this list) share 8 + 4 row blocks in its L2
-// instead of 1 + 32 in plain row-major order. One device table per N, kept.
+// The Gram's tile orders. The K-split Jacobian Gram (syrk_h3k_kernel) works on
+// 256 x 256 lower-triangle tiles in supertile order: groups of 8 block rows x 4
+// block columns, so the 32 workgroups an XCD runs at once share 8 + 4 row panels
+// in its L2 instead of 1 + 32 in plain row-major order. Shards are contiguous runs
+// of that order. Everything that works on 128 x 128 tiles (the Dense-term pass,
+// the round-5 kernel, gather / pack, the D'D slab Gram) uses the same order with
+// each 256-tile expanded into its 128-subtiles (three on the diagonal), so a
+// shard's 128-tiles are exactly its 256-tiles' area. One device table per N, kept.
 // Round 5 measured a chip-wide order (the 8 XCDs of a dispatch round on one 16 x 16 block,
 // sharing its panels in the Infinity Cache; tools/syrk_lab.hip order 1): 7 % faster on rows
 // with 40 % zeros (505 -> 473 ms, the clock 1.73 -> 1.80 GHz), but 3 % slower on dense rows
 // like the D(50k) Jacobian's (525 -> 541 ms at 1.5 GHz, gpurun_out r05j): with dense operands
 // the matrix cores' own power holds the clock down, not the HBM stream. Not kept.
-static std::vector<int2> syrk_tile_order_host(int N) {
-    const int T = (int)ceil_div(N, SY_T);
+static std::vector<int2> gram256_order_host(int64_t N) {
+    const int T = (int)ceil_div(N, SK_T);
     std::vector<int2> t;
     t.reserve((size_t)T * (T + 1) / 2);
     constexpr int SI = 8, SJ = 4;
@@ -197,6 +202,28 @@ static std::vector<int2> syrk_tile_order_host(int N) {
         for (int j0 = 0; j0 <= std::min(T - 1, i0 + SI - 1); j0 += SJ)
             for (int i = i0; i < std::min(T, i0 + SI); ++i)
                 for (int j = j0; j < std::min(j0 + SJ, i + 1); ++j) t.push_back(int2{i, j});
+    SNK_CHECK((int64_t)t.size() == (int64_t)T * (T + 1) / 2, SNK_ERR_INTERNAL, "gram tile order");
+    return t;
+}
+// the 128-subtiles (i, j <= i) of 256-tile u, in a fixed order
+static int expand256(int2 u, int T128, int2 *out) {
+    int c = 0;
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+            const int i = 2 * u.x + a, j = 2 * u.y + b;
+            if (i < T128 && j <= i) out[c++] = int2{i, j};
+        }
+    return c;
+}
+static std::vector<int2> syrk_tile_order_host(int N) {
+    const int T = (int)ceil_div(N, SY_T);
+    std::vector<int2> t;
+    t.reserve((size_t)T * (T + 1) / 2);
+    for (const int2 u : gram256_order_host(N)) {
+        int2 s[4];
+        const int c = expand256(u, T, s);
+        t.insert(t.end(), s, s + c);
+    }
     SNK_CHECK((int64_t)t.size() == (int64_t)T * (T + 1) / 2, SNK_ERR_INTERNAL, "syrk tile order");
     return t;
 }
@@ -216,14 +243,78 @@ static const int2 *syrk_tile_order(int N) {
     return d;
 }
 
-// lower-triangle tiles [t0, t1) of syrk_tile_order(N) for shard `rank` of `nranks`
-// (contiguous runs of the supertile order: each shard keeps its L2 locality)
-// (run boundaries on multiples of 8)
+// shard `rank` of `nranks`: the run [u0, u1) of the 256-tile order, proportional cuts
+// rounded to the nearest tile (contiguous runs: each shard keeps its L2 locality)
+static void gram256_range(int64_t N, int rank, int nranks, int64_t &u0, int64_t &u1) {
+    const int64_t T = ceil_div(N, SK_T), tot = T * (T + 1) / 2;
+    auto cut = [&](int r) { return (tot * r + nranks / 2) / nranks; };
+    u0 = cut(rank);
+    u1 = cut(rank + 1);
+}
+// the same shard as 128-tiles [t0, t1) of syrk_tile_order(N)
 static void gram_tile_range(int64_t N, int rank, int nranks, int64_t &t0, int64_t &t1) {
-    const int64_t T = ceil_div(N, SY_T), tot = T * (T + 1) / 2;
-    auto cut = [&](int r) { return r >= nranks ? tot : std::min(tot, (tot * r / nranks) & ~int64_t(7)); };
-    t0 = cut(rank);
-    t1 = cut(rank + 1);
+    int64_t u0, u1;
+    gram256_range(N, rank, nranks, u0, u1);
+    const int T128 = (int)ceil_div(N, SY_T);
+    const std::vector<int2> o = gram256_order_host(N);
+    int64_t c = 0;
+    t0 = t1 = 0;
+    for (int64_t u = 0; u <= (int64_t)o.size(); ++u) {
+        if (u == u0) t0 = c;
+        if (u == u1) {
+            t1 = c;
+            break;
+        }
+        int2 s[4];
+        c += expand256(o[u], T128, s);
+    }
+}
+
+// The K-split Gram's per-launch tables (one set per N, device, shard and chunk length,
+// kept): the shard's 256-tiles by local index, and one item (I, J, z, local tile) per
+// workgroup. Items run over consecutive groups of 32 tiles (about one supertile) and, inside
+// a group, chunk-major, so the workgroups an XCD runs together share the group's panels at
+// the same k; the list is dealt to the 8 XCD queues in contiguous runs and interleaved
+// (workgroup w runs on XCD w % 8).
+struct KSplitTables {
+    int64_t N, u0, u1;
+    int dev, nst, cs;
+    int2 *tiles;
+    int4 *items;
+    int64_t nitems;
+};
+static const KSplitTables &ksplit_tables(int64_t N, int64_t u0, int64_t u1, int nst, int cs) {
+    static std::mutex mu;
+    static std::deque<KSplitTables> cache;   // references stay valid as it grows
+    int dev = 0;
+    SNK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &c : cache)
+        if (c.N == N && c.u0 == u0 && c.u1 == u1 && c.dev == dev && c.nst == nst && c.cs == cs) return c;
+    const std::vector<int2> o = gram256_order_host(N);
+    const std::vector<int2> tiles(o.begin() + u0, o.begin() + u1);
+    const int S = (int)ceil_div(nst, cs), ntl = (int)tiles.size();
+    std::vector<int4> list;
+    list.reserve((size_t)ntl * S);
+    for (int g0 = 0; g0 < ntl; g0 += 32)
+        for (int z = 0; z < S; ++z)
+            for (int t = g0; t < std::min(ntl, g0 + 32); ++t) list.push_back(int4{tiles[t].x, tiles[t].y, z, t});
+    const size_t L = list.size();
+    std::vector<int4> items;
+    items.reserve(L);
+    size_t qb[9];
+    for (int x = 0; x <= 8; ++x) qb[x] = L * x / 8;
+    for (size_t j = 0; j < qb[1] - qb[0] + 1; ++j)
+        for (int x = 0; x < 8; ++x)
+            if (qb[x] + j < qb[x + 1]) items.push_back(list[qb[x] + j]);
+    SNK_CHECK(items.size() == L, SNK_ERR_INTERNAL, "k-split item table");
+    KSplitTables k{N, u0, u1, dev, nst, cs, nullptr, nullptr, (int64_t)L};
+    SNK_HIP(hipMalloc(&k.tiles, std::max<size_t>(tiles.size(), 1) * sizeof(int2)));
+    SNK_HIP(hipMalloc(&k.items, std::max<size_t>(L, 1) * sizeof(int4)));
+    if (!tiles.empty()) SNK_HIP(hipMemcpy(k.tiles, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice));
+    if (L) SNK_HIP(hipMemcpy(k.items, items.data(), L * sizeof(int4), hipMemcpyHostToDevice));
+    cache.push_back(k);
+    return cache.back();
 }
 
 static void syrk_launch(int out, const SyrkArgs &a0, int z, hipStream_t s, int rank = 0, int nranks = 1) {
@@ -496,10 +587,17 @@ static void jacobian_gram_tiles(snk_dqn m, snk_replay rb, int64_t n, float *G_de
         qnet_jacobian(L, m->theta_q, m->wt_q, src_replay(R, m->jidx, 0), R.act, m->jidx, n, m->jw, m->jact, m->jbuf,
                       Kc, false, s, ms_out ? ev[1] : nullptr);
         if (ms_out) SNK_HIP(hipEventRecord(ev[2], s));
+        // round 6 (SNK_ARITH_SYRK_KSPLIT, default): the conv-column Gram on syrk_h3k_kernel
+        // (256 x 256 tiles, fp32 partial Grams per chunk of SK_CHUNK stages), then the
+        // Dense-section pass STORES its terms into G's lower triangle and syrk_ksum_kernel
+        // adds the chunk sums (fp64) to them and writes both triangles (no mirror pass);
+        // 0: the round-5 syrk_h3q_kernel, the Dense terms added into G, then the mirror
+        const bool ksplit = arith(SNK_ARITH_SYRK_KSPLIT) != 0;
         SyrkArgs a{};
         a.x = m->jbuf; a.ld = Kc; a.K = Kc; a.kchunk = Kc; a.N = (int)n; a.g32 = G_dev; a.ldg = n;
+        int64_t ldh = 0;
         {   // h3 Gram: rows pre-split once into scaled fp16 planes (snk_syrk.hpp h3_rows_kernel)
-            const int64_t ldh = (Kc + SY_KS - 1) / SY_KS * SY_KS;
+            ldh = (Kc + SY_KS - 1) / SY_KS * SY_KS;
             const int64_t npad = (n + SW_ROWS_B - 1) / SW_ROWS_B * SW_ROWS_B;   // zero rows past n (whole row blocks)
             if (2 * npad * ldh > m->jplanes_halves) {
                 (void)hipStreamSynchronize(s);
@@ -519,7 +617,31 @@ static void jacobian_gram_tiles(snk_dqn m, snk_replay rb, int64_t n, float *G_de
             launch_check("h3_rows_kernel");
             a.xh = m->jplanes; a.xe = m->jexp; a.ldh = ldh;
         }
-        syrk_launch(SYRK_F32, a, 1, s, rank, nranks);
+        int64_t u0 = 0, u1 = 0;
+        const KSplitTables *kt = nullptr;
+        if (ksplit) {
+            gram256_range(n, rank, nranks, u0, u1);
+            const int nst = (int)(ldh / SY_KS);
+            kt = &ksplit_tables(n, u0, u1, nst, SK_CHUNK);
+            const int64_t ntl = u1 - u0, S = ceil_div(nst, SK_CHUNK), need = S * ntl * SK_T * SK_T;
+            if (need > m->gpart_floats) {
+                (void)hipStreamSynchronize(s);
+                dfree(m->gpart);
+                m->gpart = dalloc<float>(need);
+                m->gpart_floats = need;
+            }
+            if (kt->nitems) {
+                SNK_CHECK(kt->nitems < (int64_t)1 << 31, SNK_ERR_INVALID, "syrk: problem too large");
+                SNK_CHECK((int64_t)SK_T * 2 * ldh * 2 < (int64_t)1 << 31, SNK_ERR_INVALID, "syrk: rows too long");
+                SyrkKArgs k{};
+                k.xh = m->jplanes; k.ldh = ldh; k.nst = nst; k.cs = SK_CHUNK; k.items = kt->items; k.part = m->gpart;
+                k.ntl = ntl;
+                syrk_h3k_kernel<<<(unsigned)kt->nitems, 512, 0, s>>>(k);
+                launch_check("syrk_h3k_kernel");
+            }
+        } else {
+            syrk_launch(SYRK_F32, a, 1, s, rank, nranks);
+        }
         if (ms_out) SNK_HIP(hipEventRecord(ev[3], s));
         {   // Dense-section terms: a3 | dz1 | h1 pre-split into h3 segments, one DENSE h3q pass
             const int64_t st1 = ceil_div(L.K1, SY_KS), st2 = st1 + 64 / SY_KS, ldd = (st2 + 64 / SY_KS) * SY_KS;
@@ -547,10 +669,18 @@ static void jacobian_gram_tiles(snk_dqn m, snk_replay rb, int64_t n, float *G_de
             launch_check("h3_seg_rows_kernel");
             SyrkArgs d{};
             d.xh = m->dplanes; d.xe = m->dexp; d.xes = m->dexp_cap; d.ldh = ldd; d.s1 = (int)st1; d.s2 = (int)st2;
-            d.N = (int)n; d.g32 = G_dev; d.ldg = n; d.act = m->jact;
+            d.N = (int)n; d.g32 = G_dev; d.ldg = n; d.act = m->jact; d.dstore = ksplit ? 1 : 0;
             syrk_dense_launch(d, s, rank, nranks);
         }
-        if (nranks == 1) {
+        if (ksplit) {
+            if (u1 > u0) {
+                SyrkSumArgs q{};
+                q.part = m->gpart; q.S = (int)ceil_div(ldh / SY_KS, SK_CHUNK); q.ntl = u1 - u0; q.tiles = kt->tiles;
+                q.xe = m->jexp; q.N = (int)n; q.G = G_dev; q.ldg = n; q.dense = 1;
+                syrk_ksum_kernel<<<(unsigned)((u1 - u0) * 8), 256, 0, s>>>(q);
+                launch_check("syrk_ksum_kernel");
+            }
+        } else if (nranks == 1) {
             const unsigned nb = (unsigned)ceil_div(n, 64);
             mirror_kernel<<<dim3(nb, nb), 256, 0, s>>>(G_dev, (int)n, n);
             launch_check("mirror_kernel");

@@ -1053,7 +1053,7 @@ static void forward_layers(const QLayout &L, const FwdNet *net, int ng, int64_t 
                 const int nkk = L.Wo * L.Wo;
                 w3_split_kernel<<<W3S_BLOCKS + W2S_BLOCKS + (dh3prep ? w1s_blocks(nkk) : 0), 256, 0, s>>>(
                     img, w.wmax_part, w.wmax_n, w.w3h, w.w3e, n.wt + L.off_t2, w.w2h, dh3prep ? n.wt + L.off_td : nullptr,
-                    w.w1h, w.w1e);
+                    w.w1h, w.w1e, w.split_grow);
                 launch_check("w3_split_kernel");
             }
             if (lo <= 2 && hi >= 1) {

@@ -75,6 +75,9 @@ struct QWork {
     int split_fresh = 0;             // set by the trainer: w3h / w2h / w1h were written by the grad_update that
                                      //   last changed the image (UpdateTarget::s_*): the next act forward skips
                                      //   w3_split_kernel (reset there)
+    float split_grow = 0.0f;         // set by the trainer: a bound on how far any weight can move before the
+                                     //   next fresh split (the chained RMSProp steps x lr / sqrt(1 - rho), x2):
+                                     //   w3_split_kernel caps its exponents so the chained splits cannot overflow
     uint16_t *w3h = nullptr;         // h3 conv3 weights pre-split for conv_h3f_kernel's LDS-DMA staging:
     int *w3e = nullptr;              //   [36 kk][512 16-byte chunks] in the B buffers' swizzled order, and their exponent
     uint16_t *w2h = nullptr;         //   (w3e[1]: conv2's) and conv2's weights pre-split into the B2 image bytes

@@ -7,6 +7,8 @@
 #include <mutex>
 #include <string>
 
+#include <atomic>
+
 #include "snk_internal.hpp"
 
 namespace snk {
@@ -15,7 +17,8 @@ static thread_local std::string g_err;
 static thread_local hipStream_t g_user_stream = nullptr;
 static thread_local bool g_user_stream_set = false;
 // snk_set_arith knobs, production defaults (SNK_ARITH_* in include/snakehip.h)
-static int g_arith[SNK_ARITH_COUNT] = {1, 1, 1, 1, 0, 0, 1, 1, 1};
+// (relaxed atomics: a knob set on one thread while another launches is not a data race)
+static std::atomic<int> g_arith[SNK_ARITH_COUNT] = {1, 1, 1, 1, 0, 0, 1, 1, 1, 1};
 static hipStream_t g_own_stream[64] = {};
 
 void set_error(const char *fmt, ...) {
@@ -53,7 +56,7 @@ int cu_count() {
     return n;
 }
 
-int arith(int knob) { return g_arith[knob]; }
+int arith(int knob) { return g_arith[knob].load(std::memory_order_relaxed); }
 
 hipStream_t stream() {
     if (g_user_stream_set) return g_user_stream;
@@ -200,14 +203,14 @@ extern "C" int snk_set_arith(int32_t knob, int32_t value) {
         SNK_CHECK(knob >= 0 && knob < SNK_ARITH_COUNT, SNK_ERR_INVALID, "unknown arithmetic knob %d", knob);
         SNK_CHECK(value == 0 || value == 1, SNK_ERR_INVALID, "arithmetic knob %d: value %d is not 0 or 1", knob,
                   value);
-        g_arith[knob] = value;
+        g_arith[knob].store(value, std::memory_order_relaxed);
     });
 }
 
 extern "C" int snk_get_arith(int32_t knob, int32_t *value) {
     return guard([&] {
         SNK_CHECK(value && knob >= 0 && knob < SNK_ARITH_COUNT, SNK_ERR_INVALID, "unknown arithmetic knob %d", knob);
-        *value = g_arith[knob];
+        *value = g_arith[knob].load(std::memory_order_relaxed);
     });
 }
 

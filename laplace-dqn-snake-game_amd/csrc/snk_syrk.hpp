@@ -232,6 +232,7 @@ struct SyrkArgs {
     // row exponent xe[seg * xes + row] (h3_seg_rows_kernel)
     int s1, s2;
     int64_t xes;
+    int dstore;              // DENSE: store the terms into G (syrk_ksum_kernel adds the conv Gram) instead of adding
 };
 
 // h3 operands for the Gram (snk_conv_h3.hpp's split, one scale per ROW):
@@ -800,7 +801,7 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
                     double v = (double)pd[i][j][e];
                     if (a.act[row] == ac) v += (double)__builtin_ldexpf(acc[i][j][e], -(rowe(2, i, e) + ec)) + 1.0;
                     float *o = a.g32 + (int64_t)row * a.ldg + col;
-                    *o = (float)((double)*o + v);
+                    *o = a.dstore ? (float)v : (float)((double)*o + v);
                 }
         }
         return;
@@ -825,6 +826,271 @@ __global__ __launch_bounds__(512) void syrk_h3q_kernel(SyrkArgs a) {
                 a.g32[(int64_t)row * a.ldg + col] = (float)__builtin_ldexp(accd[i][j][e], -(a.xe[row] + a.xe[col]));
             }
         }
+}
+
+// ---------------------------------------------------------------------------
+// syrk_h3k_kernel (round 6, the production conv-column Gram): 256 x 256
+// lower-triangle tiles with the reduction split into chunks of cs stages.
+//
+// Why: the 128 x 128 kernel above is bound by its stage stream (32 KB of
+// L2 -> LDS bytes per 192 MFMAs; without its MFMAs it runs as long as with
+// them), and its fp64 flush accumulators (64 registers) are what
+// kept a bigger tile from fitting two waves per SIMD. A 256 x 256 tile moves
+// 64 KB per 768 MFMAs (half the bytes per MFMA) and each wave's 128 x 64 block
+// reads a quarter KB of fragments per MFMA (half again). Accumulating in fp32
+// only, a chunk of cs stages is a cs-long fp32 dot product; the chunks' fp32
+// partial tiles go to `part` and syrk_ksum_kernel sums them in fp64, so the
+// error is that of cs-stage fp32 sums added in fp64 (chunks of 320 stages:
+// ~1/8 of a one-chunk fp32 sum's error).
+//
+// Workgroup = (tile, chunk) from the host-built item table (I, J, z, local tile);
+// 8 waves, wave w owns rows 128 (w >> 2) .. +127 and columns 64 (w & 3) .. +63
+// of the tile: 8 x 4 MFMA tiles of 16 x 16 (128 fp32 accumulators). Two stage
+// buffers [operand][plane][256 rows][32 halves] (64 KB each, the 16-byte chunk of
+// row r at slot chunk ^ syrk_swz16(r), lane-linear LDS-DMA destinations as in
+// syrk_h3q_kernel: 8 pieces of 16 rows x 64 B per wave and stage). Per step the
+// four row-tile pairs' MFMAs run in groups of 24 with the next pair's fragments
+// read under them; before the last group every wave has its fragments in
+// registers, so the barrier that certifies stage st+1 also frees stage st's
+// buffer for the DMA of st+2 (one barrier per stage, one stage in flight).
+// The partial tile is stored in the accumulators' own order (one 1 KB
+// dwordx4 store per MFMA tile): part[((z * ntl + tile) * 8 + wave) * 8192 +
+// (4 i + j) * 256 + 4 lane + e].
+constexpr int SK_T = 256;                           // tile side
+constexpr int SK_STG = 2 * 2 * SK_T * SH_ROW;       // halves per stage buffer (64 KB)
+constexpr int SK_SUB = 128 * 64;                    // floats of one wave's block
+constexpr int SK_CHUNK = 160;                       // stages per chunk (5,120 k)
+
+struct SyrkKArgs {
+    const uint16_t *xh;     // h3 row planes [npad][ldh / 32][2][32] (h3_rows_kernel), npad % 256 == 0
+    int64_t ldh;
+    int nst;                // stages of the whole reduction (ldh / 32)
+    int cs;                 // stages per chunk: chunk z = stages [z cs, min(nst, (z + 1) cs))
+    const int4 *items;      // per workgroup: (I, J, z, local tile)
+    float *part;            // partial tiles (layout above)
+    int64_t ntl;            // tiles of this launch
+    uint64_t *stamps;       // measurement builds (SNK_SYRK_MEASURE): 4 words per workgroup
+};
+
+__global__ __launch_bounds__(512) void syrk_h3k_kernel(SyrkKArgs a) {
+    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * SK_STG];   // 128 KB
+#ifdef SNK_SYRK_MEASURE
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[4 * blockIdx.x] = __builtin_amdgcn_s_memtime();
+        a.stamps[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+    const int4 it = a.items[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int wr = (wave >> 2) * 128, wc = (wave & 3) * 64;
+    const int s0 = it.z * a.cs, nst = min(a.nst - s0, a.cs);
+    // DMA: wave w moves operand w >> 2, plane (w >> 1) & 1, rows 128 (w & 1) .. +127 as 8
+    // pieces of 16 rows, through one buffer descriptor on its operand's 256-row panel: the
+    // lane's part of the source (row 128 (w & 1) + (lane >> 2) of the piece and its swizzled
+    // chunk; the swizzle does not depend on the piece) is one 32-bit offset, the piece and
+    // stage part a scalar offset, so no 64-bit address per piece stays live across the loop
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int op = wv >> 2, pl = (wv >> 1) & 1;
+    const uint32_t rowb = (uint32_t)(2 * a.ldh * 2);   // bytes per plane row
+    const int drow = 128 * (wv & 1) + (lane >> 2);
+    const uint32_t voff = (uint32_t)drow * rowb + (uint32_t)(pl * SY_KS * 2) +
+                          (uint32_t)(((lane & 3) ^ syrk_swz16(drow)) * 16) + (uint32_t)s0 * (2 * SY_KS * 2);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.xh + (int64_t)(op ? it.y : it.x) * SK_T * 2 * a.ldh), 0, (int)(SK_T * rowb), 0x00020000);
+    const int ddst = ((op * 2 + pl) * SK_T + 128 * (wv & 1)) * SH_ROW;
+    auto dma = [&](int st, int buf) __attribute__((always_inline)) {
+        const uint32_t kb = (uint32_t)st * (2 * SY_KS * 2);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void *)(lds + buf * SK_STG + ddst + q * 16 * SH_ROW), 16, voff,
+                (uint32_t)(q * 16) * rowb + kb, 0, 0);
+    };
+    typedef f16x8 F2[2][2];   // [tile][plane]
+    auto frag_a = [&](int buf, int t0, F2 &f) __attribute__((always_inline)) {
+        const uint16_t *base = lds + buf * SK_STG;
+#pragma unroll
+        for (int pn = 0; pn < 2; ++pn)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int row = wr + 16 * (t0 + i) + r;
+                f[i][pn] = as_h(*reinterpret_cast<const u32x4 *>(base + (pn * SK_T + row) * SH_ROW +
+                                                                 8 * (g ^ syrk_swz16(row))));
+            }
+    };
+    auto frag_b = [&](int buf, int j0, F2 &f) __attribute__((always_inline)) {
+        const uint16_t *base = lds + buf * SK_STG;
+#pragma unroll
+        for (int pn = 0; pn < 2; ++pn)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = wc + 16 * (j0 + j) + r;
+                f[j][pn] = as_h(*reinterpret_cast<const u32x4 *>(base + ((2 + pn) * SK_T + row) * SH_ROW +
+                                                                 8 * (g ^ syrk_swz16(row))));
+            }
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // row tiles t0, t0+1 x column tiles j0, j0+1: the l*h products, then h*l, then h*h (the
+    // same order for every element: a tile's values do not depend on its position); part
+    // 0: the first MFMA only, 1: the other 11, 2: all 12
+    auto mfma4 = [&](const F2 &fa, const F2 &fb, int t0, int j0, int part) __attribute__((always_inline)) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const bool first = p == 0 && ii == 0 && jj == 0;
+                    if (part == 0 && !first) continue;
+                    if (part == 1 && first) continue;
+                    acc[t0 + ii][j0 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                        p == 0 ? fa[ii][1] : fa[ii][0], p == 1 ? fb[jj][1] : fb[jj][0], acc[t0 + ii][j0 + jj], 0, 0, 0);
+                }
+    };
+    F2 fa0, fa1, fb0, fb1;   // A row-tile pairs (alternating), B column tiles 0-1 and 2-3
+    // prologue: stage 0 landed everywhere, stage 1 in flight, stage 0's first fragments read
+    dma(0, 0);
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    __builtin_amdgcn_s_barrier();
+    if (nst > 1) dma(1, 1);
+    frag_a(0, 0, fa0);
+    frag_b(0, 0, fb0);
+    frag_b(0, 2, fb1);
+    // one row-tile pair's 24 MFMAs with the next pair's fragments read after the first
+    // (ROCm's waitcnt pass drains lgkmcnt before the first MFMA of a block of them)
+    auto group = [&](const F2 &fa, int t0, auto rd) __attribute__((always_inline)) {
+        mfma4(fa, fb0, t0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        rd();
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(fa, fb0, t0, 0, 1);
+        mfma4(fa, fb1, t0, 2, 2);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto step = [&](int st, auto bc) __attribute__((always_inline)) {
+        constexpr int B = decltype(bc)::value;
+        const bool more = st + 1 < nst;
+        group(fa0, 0, [&]() __attribute__((always_inline)) { frag_a(B, 2, fa1); });
+        group(fa1, 2, [&]() __attribute__((always_inline)) { frag_a(B, 4, fa0); });
+        group(fa0, 4, [&]() __attribute__((always_inline)) { frag_a(B, 6, fa1); });
+        // every wave's reads of this buffer are in registers and stage st+1 landed
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 2 < nst) dma(st + 2, B);
+        __builtin_amdgcn_sched_barrier(0);
+        // the last pair: its column tiles 0-1, then 2-3, each B half refilled from stage
+        // st+1 right after its last MFMA of this stage
+        mfma4(fa1, fb0, 6, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) frag_a(B ^ 1, 0, fa0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(fa1, fb0, 6, 0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) frag_b(B ^ 1, 0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma4(fa1, fb1, 6, 2, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) frag_b(B ^ 1, 2, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    int st = 0;
+    for (; st + 2 <= nst; st += 2) {
+        step(st, std::integral_constant<int, 0>{});
+        step(st + 1, std::integral_constant<int, 1>{});
+    }
+    if (st < nst) step(st, std::integral_constant<int, 0>{});
+#ifdef SNK_SYRK_MEASURE
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
+        a.stamps[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+    float *o = a.part + (((int64_t)it.z * a.ntl + it.w) * 8 + wave) * SK_SUB + 4 * lane;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4 *>(o + (4 * i + j) * 256) = acc[i][j];
+}
+
+// G from syrk_h3k_kernel's partial tiles: one workgroup per wave block (128 x 64) of a
+// tile. The S chunk partials are summed in fp64 in chunk order, scaled by
+// 2^-(e_row + e_col), plus (dense) the Dense-section terms syrk_h3q_kernel<0, 4, true>
+// stored in G's lower triangle, rounded once to fp32 and written to G[row][col] and
+// G[col][row] (the mirror: G is exactly symmetric). Only row >= col is taken from a
+// diagonal tile (its upper half computed the same sums in the other operand order).
+struct SyrkSumArgs {
+    const float *part;
+    int S;
+    int64_t ntl;
+    const int2 *tiles;      // the launch's tiles (I, J) by local index
+    const int32_t *xe;
+    int N;
+    float *G;
+    int64_t ldg;
+    int dense;
+};
+
+__global__ __launch_bounds__(256) void syrk_ksum_kernel(SyrkSumArgs a) {
+    __shared__ double sv[128][65];
+    const int t = (int)(blockIdx.x >> 3), w = (int)(blockIdx.x & 7);
+    const int2 tb = a.tiles[t];
+    const int r0 = tb.x * SK_T + (w >> 2) * 128, c0 = tb.y * SK_T + (w & 3) * 64;
+    if (r0 + 127 < c0 || r0 >= a.N || c0 >= a.N) return;   // nothing of the lower triangle
+    const int tid = threadIdx.x, N = a.N;
+    double s[8][4];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[m][e] = 0.0;
+    for (int z = 0; z < a.S; ++z) {
+        const f32x4 *p = reinterpret_cast<const f32x4 *>(a.part + (((int64_t)z * a.ntl + t) * 8 + w) * SK_SUB);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const f32x4 v = p[tid + 256 * m];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[m][e] += (double)v[e];
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int q = tid + 256 * m, ij = q >> 6, ln = q & 63;
+        const int cl = 16 * (ij & 3) + (ln & 15), ec = a.xe[min(c0 + cl, N - 1)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int rl = 16 * (ij >> 2) + 4 * (ln >> 4) + e;
+            sv[rl][cl] = __builtin_ldexp(s[m][e], -(a.xe[min(r0 + rl, N - 1)] + ec));
+        }
+    }
+    __syncthreads();
+    {   // lower: a wave stores 64 consecutive columns of a row
+        const int cl = tid & 63, col = c0 + cl;
+        for (int rl = tid >> 6; rl < 128; rl += 4) {
+            const int row = r0 + rl;
+            if (row >= N || col >= N || col > row) continue;
+            float *p = a.G + (int64_t)row * a.ldg + col;
+            double v = sv[rl][cl];
+            if (a.dense) v += (double)*p;
+            const float f = (float)v;
+            *p = f;
+            sv[rl][cl] = (double)f;
+        }
+    }
+    __syncthreads();
+    {   // upper: a wave stores 64 consecutive columns (the block's rows) of row `col`
+        const int rl = tid & 127, row = r0 + rl;
+        for (int cl = tid >> 7; cl < 64; cl += 2) {
+            const int col = c0 + cl;
+            if (row >= N || col >= N || col >= row) continue;
+            a.G[(int64_t)col * a.ldg + row] = (float)sv[rl][cl];
+        }
+    }
 }
 
 #ifdef SNK_SYRK_MEASURE

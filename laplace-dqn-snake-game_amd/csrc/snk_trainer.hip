@@ -11,6 +11,7 @@
 // epsilon) lives in device memory, so an iteration is a fixed launch sequence
 // that is captured once into a hipGraph and replayed.
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "snk_dqn.hpp"
@@ -60,11 +61,13 @@ struct snk_trainer_s {
     // through device counters, so a longer graph is the same launch sequence with the
     // per-graph launch gap and the first iteration's weight-max scan paid once per graph):
     // n = `unroll`, and n = the remainder of a run that is not a multiple of it (one graph
-    // for the tail instead of one single-iteration graph per leftover iteration; only the
-    // most recent tail length stays cached per learn mode, see snk_trainer_run)
-    static constexpr int MAXG = 64;
+    // for the tail instead of one single-iteration graph per leftover iteration; the
+    // TAILS most recently used tail lengths stay cached per learn mode, see snk_trainer_run)
+    static constexpr int MAXG = 64, TAILS = 3;
     hipGraph_t graph[2][MAXG + 1] = {};
     hipGraphExec_t exec[2][MAXG + 1] = {};
+    int64_t used[2][MAXG + 1] = {};   // last use (use_clock) of each cached graph
+    int64_t use_clock = 0;
     int unroll = 8;
     int64_t ws_gen = 0;   // dqn workspace generation the graphs were captured against
     // snk_trainer_set_trace: every update's finished gradient is also copied to
@@ -115,6 +118,10 @@ static void trainer_iteration(snk_trainer_s *h, bool learn, int n_upd, hipStream
     const bool ride = upd && h->B <= 64;
     if (chain) q->act.wmax_fresh = 1;
     if (split) q->act.split_fresh = 1;
+    // a fresh split followed by chained ones: bound the weights' movement until the next fresh
+    // split (at most `unroll` iterations of n_upd RMSProp steps) for its exponents
+    q->act.split_grow = next_split ? (float)(2.0 * h->unroll * n_upd * (double)q->lr / std::sqrt(1.0 - (double)q->rho))
+                                   : 0.0f;
     HeadArgs ha;
     SampleRider rider;
     if (ride) {
@@ -347,17 +354,21 @@ extern "C" int snk_trainer_run(snk_trainer h, int64_t iters, int32_t learn, int3
         const int g = learn ? 1 : 0;
         const int U = h->unroll;
         auto capture = [&](int n) {   // the n-iteration graph, captured once
+            h->used[g][n] = ++h->use_clock;
             if (h->exec[g][n]) return h->exec[g][n];
-            if (n != U) {   // a new tail length: drop the previous tail graph (each holds n iterations)
-                bool sync = false;
+            if (n != U) {   // a new tail length: keep the TAILS - 1 most recently used other tails
+                int cached = 0, lru = 0;
                 for (int m = 1; m <= snk_trainer_s::MAXG; ++m) {
-                    if (m == U || !h->exec[g][m]) continue;
-                    if (!sync) SNK_HIP(hipStreamSynchronize(s));
-                    sync = true;
-                    (void)hipGraphExecDestroy(h->exec[g][m]);
-                    (void)hipGraphDestroy(h->graph[g][m]);
-                    h->exec[g][m] = nullptr;
-                    h->graph[g][m] = nullptr;
+                    if (m == U || m == n || !h->exec[g][m]) continue;
+                    ++cached;
+                    if (!lru || h->used[g][m] < h->used[g][lru]) lru = m;
+                }
+                if (cached >= snk_trainer_s::TAILS) {   // evict the least recently used one (each holds m iterations)
+                    SNK_HIP(hipStreamSynchronize(s));
+                    (void)hipGraphExecDestroy(h->exec[g][lru]);
+                    (void)hipGraphDestroy(h->graph[g][lru]);
+                    h->exec[g][lru] = nullptr;
+                    h->graph[g][lru] = nullptr;
                 }
             }
             SNK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));

@@ -58,6 +58,13 @@ class Comm:
     def handle(self):
         return self._h
 
+    def info(self) -> tuple[int, int]:
+        """(ranks, rank) as RCCL reports them for this communicator (ncclCommCount,
+        ncclCommUserRank)."""
+        n, r = C.c_int32(0), C.c_int32(0)
+        call("snk_comm_info", self._h, C.byref(n), C.byref(r))
+        return n.value, r.value
+
     def allreduce_mean(self, dev_ptr: int, n: int) -> None:
         call("snk_comm_allreduce_mean", self._h, vp(dev_ptr), n)
 

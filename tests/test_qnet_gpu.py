@@ -228,6 +228,24 @@ def test_trainer_schedule_and_graph_determinism(snk):
     assert s0["env_steps"] >= 1001 and s0["episodes"] > 0
 
 
+def test_trainer_alternating_tail_graphs_match_eager(snk):
+    """run() lengths that leave alternating remainders (graph_unroll 4: 3, 5 -> 4 + 1,
+    3, 2, 6 -> 4 + 2, 3, 1) replay cached tail graphs (the 3 most recently used per learn mode)
+    and capture new ones as they come; every iteration equals the eager launch sequence bit for
+    bit (both nets, losses, counters)."""
+    outs = []
+    for graph in (False, True):
+        tr = snk.Trainer(n_envs=128, board_size=12, n_frames=2, capacity=2000, batch_size=64, n_batches=10_000,
+                         target_update_rate=5, decay=1e-3, seed=78, graph_unroll=4)
+        snk.fill_buffer_(tr, graph=graph)
+        for it in (3, 5, 3, 2, 6, 3, 1, 2, 3):
+            tr.run(it, learn=True, graph=graph)
+        outs.append((tr.model.get_params(), tr.model.get_params(snk.SNK_NET_TARGET), np.array(tr.losses)))
+    for x, y in zip(*outs):
+        assert np.array_equal(x, y)
+    assert outs[0][2].size == 28 and np.isfinite(outs[0][2]).all()
+
+
 @pytest.mark.parametrize("bs,C,B", [(12, 2, 300), (10, 1, 257)])
 def test_x6_split_forward_matches_fp32_and_oracle(snk, bs, C, B):
     """The bf16x6 split-precision forward (default) has the error class of the
@@ -511,3 +529,45 @@ def test_split_chain_matches_fresh_splits(snk):
                             tr.model.get_params(snk.SNK_NET_TARGET))
     for x, y in zip(res[True], res[False]):
         assert np.array_equal(x, y)
+
+
+def test_split_chain_exponent_cap_keeps_q_finite(snk):
+    """a chained split reuses the exponents of the graph's first w3_split_kernel, and
+    RMSProp moves a weight by up to lr / sqrt(1 - rho) per step whatever its size, so a tensor (or
+    Dense1 row) with a tiny maximum would grow past the fp16 range of its split within a graph.
+    w3_split_kernel caps the exponents with the trainer's bound on that movement
+    (snk_conv_h3f.hpp h3_exp_w). Here conv3's whole tensor and one Dense1 row start at 1e-3 of
+    their glorot scale (maxima ~1e-4, 30x growth after two steps): 16 captured iterations
+    with learning must keep every Q-value, loss and weight finite, and the chained run must
+    match fresh splits every iteration (split_chain=False) to the h3 error class."""
+    n, U = 4096, 16
+    res = {}
+    for chained in (True, False):
+        with snk.arith(split_chain=chained):
+            tr = snk.Trainer(n_envs=n, board_size=12, n_frames=2, capacity=20_000, batch_size=64, n_batches=10_000,
+                             epsilon=0.05, epsilon_end=0.05, decay=0.0, seed=0x5D, graph_unroll=U)
+            snk.fill_buffer_(tr, graph=True)
+            th = tr.model.get_params()
+            c3 = (9 * 2 * 16 + 16) + (9 * 16 * 32 + 32)        # conv3 weights (Flux order)
+            d1 = c3 + 36 * 32 * 64 + 64                        # Dense1 W (64 x 3136, column-major)
+            th[c3:c3 + 36 * 32 * 64] *= 1e-3
+            th[d1:d1 + 64 * 3136:64] *= 1e-3                   # row (output) 0
+            m_row0 = float(np.abs(th[d1:d1 + 64 * 3136:64]).max())
+            tr.model.set_params(th)
+            tr.model.set_params(th, snk.SNK_NET_TARGET)
+            acts = snk.DeviceArray.from_host(np.zeros((U, n), np.uint8))
+            qs = snk.DeviceArray.from_host(np.zeros((U, n, 3), np.float32))
+            tr.set_act_trace(acts, qs)
+            tr.run(U, learn=True, graph=True)
+            res[chained] = (acts.numpy(), qs.numpy(), np.array(tr.losses), tr.model.get_params())
+    a, q, loss, th = res[True]
+    assert np.isfinite(q).all() and np.isfinite(loss).all() and np.isfinite(th).all()
+    # the scenario happened: the row grew far past the 32x its split's headroom alone allows
+    assert np.abs(th[d1:d1 + 64 * 3136:64]).max() > 32 * m_row0
+    # the same trajectory while the actions agree (the capped exponents change only the split's
+    # 2^-22 representation error)
+    a2, q2, _, _ = res[False]
+    for t in range(U):
+        np.testing.assert_allclose(q[t], q2[t], rtol=1e-4, atol=1e-6 * np.abs(q2[t]).max())
+        if not np.array_equal(a[t], a2[t]):
+            break
