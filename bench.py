@@ -494,6 +494,7 @@ def d_build(args, snk, tr) -> dict:
         lap.fit_center()
         _lib.call("snk_synchronize")
         t_fit = time.perf_counter() - t0
+        lap.gram()                                       # first call: allocates the partial tiles
         t0 = time.perf_counter()
         _, gms = lap.gram()
         t_gram = time.perf_counter() - t0
@@ -521,11 +522,21 @@ def d_build(args, snk, tr) -> dict:
                                    "weight_stream_GBs": msteps * wbytes / t_ls / 1e9,
                                    "weight_stream_frac_hbm": msteps * wbytes / t_ls / 1e9 / PEAK_HBM_GBS}
         del lap58
+        ks = snk.get_arith("syrk_ksplit")
         res["snapshot_gram"] = {"kind": "compute_D.jl D (P x K Float64 snapshots) -> Welford, centre, G = D'D",
                                 "K": K, "n_params": P, "welford_center_ms": 1e3 * t_fit,
-                                "welford_center_GBs": 28.0 * K * P / t_fit / 1e9,
+                                # Welford reads D; the centring reads and writes D and writes the fp32
+                                # copy (and, k-split, its fp16 h / l planes)
+                                "welford_center_GBs": (32.0 if ks else 28.0) * K * P / t_fit / 1e9,
+                                "gram_kernel": ("syrk_h3k_kernel: fp16 h3 split (one exponent per row and "
+                                                "1024-column chunk) on v_mfma_f32_16x16x32_f16, 256 x 256 tiles, "
+                                                "fp32 chunk partials summed in fp64 by syrk_ksum_kernel (in "
+                                                "gram_total_ms, not in gram_kernel_ms)" if ks else
+                                                "syrk_slab_kernel: bf16 x6 split, fp64 slabs"),
                                 "gram_kernel_ms": gms, "gram_total_ms": 1e3 * t_gram,
-                                "gram_tflops": fl / (gms * 1e-3) / 1e12}
+                                "gram_tflops": fl / (gms * 1e-3) / 1e12,
+                                "gram_frac_peak": fl / (gms * 1e-3) / 1e12 / (PEAK_BF16_TFLOPS / (H3_PRODUCTS if ks
+                                                                                                   else X6_PRODUCTS))}
     return res
 
 

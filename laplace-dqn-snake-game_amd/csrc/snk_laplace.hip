@@ -30,6 +30,15 @@ struct snk_laplace_s {
     double *D = nullptr, *mean = nullptr, *var = nullptr, *G = nullptr, *slab = nullptr;
     float *D32 = nullptr;
     int64_t slab_cap = 0;
+    // the K-split h3 snapshot Gram (SNK_ARITH_SYRK_KSPLIT): the centred rows split by
+    // lap_center_split_kernel (valid after a fit_center that made them), their per-chunk
+    // exponents, and syrk_h3k_kernel's partial tiles
+    uint16_t *planes = nullptr;
+    int32_t *pexp = nullptr;
+    int64_t ldh = 0;
+    int planes_valid = 0;
+    float *gpart = nullptr;
+    int64_t gpart_floats = 0;
 };
 
 namespace snk {
@@ -84,6 +93,50 @@ __global__ void lap_center_kernel(double *__restrict__ D, int64_t P, int K, cons
         }
         D32[t] = v;
     }
+}
+
+// compute_D.jl:80-81 D .-= mean with lap_center_kernel's arithmetic (bit for bit), fused
+// with the fp32 copy and its h3 split for the K-split snapshot Gram (syrk_h3k_kernel): one
+// workgroup per (snapshot row, chunk of LAP_CS stages = 1024 columns); the chunk's own
+// power-of-two exponent xe[chunk * xes + row] from its max |c| (scales factor out of each
+// chunk's partial Gram, syrk_ksum_kernel applies them per chunk). Rows are split as the
+// fp32 values D32 holds. 4 more bytes per entry than the plain centring (the planes).
+constexpr int LAP_CS = 32;
+__global__ __launch_bounds__(256) void lap_center_split_kernel(double *__restrict__ D, int64_t P, int K,
+                                                               const double *__restrict__ mean, float *__restrict__ D32,
+                                                               int64_t ld32, uint16_t *__restrict__ planes, int64_t ldh,
+                                                               int32_t *__restrict__ xe, int64_t xes) {
+    constexpr int CW = LAP_CS * SY_KS;   // 1024 columns
+    __shared__ __attribute__((aligned(16))) float cs[CW];
+    __shared__ float red4[4];
+    const int k = blockIdx.y, tid = threadIdx.x;
+    const int64_t z = blockIdx.x, p0 = z * CW;
+    float m = 0.0f;
+#pragma unroll
+    for (int i = 0; i < CW / 256; ++i) {   // coalesced: consecutive lanes, consecutive columns
+        const int64_t p = p0 + tid + 256 * i;
+        float v = 0.0f;
+        if (p < P) {
+            const double cc = D[(int64_t)k * P + p] - mean[p];
+            D[(int64_t)k * P + p] = cc;
+            v = (float)cc;
+        }
+        if (p < ld32) D32[(int64_t)k * ld32 + p] = v;
+        cs[tid + 256 * i] = v;
+        m = fmaxf(m, fabsf(v));
+    }
+    m = wave_max(m);
+    if ((tid & 63) == 0) red4[tid >> 6] = m;
+    __syncthreads();
+    const int e = h3_exp(fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3])));
+    if (tid == 0) xe[z * xes + k] = e;
+    const f32x4 c = *reinterpret_cast<const f32x4 *>(&cs[4 * tid]);   // columns 4 tid .. +3
+    u32x2 h, l;
+    h3_split4(c, e, h, l);
+    u32x2 *o = reinterpret_cast<u32x2 *>(planes + (int64_t)k * 2 * ldh + z * 2 * CW);
+    const int q = (tid >> 3) * 16 + (tid & 7);   // stage tid / 8, 4-half piece tid % 8
+    o[q] = h;
+    o[q + 8] = l;
 }
 
 // sum the K-split partial Grams (lower triangle) in split order; write both triangles
@@ -430,7 +483,8 @@ extern "C" int snk_laplace_destroy(snk_laplace h) {
     return guard([&] {
         if (!h) return;
         (void)hipStreamSynchronize(stream());
-        for (void *p : {(void *)h->D, (void *)h->mean, (void *)h->var, (void *)h->G, (void *)h->slab, (void *)h->D32})
+        for (void *p : {(void *)h->D, (void *)h->mean, (void *)h->var, (void *)h->G, (void *)h->slab, (void *)h->D32,
+                        (void *)h->planes, (void *)h->pexp, (void *)h->gpart})
             dfree(p);
         delete h;
     });
@@ -496,9 +550,29 @@ extern "C" int snk_laplace_fit_center(snk_laplace h) {
         hipStream_t s = stream();
         lap_welford_kernel<<<ceil_div(h->P, 256), 256, 0, s>>>(h->D, h->P, h->K, h->mean, h->var);
         launch_check("lap_welford_kernel");
-        lap_center_kernel<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)h->K * h->ld32, 256), 16384), 256, 0, s>>>(
-            h->D, h->P, h->K, h->mean, h->D32, h->ld32);
-        launch_check("lap_center_kernel");
+        h->planes_valid = 0;
+        if (arith(SNK_ARITH_SYRK_KSPLIT)) {   // centring + fp32 copy + the h3 planes of the snapshot Gram
+            const int64_t ldh = ceil_div(h->ld32, LAP_CS * SY_KS) * (LAP_CS * SY_KS), kpad = ceil_div(h->K, SK_T) * SK_T;
+            const int64_t nch = ldh / (LAP_CS * SY_KS);
+            SNK_CHECK(nch <= 65535 && h->K <= 65535, SNK_ERR_INVALID, "snapshot Gram too large");
+            if (!h->planes || h->ldh != ldh) {
+                SNK_HIP(hipStreamSynchronize(s));
+                dfree(h->planes);
+                dfree(h->pexp);
+                h->planes = dalloc<uint16_t>(kpad * 2 * ldh);
+                h->pexp = dalloc<int32_t>(nch * h->K);
+                h->ldh = ldh;
+                SNK_HIP(hipMemsetAsync(h->planes, 0, (size_t)kpad * 2 * ldh * 2, s));   // rows K..kpad stay zero
+            }
+            lap_center_split_kernel<<<dim3((unsigned)nch, (unsigned)h->K), 256, 0, s>>>(
+                h->D, h->P, h->K, h->mean, h->D32, h->ld32, h->planes, ldh, h->pexp, h->K);
+            launch_check("lap_center_split_kernel");
+            h->planes_valid = 1;
+        } else {
+            lap_center_kernel<<<(unsigned)std::min<int64_t>(ceil_div((int64_t)h->K * h->ld32, 256), 16384), 256, 0, s>>>(
+                h->D, h->P, h->K, h->mean, h->D32, h->ld32);
+            launch_check("lap_center_kernel");
+        }
     });
 }
 
@@ -506,6 +580,46 @@ extern "C" int snk_laplace_gram(snk_laplace h, float *ms_out) {
     return guard([&] {
         SNK_CHECK(h, SNK_ERR_INVALID, "NULL argument");
         hipStream_t s = stream();
+        if (arith(SNK_ARITH_SYRK_KSPLIT) && h->planes_valid) {
+            // the h3 K-split Gram over the planes fit_center split (chunks of LAP_CS stages, one
+            // exponent per row and chunk), the chunk partials summed in fp64 into G (both triangles)
+            const int nst = (int)(h->ldh / SY_KS), S = nst / LAP_CS;
+            const int64_t T = ceil_div(h->K, SK_T), ntl = T * (T + 1) / 2;
+            const KSplitTables &kt = ksplit_tables(h->K, 0, ntl, nst, LAP_CS);
+            const int64_t need = (int64_t)S * ntl * SK_T * SK_T;
+            if (need > h->gpart_floats) {
+                SNK_HIP(hipStreamSynchronize(s));
+                dfree(h->gpart);
+                h->gpart = dalloc<float>(need);
+                h->gpart_floats = need;
+            }
+            SNK_CHECK(kt.nitems < (int64_t)1 << 31 && (int64_t)SK_T * 2 * h->ldh * 2 < (int64_t)1 << 31,
+                      SNK_ERR_INVALID, "snapshot Gram too large");
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (ms_out) {
+                SNK_HIP(hipEventCreate(&e0));
+                SNK_HIP(hipEventCreate(&e1));
+                SNK_HIP(hipEventRecord(e0, s));
+            }
+            SyrkKArgs k{};
+            k.xh = h->planes; k.ldh = h->ldh; k.nst = nst; k.cs = LAP_CS; k.items = kt.items; k.part = h->gpart;
+            k.ntl = ntl;
+            syrk_h3k_kernel<<<(unsigned)kt.nitems, 512, 0, s>>>(k);
+            launch_check("syrk_h3k_kernel");
+            if (ms_out) SNK_HIP(hipEventRecord(e1, s));
+            SyrkSumArgs<double> q{};
+            q.part = h->gpart; q.S = S; q.ntl = ntl; q.tiles = kt.tiles; q.xe = h->pexp; q.xes = h->K; q.N = h->K;
+            q.G = h->G; q.ldg = h->K; q.dense = 0;
+            syrk_ksum_kernel<double><<<(unsigned)(ntl * 64), 256, 0, s>>>(q);
+            launch_check("syrk_ksum_kernel");
+            if (ms_out) {
+                SNK_HIP(hipEventSynchronize(e1));
+                SNK_HIP(hipEventElapsedTime(ms_out, e0, e1));
+                (void)hipEventDestroy(e0);
+                (void)hipEventDestroy(e1);
+            }
+            return;
+        }
         const int64_t T = ceil_div(h->K, SY_T), tiles = T * (T + 1) / 2;
         // split the P reduction so the launch holds ~2 workgroups per CU
         int z = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(512, tiles), ceil_div(h->ld32, 4096)));
@@ -674,10 +788,10 @@ static void jacobian_gram_tiles(snk_dqn m, snk_replay rb, int64_t n, float *G_de
         }
         if (ksplit) {
             if (u1 > u0) {
-                SyrkSumArgs q{};
+                SyrkSumArgs<float> q{};
                 q.part = m->gpart; q.S = (int)ceil_div(ldh / SY_KS, SK_CHUNK); q.ntl = u1 - u0; q.tiles = kt->tiles;
-                q.xe = m->jexp; q.N = (int)n; q.G = G_dev; q.ldg = n; q.dense = 1;
-                syrk_ksum_kernel<<<(unsigned)((u1 - u0) * 8), 256, 0, s>>>(q);
+                q.xe = m->jexp; q.xes = 0; q.N = (int)n; q.G = G_dev; q.ldg = n; q.dense = 1;
+                syrk_ksum_kernel<float><<<(unsigned)((u1 - u0) * 64), 256, 0, s>>>(q);
                 launch_check("syrk_ksum_kernel");
             }
         } else if (nranks == 1) {

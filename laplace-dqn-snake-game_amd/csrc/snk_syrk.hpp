@@ -1019,77 +1019,83 @@ __global__ __launch_bounds__(512) void syrk_h3k_kernel(SyrkKArgs a) {
         for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4 *>(o + (4 * i + j) * 256) = acc[i][j];
 }
 
-// G from syrk_h3k_kernel's partial tiles: one workgroup per wave block (128 x 64) of a
-// tile. The S chunk partials are summed in fp64 in chunk order, scaled by
-// 2^-(e_row + e_col), plus (dense) the Dense-section terms syrk_h3q_kernel<0, 4, true>
-// stored in G's lower triangle, rounded once to fp32 and written to G[row][col] and
-// G[col][row] (the mirror: G is exactly symmetric). Only row >= col is taken from a
-// diagonal tile (its upper half computed the same sums in the other operand order).
+// G from syrk_h3k_kernel's partial tiles. One workgroup per 4 MFMA tiles (16 x 16) of a wave
+// block, one thread per accumulator lane: its float4 of each chunk (S coalesced 1 KB loads
+// per wave, many workgroups in flight, no LDS) summed in fp64 in chunk order and scaled by
+// 2^-(e_row + e_col) (xes == 0: one exponent per row for every chunk, applied to the sum;
+// xes > 0: chunk z's rows carry exponents xe[z * xes + row], applied per chunk), plus
+// (dense) the Dense-section terms syrk_h3q_kernel<0, 4, true> stored in G's lower
+// triangle, rounded once to OutT and written to G[row][col] and G[col][row] (the mirror: G
+// is exactly symmetric; the lane's 4 rows are 4 consecutive columns of the mirror row). Only
+// row >= col is taken from a diagonal tile (its upper half computed the same sums in the
+// other operand order).
+template <typename OutT>
 struct SyrkSumArgs {
     const float *part;
     int S;
     int64_t ntl;
     const int2 *tiles;      // the launch's tiles (I, J) by local index
     const int32_t *xe;
+    int64_t xes;
     int N;
-    float *G;
+    OutT *G;
     int64_t ldg;
     int dense;
 };
 
-__global__ __launch_bounds__(256) void syrk_ksum_kernel(SyrkSumArgs a) {
-    __shared__ double sv[128][65];
-    const int t = (int)(blockIdx.x >> 3), w = (int)(blockIdx.x & 7);
+template <typename OutT>
+__global__ __launch_bounds__(256) void syrk_ksum_kernel(SyrkSumArgs<OutT> a) {
+    const int64_t b = blockIdx.x;
+    const int t = (int)(b >> 6), w = (int)((b >> 3) & 7), m = (int)(b & 7);
     const int2 tb = a.tiles[t];
-    const int r0 = tb.x * SK_T + (w >> 2) * 128, c0 = tb.y * SK_T + (w & 3) * 64;
-    if (r0 + 127 < c0 || r0 >= a.N || c0 >= a.N) return;   // nothing of the lower triangle
-    const int tid = threadIdx.x, N = a.N;
-    double s[8][4];
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) s[m][e] = 0.0;
+    const int q = 256 * m + threadIdx.x, ij = q >> 6, ln = q & 63;   // float4 q of the wave block
+    const int row0 = tb.x * SK_T + (w >> 2) * 128 + 16 * (ij >> 2) + 4 * (ln >> 4);   // + e
+    const int col = tb.y * SK_T + (w & 3) * 64 + 16 * (ij & 3) + (ln & 15);
+    const int N = a.N;
+    if (row0 + 3 < col || row0 >= N || col >= N) return;   // no lower-triangle element
+    const int rc[4] = {min(row0, N - 1), min(row0 + 1, N - 1), min(row0 + 2, N - 1), min(row0 + 3, N - 1)};
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    const f32x4 *p = reinterpret_cast<const f32x4 *>(a.part + ((int64_t)t * 8 + w) * SK_SUB) + q;
+    const int64_t zst = a.ntl * 8 * (SK_SUB / 4);   // float4 stride between chunks
     for (int z = 0; z < a.S; ++z) {
-        const f32x4 *p = reinterpret_cast<const f32x4 *>(a.part + (((int64_t)z * a.ntl + t) * 8 + w) * SK_SUB);
+        const f32x4 v = p[z * zst];
+        if (a.xes) {
+            const int32_t *xz = a.xe + z * a.xes;
+            const int ec = xz[col];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const f32x4 v = p[tid + 256 * m];
+            for (int e = 0; e < 4; ++e) s[e] += __builtin_ldexp((double)v[e], -(xz[rc[e]] + ec));
+        } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) s[m][e] += (double)v[e];
+            for (int e = 0; e < 4; ++e) s[e] += (double)v[e];
         }
     }
+    OutT f[4];
+    const int ec = a.xes ? 0 : a.xe[col];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const int q = tid + 256 * m, ij = q >> 6, ln = q & 63;
-        const int cl = 16 * (ij & 3) + (ln & 15), ec = a.xe[min(c0 + cl, N - 1)];
+    for (int e = 0; e < 4; ++e) {
+        const int row = row0 + e;
+        double v = a.xes ? s[e] : __builtin_ldexp(s[e], -(a.xe[rc[e]] + ec));
+        f[e] = (OutT)0;
+        if (row >= N || col > row) continue;
+        OutT *g = a.G + (int64_t)row * a.ldg + col;
+        if (a.dense) v += (double)*g;
+        f[e] = (OutT)v;
+        *g = f[e];
+    }
+    // the mirror: G[col][row0 .. row0 + 3], the entries with row > col
+    OutT *u = a.G + (int64_t)col * a.ldg + row0;
+    if (row0 > col && row0 + 3 < N && ((uintptr_t)u % (4 * sizeof(OutT))) == 0) {
+        if constexpr (sizeof(OutT) == 4) {
+            *reinterpret_cast<f32x4 *>(u) = f32x4{(float)f[0], (float)f[1], (float)f[2], (float)f[3]};
+        } else {
+            typedef double f64x2 __attribute__((ext_vector_type(2)));
+            reinterpret_cast<f64x2 *>(u)[0] = f64x2{(double)f[0], (double)f[1]};
+            reinterpret_cast<f64x2 *>(u)[1] = f64x2{(double)f[2], (double)f[3]};
+        }
+    } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int rl = 16 * (ij >> 2) + 4 * (ln >> 4) + e;
-            sv[rl][cl] = __builtin_ldexp(s[m][e], -(a.xe[min(r0 + rl, N - 1)] + ec));
-        }
-    }
-    __syncthreads();
-    {   // lower: a wave stores 64 consecutive columns of a row
-        const int cl = tid & 63, col = c0 + cl;
-        for (int rl = tid >> 6; rl < 128; rl += 4) {
-            const int row = r0 + rl;
-            if (row >= N || col >= N || col > row) continue;
-            float *p = a.G + (int64_t)row * a.ldg + col;
-            double v = sv[rl][cl];
-            if (a.dense) v += (double)*p;
-            const float f = (float)v;
-            *p = f;
-            sv[rl][cl] = (double)f;
-        }
-    }
-    __syncthreads();
-    {   // upper: a wave stores 64 consecutive columns (the block's rows) of row `col`
-        const int rl = tid & 127, row = r0 + rl;
-        for (int cl = tid >> 7; cl < 64; cl += 2) {
-            const int col = c0 + cl;
-            if (row >= N || col >= N || col >= row) continue;
-            a.G[(int64_t)col * a.ldg + row] = (float)sv[rl][cl];
-        }
+        for (int e = 0; e < 4; ++e)
+            if (row0 + e < N && row0 + e > col) u[e] = f[e];
     }
 }
 

@@ -117,6 +117,33 @@ def test_gram_reference_scale_entrywise(snk):
     assert big.sum() > K * K // 2 and (Gref[big] < 0).sum() > 1000 and rel.max() <= 1e-5
 
 
+def test_gram_ksplit_and_x6_slab_paths(snk):
+    """compute_D.jl's D'D on the production path (fit_center splits the centred rows into h3
+    planes, one power-of-two exponent per row and 1024-column chunk; syrk_h3k_kernel's fp32 chunk
+    partials summed in fp64 by syrk_ksum_kernel) and on the round-5 x6 slab kernel
+    (snk.arith(syrk_ksplit=False)): both within 1e-5 sqrt(G_ii G_jj) of the fp64 oracle, exactly
+    symmetric, the centred D bit-identical either way. K = 300 snapshots over two 256-row
+    blocks (a partial tile), P = 20,000 (a partial last chunk)."""
+    K, P = 300, 20_000
+    rng = np.random.default_rng(11)
+    D0 = rng.standard_normal((K, P)) * 1e-2 + rng.standard_normal(P)[None, :]
+    Dc, _, _ = oracle.welford_center(D0)
+    Gref = Dc @ Dc.T
+    out = {}
+    for ks in (True, False):
+        with snk.arith(syrk_ksplit=ks):
+            lap = snk.LaplaceD(P, K)
+            for k in range(K):
+                lap.set_column(k, D0[k])
+            lap.fit_center()
+            assert np.array_equal(lap.D(), Dc)
+            G, _ = lap.gram()
+        assert np.array_equal(G, G.T)
+        out[ks] = _gram_close(G, Gref)
+        assert out[ks] <= 1e-5, (ks, out[ks])
+    print(f"D'D normalised max error: k-split h3 {out[True]:.2e}, x6 slab {out[False]:.2e}")
+
+
 def test_gram_matches_restated_oracle_small(snk):
     rng = np.random.default_rng(1)
     D0 = rng.standard_normal((20, 333))

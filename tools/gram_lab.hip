@@ -194,13 +194,13 @@ int main(int argc, char **argv) {
             CK(hipMemcpy(di, items.data(), items.size() * 16, hipMemcpyHostToDevice));
             SyrkKArgs k{};
             k.xh = xhl; k.ldh = ldh; k.nst = nst; k.cs = cs; k.items = di; k.part = part; k.ntl = nt256; k.stamps = st;
-            SyrkSumArgs s{};
-            s.part = part; s.S = S; s.ntl = nt256; s.tiles = dt; s.xe = xe; s.N = n; s.G = G; s.ldg = n; s.dense = 0;
+            SyrkSumArgs<float> s{};
+            s.part = part; s.S = S; s.ntl = nt256; s.tiles = dt; s.xe = xe; s.xes = 0; s.N = n; s.G = G; s.ldg = n; s.dense = 0;
             CK(hipMemset(G, 0, (size_t)n * n * 4));
             CK(hipEventRecord(e0));
             syrk_h3k_kernel<<<(unsigned)items.size(), 512>>>(k);
             CK(hipEventRecord(e1));
-            syrk_ksum_kernel<<<(unsigned)(nt256 * 8), 256>>>(s);
+            syrk_ksum_kernel<float><<<(unsigned)(nt256 * 64), 256>>>(s);
             CK(hipEventRecord(e2));
             CK(hipEventSynchronize(e2));
             CK(hipGetLastError());
