@@ -94,6 +94,26 @@ def _latest_pmc(kern: str, pattern: str):
     return {}
 
 
+def _update_pmc() -> dict:
+    """MFMA busy (nominal clock) and LDS conflicts of the five B = 64 update kernels from the
+    newest committed profiles/*_pmc_update.json (tools/pmc_round.sh over the training loop;
+    microsecond dispatches carry no clock: pmc_summary.py's 0.3 ms rule)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_update.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        out = {k.split("(")[0]: {"mfma_busy_nominal_clock": v.get("mfma_busy"),
+                                 "lds_bank_conflict_frac": v.get("lds_conflict_frac"),
+                                 "clock_note": v.get("clock_note")}
+               for k, v in d.items() if "mfma_busy" in v}
+        if out:
+            out["source"] = os.path.relpath(f, REPO)
+            return out
+    return {}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -190,8 +210,9 @@ def _deep_traffic(d: int, n: int, bs: int) -> dict:
     if d != 3 or n != 65536 or bs != 20:
         return {}
     t = _latest_traffic("deep_conv3_kernel<20>", "*_deep_traffic.json")
-    return ({"traffic": t["bytes_per_launch"], "traffic_source": t["source"],
-             "traffic_over_algorithmic": t["bytes_per_launch"] / t["algorithmic_bytes_per_launch"]} if t else {})
+    return dict(({"traffic": t["bytes_per_launch"], "traffic_source": t["source"],
+                  "traffic_over_algorithmic": t["bytes_per_launch"] / t["algorithmic_bytes_per_launch"]} if t else {}),
+                **_latest_pmc("deep_conv3_kernel<20>", "*_pmc_deep.json"))
 
 
 def configs2(args, snk, graph) -> dict:
@@ -741,13 +762,24 @@ def main():
             rr["ms_per_update_marginal"] = (rr["ms_per_step"] - out["ms_per_step"]) / (rr["updates_per_step"] - 1)
             ufl = update_flop(64, bs, C)
             utf = ufl / (rr["ms_per_update_marginal"] * 1e-3) / 1e12 if rr["ms_per_update_marginal"] > 0 else 0.0
+            x6peak = PEAK_BF16_TFLOPS / X6_PRODUCTS
             rr["update_roofline"] = {"bound": "mfma", "flop_per_update": ufl, "achieved": utf,
                                      "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s (fp32)",
                                      "frac": utf / PEAK_FP32_TFLOPS,
+                                     "peak_x6_equivalent": x6peak, "frac_vs_x6_equivalent": utf / x6peak,
+                                     "peak_note": "the update's GEMMs run on three arithmetics: the bf16 x6 split "
+                                                  "(upd_fwd's conv2 / conv3, 419 TFLOP/s fp32-equivalent), the fp16 "
+                                                  "h3 split (conv3_bwd / conv2_bwd data gradients, 839) and exact "
+                                                  "f32 / f64 MFMA (weight gradients, Dense1, 157.3 / 78.6): frac is "
+                                                  "quoted against the fp32 peak, frac_vs_x6_equivalent against the "
+                                                  "peak of the arithmetic that carries most of its FLOP",
                                      "note": "4 B F (B = 64, F = the 3136->64 reference net's forward FLOP) over "
                                              "the marginal update time; the update is a chain of 5 dependent "
                                              "launches (upd_fwd with Dense1 and both heads, d1_bwd, conv3_bwd, "
                                              "conv2_bwd, grad_update), latency-bound at B = 64"}
+            up = _update_pmc()
+            if up:
+                rr["update_roofline"]["kernels_pmc"] = up
         except Exception as e:   # report, do not fail the headline line
             out["reference_ratio"] = {"error": str(e)}
         out["updates_per_s"] = args.updates_per_iter * args.steps / elapsed

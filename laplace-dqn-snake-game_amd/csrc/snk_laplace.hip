@@ -112,13 +112,21 @@ __global__ __launch_bounds__(256) void lap_center_split_kernel(double *__restric
     const int k = blockIdx.y, tid = threadIdx.x;
     const int64_t z = blockIdx.x, p0 = z * CW;
     float m = 0.0f;
+    double dv[CW / 256], mv[CW / 256];
+    double *drow = D + (int64_t)k * P;
 #pragma unroll
-    for (int i = 0; i < CW / 256; ++i) {   // coalesced: consecutive lanes, consecutive columns
+    for (int i = 0; i < CW / 256; ++i) {   // coalesced: consecutive lanes, consecutive columns; all loads first
+        const int64_t p = p0 + tid + 256 * i;
+        dv[i] = p < P ? drow[p] : 0.0;
+        mv[i] = p < P ? mean[p] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < CW / 256; ++i) {
         const int64_t p = p0 + tid + 256 * i;
         float v = 0.0f;
         if (p < P) {
-            const double cc = D[(int64_t)k * P + p] - mean[p];
-            D[(int64_t)k * P + p] = cc;
+            const double cc = dv[i] - mv[i];
+            drow[p] = cc;
             v = (float)cc;
         }
         if (p < ld32) D32[(int64_t)k * ld32 + p] = v;

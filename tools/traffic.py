@@ -26,7 +26,7 @@ def main():
     alg = float(sys.argv[4]) if len(sys.argv) > 4 else None
     f, nf, name = avg(f"{d}/p2/run_counter_collection.csv", "FETCH_SIZE", kern)
     w, nw, _ = avg(f"{d}/p3/run_counter_collection.csv", "WRITE_SIZE", kern)
-    res = {"kernel": name.replace("void snk::", ""), "fetch_kib": f, "write_kib": w, "launches": [nf, nw],
+    res = {"kernel": name.replace("void ", "").replace("snk::", ""), "fetch_kib": f, "write_kib": w, "launches": [nf, nw],
            "bytes_per_launch": (2.0 * f + w) * 1024.0, "algorithmic_bytes_per_launch": alg,
            "how": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes), per-launch mean; "
                   "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes"}
