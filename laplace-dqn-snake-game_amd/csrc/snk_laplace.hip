@@ -469,6 +469,21 @@ static void jac_ensure(snk_dqn_s *h, int64_t n, int64_t floats) {
 
 using namespace snk;
 
+// the K-split snapshot Gram's operand planes and exponents (allocated once; rows K..kpad zero)
+static void lap_planes_ensure(snk_laplace h, hipStream_t s) {
+    const int64_t ldh = ceil_div(h->ld32, LAP_CS * SY_KS) * (LAP_CS * SY_KS), kpad = ceil_div(h->K, SK_T) * SK_T;
+    const int64_t nch = ldh / (LAP_CS * SY_KS);
+    SNK_CHECK(nch <= 65535 && h->K <= 65535, SNK_ERR_INVALID, "snapshot Gram too large");
+    if (h->planes && h->ldh == ldh) return;
+    SNK_HIP(hipStreamSynchronize(s));
+    dfree(h->planes);
+    dfree(h->pexp);
+    h->planes = dalloc<uint16_t>(kpad * 2 * ldh);
+    h->pexp = dalloc<int32_t>(nch * h->K);
+    h->ldh = ldh;
+    SNK_HIP(hipMemsetAsync(h->planes, 0, (size_t)kpad * 2 * ldh * 2, s));
+}
+
 extern "C" int snk_laplace_create(snk_laplace *out, int64_t P, int32_t K) {
     return guard([&] {
         SNK_CHECK(out && P > 0 && K > 0, SNK_ERR_INVALID, "bad Laplace geometry P=%lld K=%d", (long long)P, K);
@@ -482,6 +497,7 @@ extern "C" int snk_laplace_create(snk_laplace *out, int64_t P, int32_t K) {
         h->G = dalloc<double>((size_t)K * K);
         h->D32 = dalloc<float>((size_t)K * h->ld32);
         SNK_HIP(hipMemsetAsync(h->D, 0, (size_t)K * P * 8, stream()));   // zeros(Float64, (P, K))
+        if (arith(SNK_ARITH_SYRK_KSPLIT)) lap_planes_ensure(h, stream());  // the K-split Gram's operand planes
         SNK_HIP(hipStreamSynchronize(stream()));
         *out = h;
     });
@@ -560,18 +576,8 @@ extern "C" int snk_laplace_fit_center(snk_laplace h) {
         launch_check("lap_welford_kernel");
         h->planes_valid = 0;
         if (arith(SNK_ARITH_SYRK_KSPLIT)) {   // centring + fp32 copy + the h3 planes of the snapshot Gram
-            const int64_t ldh = ceil_div(h->ld32, LAP_CS * SY_KS) * (LAP_CS * SY_KS), kpad = ceil_div(h->K, SK_T) * SK_T;
-            const int64_t nch = ldh / (LAP_CS * SY_KS);
-            SNK_CHECK(nch <= 65535 && h->K <= 65535, SNK_ERR_INVALID, "snapshot Gram too large");
-            if (!h->planes || h->ldh != ldh) {
-                SNK_HIP(hipStreamSynchronize(s));
-                dfree(h->planes);
-                dfree(h->pexp);
-                h->planes = dalloc<uint16_t>(kpad * 2 * ldh);
-                h->pexp = dalloc<int32_t>(nch * h->K);
-                h->ldh = ldh;
-                SNK_HIP(hipMemsetAsync(h->planes, 0, (size_t)kpad * 2 * ldh * 2, s));   // rows K..kpad stay zero
-            }
+            lap_planes_ensure(h, s);
+            const int64_t ldh = h->ldh, nch = ldh / (LAP_CS * SY_KS);
             lap_center_split_kernel<<<dim3((unsigned)nch, (unsigned)h->K), 256, 0, s>>>(
                 h->D, h->P, h->K, h->mean, h->D32, h->ld32, h->planes, ldh, h->pexp, h->K);
             launch_check("lap_center_split_kernel");

@@ -416,7 +416,7 @@ def test_trainer_episode_stats_fold(snk, n_envs):
 
 @pytest.mark.parametrize("bs,C", [(9, 2), (10, 1), (11, 2), (13, 1), (13, 2)])
 def test_h3f_act_forward_boards_vs_oracle(snk, bs, C):
-    """conv_h3f_kernel (conv1 on the matrix cores, conv2 + conv3 on the h3 split; >= 1024
+    """conv_h3f_kernel (conv1 on the VALU in fp32, conv2 + conv3 on the h3 split; >= 1024
     states) at the other board sides it serves: odd sides leave a partial conv1 tile per group,
     13 runs the register-staged (non-DMA) form, 1100 states a partial last group of four.
     Q of every 7th state and the last four within 1e-5 * max(1, |q|) of the fp64 oracle."""
