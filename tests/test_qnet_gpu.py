@@ -140,7 +140,7 @@ def test_backward_wide_dynamic_range_vs_oracle(snk, scale):
     """The conv3 / conv2 data gradients run on the fp16 h3 split with ONE power-of-two
     scale per sample (dz) and per block (weights): an element far below its sample's
     maximum keeps only what the fp16 subnormal range holds of its low part (absolute
-    error <= 2^-40 of the scaled maximum, DESIGN.md §4 backward row). Here a few Dense1
+    error <= 2^-40 of the scaled maximum, DESIGN.md §4 "Error bound of the h3 data gradients"). Here a few Dense1
     weight columns are scaled by `scale`, so dz3 of each sample has a handful of
     entries `scale` times larger than the rest and dz2 inherits the spread. Every
     parameter section's gradient (conv1, conv2, conv3, Dense1 weights) must still
