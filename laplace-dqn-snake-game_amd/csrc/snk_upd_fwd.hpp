@@ -670,6 +670,26 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
         // slab with sc1 stores and waits for them, then one lane counts with a relaxed agent
         // atomic; the last arriver, told by the value its add returned, reads every slab with
         // sc1 loads (head_pair_one), which bypass the stale L1 and find the data in memory.
+        // Why this is ordered without a release / acquire pair (an ISA-level
+        // argument, gfx950 only, not one the HIP / C++ memory model gives):
+        //  (1) the slab stores are agent-scope relaxed atomic stores: `global_store ... sc1`,
+        //      which write through the XCD's L2 to the memory side (MALL / HBM) that every XCD
+        //      reads;
+        //  (2) stores retire in vmcnt in issue order and a store's count drops only when the
+        //      memory side acknowledged it at the requested scope, so after `s_waitcnt
+        //      vmcnt(0)` every lane's slab value is visible to agent-scope readers;
+        //  (3) the asm's "memory" clobber keeps the compiler from sinking the stores below it
+        //      or hoisting the ticket above it, so the ticket add is issued after (2);
+        //  (4) the add is an agent-scope RMW on one address: its results are totally ordered,
+        //      so the workgroup that reads 3 comes after the other three's adds, hence after
+        //      their slabs were visible;
+        //  (5) the reader loads the slabs with agent-scope relaxed atomic loads (`global_load
+        //      ... sc1`: L1 bypassed, no stale line), issued only after its own add returned
+        //      (a control dependence plus the compiler barrier below, so no load is
+        //      speculated above the branch).
+        // The UPD_SC1 = 0 build (an acq_rel ticket: wbl2 + inv per workgroup, 0.0703 against
+        // 0.0734 ms per update, profiles/r05n_ab.txt) is the formally ordered cross-check:
+        // `make variant VNAME=acqrel VDEFS=-DUPD_SC1=0` and test_update_heads_fused_bitexact.
         uint32_t last = 0;
 #if UPD_SC1
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -681,6 +701,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
 #endif
         last = __shfl(last, 0, 64);
         if (!last) return;
+        asm volatile("" ::: "memory");   // (5): no slab load above the ticket's result
         if (tid == 0) __hip_atomic_store(args.ticket + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         head_pair_one(args.hn[0], args.hn[1], 2, args.S, L, args.ha, s, tid, hpre);
         UPD_CLK(6);
