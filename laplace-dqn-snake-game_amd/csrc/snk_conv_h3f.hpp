@@ -751,17 +751,21 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
                 for (int pl = 0; pl < 2; ++pl) f.a[k][pl] = pa[pl * PL];
             }
         };
-        auto mfma_block = [&](const Frag &f) {
+        // part 0: only the first MFMA (tile 0, column tile 0, l*h); 1: the rest; 2: all
+        auto mfma_block = [&](const Frag &f, int part = 2) {
 #pragma unroll
             for (int k = 0; k < NT; ++k) {
                 const f16x8 ah = as_h(f.a[k][0]), al = as_h(f.a[k][1]);
 #pragma unroll
                 for (int ct = 0; ct < 2; ++ct) {
                     const f16x8 bh = as_h(f.b[ct][0]), bl = as_h(f.b[ct][1]);
+                    const bool first = k == 0 && ct == 0;
                     f32x4v c = acc[k][ct];
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+                    if (part == 2 || (part == 0) == first) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+                    if (part != 0) {
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+                    }
                     acc[k][ct] = c;
                 }
             }
@@ -777,6 +781,10 @@ __global__ __launch_bounds__(512) void conv_h3f_kernel(H3FArgs a_, int S) {
                 // but the newest LA - 3 DMAs landed (offsets <= kk + 3, read at steps <= kk + 2),
                 // the barrier publishes them
 #if SNK_H3F_VAR == 0
+                // (round 6 measured pinning this order with scheduling barriers, the first MFMA,
+                // then the next offset's 12 fragment reads, then the other MFMAs, as the Gram
+                // kernel does: 3.4 % slower on the headline than the compiler's own interleave,
+                // gpurun_out r06g; not kept)
                 dma(kk + H3F_LA);
                 frag_read(kk + 1, nxt);
                 mfma_block(cur);

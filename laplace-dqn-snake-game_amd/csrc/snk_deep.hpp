@@ -362,6 +362,60 @@ __device__ __forceinline__ u32x2 dfr_tr44(const u32x2 &v, int lane) {
                  (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v[1])};
 }
 
+// The K loop of one deep_front layer, software-pipelined: for each of the KK kernel offsets
+// (fully unrolled) two weight fragments (A, column tiles c2 = 0, 1) and NT activation
+// fragments (B, row tiles) feed 2 NT MFMAs. Each row tile's fragment for offset kk+1 is read
+// right after that tile's two MFMAs of offset kk (its registers are free then: one buffer of NT
+// fragments, as the 256-register budget of two waves per SIMD needs), the next offset's weights
+// after the first tile; scheduling barriers pin the order (left to itself the scheduler sank
+// every read next to its MFMAs, which then waited a full LDS round trip each). acc[t][c2]
+// accumulates over kk in order: the results are those of the plain loop.
+// PLAIN (the training forward, KEEP: its extra stores' addresses leave no registers for the
+// pipeline at 20x20): each offset's fragments read, then its MFMAs, no pinning.
+template <int KK, int NT, bool PLAIN, typename WF, typename XF>
+__device__ __forceinline__ void dfr_pipeline(WF wfrag, XF xfrag, f32x4 (&acc)[NT][2]) {
+    if constexpr (PLAIN) {
+#pragma unroll 3
+        for (int kk = 0; kk < KK; ++kk) {
+            bf16x8 wa[2];
+#pragma unroll
+            for (int c2 = 0; c2 < 2; ++c2) wa[c2] = wfrag(kk, c2);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const bf16x8 xv = xfrag(kk, t);
+#pragma unroll
+                for (int c2 = 0; c2 < 2; ++c2)
+                    acc[t][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[t][c2], 0, 0, 0);
+            }
+        }
+        return;
+    }
+    bf16x8 wa[2][2], xv[NT];
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) wa[0][c2] = wfrag(0, c2);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) xv[t] = xfrag(0, t);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+        const int b = kk & 1;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+#pragma unroll
+            for (int c2 = 0; c2 < 2; ++c2)
+                acc[t][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[b][c2], xv[t], acc[t][c2], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (kk + 1 < KK) {
+                if (t == 0) {
+#pragma unroll
+                    for (int c2 = 0; c2 < 2; ++c2) wa[b ^ 1][c2] = wfrag(kk + 1, c2);
+                }
+                xv[t] = xfrag(kk + 1, t);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 template <int C, int H, bool KEEP>
 __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const float *__restrict__ img0,
                                                          const uint16_t *__restrict__ wimg1,
@@ -449,13 +503,14 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                 int i, j;
                 tpos(t, i, j);
                 const int bb = min(i, H - 1) + min(j, H - 1) * HB;
-                uint32_t w[4];
+                // branch-free gather: every lane loads (k past 9C reads cell 0 and is masked to
+                // zero), all eight loads in flight before the first use
+                uint32_t w[4], v[8];
 #pragma unroll
-                for (int e2 = 0; e2 < 4; ++e2) {
-                    const uint32_t v0 = bofs[2 * e2] >= 0 ? BD[bb + bofs[2 * e2]] : 0u;
-                    const uint32_t v1 = bofs[2 * e2 + 1] >= 0 ? BD[bb + bofs[2 * e2 + 1]] : 0u;
-                    w[e2] = v0 | (v1 << 16);
-                }
+                for (int e = 0; e < 8; ++e) v[e] = BD[bb + max(bofs[e], 0)];
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2)
+                    w[e2] = (bofs[2 * e2] >= 0 ? v[2 * e2] : 0u) | ((bofs[2 * e2 + 1] >= 0 ? v[2 * e2 + 1] : 0u) << 16);
                 const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, as_bf(u32x4{w[0], w[1], w[2], w[3]}),
                                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
                 const u32x2 o = relu_bf16x4(acc, b0);
@@ -474,23 +529,23 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
             f32x4 acc[HALF][2];
 #pragma unroll
             for (int ii = 0; ii < HALF; ++ii) acc[ii][0] = acc[ii][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 3
-            for (int kk = 0; kk < 9; ++kk) {
-                const int koff = ((kk % 3) + (kk / 3) * PJ) * XST;
-                bf16x8 wa[2];
+            // branch-free: a missing tile computes the SIMD's tile 0 again (never stored); the
+            // nine kernel offsets unrolled with offset kk+1's fragments read under kk's MFMAs
+            int xb[HALF];
 #pragma unroll
-                for (int c2 = 0; c2 < 2; ++c2)
-                    wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(W1s + (kk * 32 + c2 * 16) * 32 + wl));
-#pragma unroll
-                for (int ii = 0; ii < HALF; ++ii) {
-                    const int i = half * HALF + ii, t = simd + 4 * i;
-                    if (i >= TPS || (i == TPS - 1 && !last_ok)) continue;
-                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(X + xl + tbase(t) * XST + koff));
-#pragma unroll
-                    for (int c2 = 0; c2 < 2; ++c2)
-                        acc[ii][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[ii][c2], 0, 0, 0);
-                }
+            for (int ii = 0; ii < HALF; ++ii) {
+                const int i = half * HALF + ii;
+                const bool live = i < TPS && !(i == TPS - 1 && !last_ok);
+                xb[ii] = xl + tbase(simd + 4 * (live ? i : 0)) * XST;
             }
+            dfr_pipeline<9, HALF, KEEP>(
+                [&](int kk, int c2) __attribute__((always_inline)) {
+                    return as_bf(*reinterpret_cast<const u32x4 *>(W1s + (kk * 32 + c2 * 16) * 32 + wl));
+                },
+                [&](int kk, int ii) __attribute__((always_inline)) {
+                    return as_bf(*reinterpret_cast<const u32x4 *>(X + xb[ii] + ((kk % 3) + (kk / 3) * PJ) * XST));
+                },
+                acc);
             __syncthreads();   // every wave's L1 reads of X are done: X takes the L1 output
 #pragma unroll
             for (int ii = 0; ii < HALF; ++ii) {
@@ -517,23 +572,17 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
             f32x4 acc[TPS][2];
 #pragma unroll
             for (int ii = 0; ii < TPS; ++ii) acc[ii][0] = acc[ii][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 3
-            for (int kk = 0; kk < 9; ++kk) {
-                const int koff = ((kk % 3) + (kk / 3) * PJ) * XST;
-                bf16x8 wa[2];
+            int xb[TPS];
 #pragma unroll
-                for (int c2 = 0; c2 < 2; ++c2)
-                    wa[c2] = as_bf(*reinterpret_cast<const u32x4 *>(W2s + (kk * 64 + (2 * half + c2) * 16) * 32 + wl));
-#pragma unroll
-                for (int ii = 0; ii < TPS; ++ii) {
-                    const int t = simd + 4 * ii;
-                    if (ii == TPS - 1 && !last_ok) continue;
-                    const bf16x8 xv = as_bf(*reinterpret_cast<const u32x4 *>(X + xl + tbase(t) * XST + koff));
-#pragma unroll
-                    for (int c2 = 0; c2 < 2; ++c2)
-                        acc[ii][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[c2], xv, acc[ii][c2], 0, 0, 0);
-                }
-            }
+            for (int ii = 0; ii < TPS; ++ii) xb[ii] = xl + tbase(simd + 4 * ((ii == TPS - 1 && !last_ok) ? 0 : ii)) * XST;
+            dfr_pipeline<9, TPS, KEEP>(
+                [&](int kk, int c2) __attribute__((always_inline)) {
+                    return as_bf(*reinterpret_cast<const u32x4 *>(W2s + (kk * 64 + (2 * half + c2) * 16) * 32 + wl));
+                },
+                [&](int kk, int ii) __attribute__((always_inline)) {
+                    return as_bf(*reinterpret_cast<const u32x4 *>(X + xb[ii] + ((kk % 3) + (kk / 3) * PJ) * XST));
+                },
+                acc);
 #pragma unroll
             for (int ii = 0; ii < TPS; ++ii) {
                 if (ii == TPS - 1 && !last_ok) continue;
