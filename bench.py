@@ -94,6 +94,21 @@ def _latest_pmc(kern: str, pattern: str):
     return {}
 
 
+class _stdout_to_stderr:
+    """RCCL prints its version banner to stdout when a communicator is created; the bench's
+    stdout is the one JSON line, so fd 1 points at fd 2 for the duration."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.fd = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.fd, 1)
+        os.close(self.fd)
+
+
 def _update_pmc() -> dict:
     """MFMA busy (nominal clock) and LDS conflicts of the five B = 64 update kernels from the
     newest committed profiles/*_pmc_update.json (tools/pmc_round.sh over the training loop;
@@ -412,8 +427,9 @@ def d_build_gram(args, snk, model, dist, rank, world) -> dict:
         gather_check = None
     else:
         import torch
-        comm = snk.Comm(world, rank, snk.dist.broadcast_bytes(dist, snk.Comm.unique_id() if rank == 0 else None,
-                                                               rank))
+        uid = snk.dist.broadcast_bytes(dist, snk.Comm.unique_id() if rank == 0 else None, rank)
+        with _stdout_to_stderr():
+            comm = snk.Comm(world, rank, uid)
         G.zero()
         snk.jacobian_gram_shard(model, rb, n, rank, world, G)     # warm-up
         sync()
@@ -588,7 +604,8 @@ def main():
                      updates_per_iter=args.updates_per_iter, seed=1234 + rank)
     comm = None
     if world > 1:
-        comm = snk.dist_attach(tr, dist, rank, world)
+        with _stdout_to_stderr():
+            comm = snk.dist_attach(tr, dist, rank, world)
     graph = not args.no_graph
     snk.fill_buffer_(tr, graph=graph)                    # fill_buffer!: untimed
     tr.run(args.warmup, learn=True, graph=graph)
@@ -627,7 +644,8 @@ def main():
     if comm is not None:
         rccl_nranks, rccl_rank = comm.info()
     else:
-        c1 = snk.Comm(1, 0, snk.Comm.unique_id())
+        with _stdout_to_stderr():
+            c1 = snk.Comm(1, 0, snk.Comm.unique_id())
         rccl_nranks, rccl_rank = c1.info()
         del c1
     if rccl_nranks != world or rccl_rank != rank:

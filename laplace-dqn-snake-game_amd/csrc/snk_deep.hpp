@@ -362,6 +362,15 @@ __device__ __forceinline__ u32x2 dfr_tr44(const u32x2 &v, int lane) {
                  (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v[1])};
 }
 
+// A workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then
+// s_barrier. __syncthreads' fence also waits for every outstanding global load and store
+// (s_waitcnt vmcnt(0)): in deep_front_kernel that put the previous sample's a2 stores and the
+// next sample's board loads on the critical path at every one of its four barriers per sample.
+__device__ __forceinline__ void dfr_lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) (vmcnt, expcnt left at their maxima)
+    __builtin_amdgcn_s_barrier();
+}
+
 // The K loop of one deep_front layer, software-pipelined: for each of the KK kernel offsets
 // (fully unrolled) two weight fragments (A, column tiles c2 = 0, 1) and NT activation
 // fragments (B, row tiles) feed 2 NT MFMAs. Each row tile's fragment for offset kk+1 is read
@@ -492,7 +501,7 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                 BD[c * PL + (cell % H + 1) + (cell / H + 1) * HB] = f2bf(bv[u]);
             }
         }
-        __syncthreads();   // boards in; X free (last read by the previous sample's L2)
+        dfr_lds_barrier();   // boards in; X free (last read by the previous sample's L2)
         // ---- L0: column tile `half` of the SIMD's row tiles
         {
             const bf16x8 wa = as_bf(*reinterpret_cast<const u32x4 *>(W0s + half * 16 * 32 + wl));
@@ -522,7 +531,7 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                     *reinterpret_cast<u32x2 *>(X + ((ti + 1) + (tj + 1) * PJ) * XST + half * 16 + 4 * (r >> 2)) = ot;
             }
         }
-        __syncthreads();
+        dfr_lds_barrier();
         // ---- L1: this half's share of the SIMD's row tiles, both column tiles; the
         // result replaces L0's in X after a barrier
         {
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                     return as_bf(*reinterpret_cast<const u32x4 *>(X + xb[ii] + ((kk % 3) + (kk / 3) * PJ) * XST));
                 },
                 acc);
-            __syncthreads();   // every wave's L1 reads of X are done: X takes the L1 output
+            dfr_lds_barrier();   // every wave's L1 reads of X are done: X takes the L1 output
 #pragma unroll
             for (int ii = 0; ii < HALF; ++ii) {
                 const int i2 = half * HALF + ii, t = simd + 4 * i2;
@@ -565,7 +574,7 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                 }
             }
         }
-        __syncthreads();
+        dfr_lds_barrier();
         if (s + gridDim.x < S) bload(s + gridDim.x);   // the next sample's boards, in flight through L2
         // ---- L2: all the SIMD's row tiles, column tiles 2*half, 2*half + 1
         {
@@ -764,13 +773,16 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
                 *reinterpret_cast<u32x2 *>(y + (sg * WO * WO + o) * 64 + (2 * half + c2) * 16 + 4 * g) =
                     relu_bf16x4(acc[i][c2], bb[c2]);
         }
-        __syncthreads();   // every wave is done reading this pair's inputs
+        // LDS-only barriers (dfr_lds_barrier): a __syncthreads fence drained the pair's a3 stores
+        // (and the ring's refills for the next pair) before the next pair's input loads were even
+        // issued; the refills are counted by the offset loop's own vmcnt waits
+        dfr_lds_barrier();   // every wave is done reading this pair's inputs
         if (more) {   // the next pair's inputs
 #pragma unroll
             for (int u = 0; u < APT; ++u)
                 if (tid + u * 512 < APIECES) apark(u, apiece(pn, u));
         }
-        __syncthreads();
+        dfr_lds_barrier();
     }
     __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // the ring's last refills land before the workgroup ends
 }

@@ -27,7 +27,7 @@ for rep in $(seq 0 $((REPS - 1))); do
   for v in "$@"; do
     n=$(echo $v | tr ':=' '__')
     env $(env_of $v) timeout -k 10 300 python bench.py $BA $(args_of $v) > $OUT/b_$n.$rep.json 2> $OUT/b_$n.$rep.err || exit 4
-    python -c "import json;d=json.load(open('$OUT/b_$n.$rep.json'));r=d.get('reference_ratio',{});print('$rep $v',d['value'],d['ms_per_step'],(d.get('roofline') or {}).get('avg_launch_ms'),r.get('ms_per_update_marginal'))"
+    python -c "import json;d=json.loads(open('$OUT/b_$n.$rep.json').read().strip().splitlines()[-1]);r=d.get('reference_ratio',{});print('$rep $v',d['value'],d['ms_per_step'],(d.get('roofline') or {}).get('avg_launch_ms'),r.get('ms_per_update_marginal'))"
   done
 done
 echo done
