@@ -695,6 +695,7 @@ def main():
         "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
                         "food_faults": faults},
         "rccl_nranks": rccl_nranks,
+        "build": _lib.build_provenance(),
         "roofline": None,
         "cpu_baseline": None,
     }

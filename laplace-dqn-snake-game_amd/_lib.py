@@ -54,6 +54,7 @@ P = C.POINTER
 _PROTOS = {
     "snk_last_error": [],
     "snk_version": [P(i32)],
+    "snk_build_source_sha256": [],
     "snk_device_count": [P(i32)],
     "snk_set_device": [i32],
     "snk_set_stream": [vp],
@@ -175,7 +176,7 @@ class TrainerStats(C.Structure):
         super().__init__(C.sizeof(self), *args, **kw)
 
 
-_RESTYPE = {"snk_last_error": C.c_char_p}
+_RESTYPE = {"snk_last_error": C.c_char_p, "snk_build_source_sha256": C.c_char_p}
 
 
 def header_symbols() -> list[str]:
@@ -204,6 +205,29 @@ def load():
         fn.restype = _RESTYPE.get(name, C.c_int)
     _lib = lib
     return lib
+
+
+def source_sha256(csrc: str | None = None) -> str:
+    """The build-provenance hash of a source tree, as csrc/Makefile computes it
+    (`sha256sum $(sort *.hip *.hpp ../../include/snakehip.h Makefile) | sha256sum`)."""
+    import glob
+    import hashlib
+    csrc = csrc or os.path.join(_HERE, "csrc")
+    names = [os.path.basename(f) for f in glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp"))]
+    names += ["../../include/snakehip.h", "Makefile"]
+    lines = ""
+    for n in sorted(names):
+        with open(os.path.join(csrc, n), "rb") as f:
+            lines += f"{hashlib.sha256(f.read()).hexdigest()}  {n}\n"
+    return hashlib.sha256(lines.encode()).hexdigest()
+
+
+def build_provenance() -> dict:
+    """Which sources the loaded library was linked from, against the tree beside it."""
+    lib_h = load().snk_build_source_sha256().decode()
+    tree_h = source_sha256()
+    return {"lib": os.path.basename(LIB_PATH), "lib_source_sha256": lib_h, "tree_source_sha256": tree_h,
+            "lib_matches_tree": lib_h == tree_h}
 
 
 def check(status: int):

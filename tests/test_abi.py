@@ -27,6 +27,14 @@ def test_library_is_gfx950_code_object():
     assert b"env_step_kernel" in blob
 
 
+def test_library_built_from_tree_sources():
+    """Build provenance: the .so carries the sha256 of the sources it was linked
+    from (csrc/Makefile); it must equal the hash of the sources in this tree."""
+    p = _lib.build_provenance()
+    assert len(p["lib_source_sha256"]) == 64
+    assert p["lib_matches_tree"], (p, "libsnakehip.so is stale: rebuild with __graft_entry__.build()")
+
+
 def test_food_list_host_matches_oracle():
     """snk_food_list is host code (no device needed): same Xoshiro(42)."""
     for bs in (10, 12, 20):
