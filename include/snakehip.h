@@ -41,7 +41,7 @@ extern "C" {
 /* ---------------------------------------------------------------- runtime */
 const char *snk_last_error(void);
 int snk_version(int32_t *version_out);
-/* sha256 (hex) of the sources this library was linked from: csrc/*.hip, csrc/*.hpp, this
+/* sha256 (hex) of the sources this library was linked from: the csrc .hip and .hpp files, this
    header and csrc/Makefile, as `sha256sum <sorted files> | sha256sum` in csrc/ (build provenance) */
 const char *snk_build_source_sha256(void);
 int snk_device_count(int32_t *n_out);
