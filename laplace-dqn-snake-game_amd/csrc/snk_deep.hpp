@@ -640,6 +640,15 @@ struct DeepL3Shape {
 };
 __device__ __forceinline__ int dl3_slot(int row, int c) { return row * 64 + 8 * (c ^ (row & 7)); }
 
+// measurement builds only (-DSNK_DL3_VAR=n with SNK_ENV_CLOCKS; wrong results by design): the
+// pair loop without the next pair's input loads (1), the per-offset barriers (2), the MFMAs (3)
+// or the activation fragment reads (4) (`profiles/r06k_dl3_vars.txt`)
+#ifndef SNK_DL3_VAR
+#define SNK_DL3_VAR 0
+#endif
+#if SNK_DL3_VAR && !defined(SNK_ENV_CLOCKS)
+#error "SNK_DL3_VAR: measurement (clocks) builds only"
+#endif
 template <int H>
 __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restrict__ x,
                                                          const uint16_t *__restrict__ wimg,
@@ -740,7 +749,7 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         for (int kk = 0; kk < 36; ++kk) {
             __builtin_amdgcn_s_waitcnt(waitcnt_vm(Sh::WSLOTS - 3));
             __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-            __builtin_amdgcn_s_barrier();
+            if (SNK_DL3_VAR != 2) __builtin_amdgcn_s_barrier();
             wdma(kk + Sh::WSLOTS - 1);
             if (kk == 0) wread(0, wcur);
             wread(kk + 1, wnext);   // kk = 35: offset 0 of the next pair (slot 36 % 4), harmless
@@ -751,10 +760,17 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
                 for (int i = 0; i < TPS; ++i) {
                     if (i == TPS - 1 && !last_ok) continue;   // only the last tile can be missing
 #pragma unroll
-                    for (int c2 = 0; c2 < 2; ++c2)
-                        acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wcur[2 * c + c2]), xv[i], acc[i][c2],
-                                                                             0, 0, 0);
-                    xv[i] = xread(nk, nc, i);
+                    for (int c2 = 0; c2 < 2; ++c2) {
+                        if (SNK_DL3_VAR != 3)
+                            acc[i][c2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wcur[2 * c + c2]), xv[i], acc[i][c2],
+                                                                                 0, 0, 0);
+                        else
+                            asm volatile("" : "+v"(acc[i][c2]) : "v"(wcur[2 * c + c2]), "v"(xv[i]));
+                    }
+                    if (SNK_DL3_VAR != 4)
+                        xv[i] = xread(nk, nc, i);
+                    else
+                        asm volatile("" : "+v"(xv[i]));
                 }
             }
 #pragma unroll
@@ -777,7 +793,7 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
         // (and the ring's refills for the next pair) before the next pair's input loads were even
         // issued; the refills are counted by the offset loop's own vmcnt waits
         dfr_lds_barrier();   // every wave is done reading this pair's inputs
-        if (more) {   // the next pair's inputs
+        if (more && SNK_DL3_VAR != 1) {   // the next pair's inputs
 #pragma unroll
             for (int u = 0; u < APT; ++u)
                 if (tid + u * 512 < APIECES) apark(u, apiece(pn, u));
