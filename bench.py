@@ -320,7 +320,7 @@ def configs3_per_rank(args, snk, graph) -> dict:
                          "achieved": tf, "peak": peak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / peak,
                          "avg_launch_ms": loop_ms.value, "flop_per_launch": fl,
                          "avg_launch_ms_how": "HIP events recorded by the launch's dispatch (hipExtLaunchKernelGGL), "
-                                              "mean of 10 eager training iterations"},
+                                              "median of 10 eager training iterations behind graph replays"},
             "train_stats": {"updates": st["updates"], "episodes": st["episodes"], "env_steps": st["env_steps"],
                             "food_faults": tr.game.check_faults()}}
 
@@ -714,18 +714,13 @@ def main():
         # three; ms[0] is then the conv3 weight-max scan (the h3 weight scale)
         fused = ms[1] == 0.0
         flop_dom = flop_conv3 + (flop_conv2 + flop_conv1 if fused else 0.0)
-        # the dominant kernel's duration INSIDE the training loop: eager iterations after the
-        # timed region, HIP events recorded by the kernel's own dispatch (hipExtLaunchKernelGGL)
-        # on the library stream; the median of 200 (the first dozens after the graph loop run up
-        # to 15 % longer, as rocprofv3's trace of the same launches shows); back to back in
-        # isolation (ms[2]) it runs hotter and slower
+        # the dominant kernel's duration INSIDE the training loop: 50 eager training iterations,
+        # each queued behind a replay of the learning graph (the GPU as busy as in the timed
+        # loop), HIP events recorded by the kernel's own dispatch (hipExtLaunchKernelGGL) on the
+        # library stream, the median; back to back in isolation (ms[2]) it runs slower
         loop_ms = _lib.f64(0)
-        ev = []
-        for _ in range(200):
-            _lib.call("snk_trainer_time_act_kernel", tr.handle, 1, ctypes.byref(loop_ms))
-            if loop_ms.value > 0:
-                ev.append(loop_ms.value)
-        dom_ms = float(np.median(ev)) if ev else ms[2]
+        _lib.call("snk_trainer_time_act_kernel", tr.handle, 50, ctypes.byref(loop_ms))
+        dom_ms = loop_ms.value if loop_ms.value > 0 else ms[2]
         tf = flop_dom / (dom_ms * 1e-3) / 1e12
         # the forward GEMMs run fp32 products as 6 exact bf16 split products on the
         # bf16 MFMA (snk.arith(conv_fp32=True): native f32 MFMA): the fp32-equivalent peak is
@@ -745,9 +740,9 @@ def main():
                            "achieved": tf, "peak": peak, "unit": "TFLOP/s (fp32-equivalent)", "frac": tf / peak,
                            "traffic": None, "avg_launch_ms": dom_ms,
                            "avg_launch_ms_how": ("median of HIP events recorded by the launch's dispatch "
-                                                 "(hipExtLaunchKernelGGL) in 200 eager training iterations"
-                                                 if ev else "HIP events, back-to-back launches"),
-                           "mean_launch_ms": float(np.mean(ev)) if ev else None,
+                                                 "(hipExtLaunchKernelGGL) in 50 eager training iterations, each "
+                                                 "queued behind a learning-graph replay"
+                                                 if loop_ms.value > 0 else "HIP events, back-to-back launches"),
                            "isolated_back_to_back_ms": ms[2], "flop_per_launch": flop_dom,
                            "flop_note": "conv1's 2*n*bs^2*16*9C FLOP (1 % of the launch) run on the VALU and are "
                                         "counted against the MFMA peak" if fused else None,

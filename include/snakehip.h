@@ -286,10 +286,11 @@ int snk_trainer_stats(snk_trainer t, snk_trainer_stats_t *out);
 /* tr.losses: loss of update u at host[u % loss_log_capacity] */
 int snk_trainer_losses(snk_trainer t, double *host, int64_t n);
 int snk_trainer_act_ptr(snk_trainer t, uint8_t **act_dev);
-/* measurement: `iters` real (learning) trainer iterations, eager, with HIP events
- * around the act forward's fused conv kernel (conv_h3f_kernel) on the library
- * stream: *ms_out = its mean duration inside the training loop (0 when this
- * trainer's act forward does not run it) */
+/* measurement: `iters` real (learning) trainer iterations, eager, each queued behind one
+ * replay of the learning graph (no host wait between them), with HIP events recorded by the
+ * dispatch of the act forward's fused conv kernel (conv_h3f_kernel) on the library stream:
+ * *ms_out = its median duration inside the training loop (0 when this trainer's act forward
+ * does not run it). The graph replays are real training steps too. */
 int snk_trainer_time_act_kernel(snk_trainer t, int32_t iters, double *ms_out);
 
 /* ---------------------------------------------------------------- multi-GPU
