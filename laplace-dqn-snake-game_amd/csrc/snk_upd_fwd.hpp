@@ -689,7 +689,8 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
         //      speculated above the branch).
         // The UPD_SC1 = 0 build (an acq_rel ticket: wbl2 + inv per workgroup, 0.0703 against
         // 0.0734 ms per update, profiles/r05n_ab.txt) is the formally ordered cross-check:
-        // `make variant VNAME=acqrel VDEFS=-DUPD_SC1=0` and test_update_heads_fused_bitexact.
+        // libsnakehip_acqrel.so (csrc/Makefile, built with the library) and
+        // test_update_sc1_handoff_matches_acq_rel_build (bit-identical loss and gradient).
         uint32_t last = 0;
 #if UPD_SC1
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -481,6 +481,48 @@ def test_update_heads_fused_bitexact(snk, B):
     assert np.array_equal(res[True][1], res[False][1])
 
 
+def _handoff_case(snk, B=64):
+    """One update's loss and gradient through upd_fwd_kernel's fused heads (the sc1 slab
+    hand-off in the shipping build), on fixed inputs."""
+    g, rb = _random_replay(snk, 12, 2)
+    m = snk.DQNModel(12, 3, n_frames=2, seed=21)
+    rng = np.random.default_rng(1)
+    m.set_params(m.get_params() + rng.standard_normal(m.P).astype(np.float32) * 0.01, snk.SNK_NET_TARGET)
+    idx, _ = snk.sample(rb, seed=4)
+    loss = m.loss_grad(rb, idx, B)
+    return np.float64(loss), m.grad.copy()
+
+
+def test_update_sc1_handoff_matches_acq_rel_build(snk, tmp_path):
+    """upd_fwd_kernel hands the Dense1 slabs to the sample's last workgroup
+    with sc1 stores, an in-order vmcnt wait and a relaxed ticket: an ISA-level argument
+    (snk_upd_fwd.hpp), not a C++ happens-before. The formally ordered build (-DUPD_SC1=0: an
+    acq_rel ticket, libsnakehip_acqrel.so, built by __graft_entry__.build()) runs the same update
+    in a child process: loss and gradient bit-identical, for B = 64 and 37."""
+    import os
+    import subprocess
+    import sys
+    from snake_amd import _lib
+    lib = os.path.join(os.path.dirname(_lib.LIB_PATH), "libsnakehip_acqrel.so")
+    assert os.path.exists(lib), "libsnakehip_acqrel.so is not built (__graft_entry__.build())"
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for B in (64, 37):
+        out = tmp_path / f"acq{B}.npz"
+        code = (f"import sys; sys.path[:0] = [{root!r}, {here!r}, {os.path.join(root, 'oracle')!r}]\n"
+                "import numpy as np, snake_amd as snk\n"
+                "from snake_amd import _lib\n"
+                "assert _lib.LIB_PATH.endswith('libsnakehip_acqrel.so')\n"
+                "from test_qnet_gpu import _handoff_case\n"
+                f"loss, grad = _handoff_case(snk, {B})\n"
+                f"np.savez({str(out)!r}, loss=loss, grad=grad)\n")
+        subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SNK_LIB=lib), check=True, timeout=240)
+        ref = np.load(out)
+        loss, grad = _handoff_case(snk, B)
+        assert loss == ref["loss"], (float(loss), float(ref["loss"]))
+        assert np.array_equal(grad, ref["grad"])
+
+
 def test_env_fused_act_head_bitexact(snk):
     """The trainer's act head inside env_step_kernel (4096 envs: the act forward stops at
     Dense1's slabs; the step computes each env's Q-values and epsilon-greedy action first,
