@@ -600,3 +600,26 @@ extern "C" int snk_dqn_time_deep_layers(snk_dqn h, snk_env env, int32_t reps, do
         deep_time_layers(h, src_env(E), E.n, ha, reps, ms_out, stream());
     });
 }
+
+#ifdef SNK_ENV_CLOCKS
+// profiling builds: out[wg][8] = deep_front_kernel's per-phase time sums of the LAST launch
+// (s_memrealtime ticks, 100 MHz; slot 6 = the workgroup's sample count)
+extern "C" int snk_dfr_debug_clocks(int64_t n_wg, uint64_t *out_host, int32_t arm) {
+    return guard([&] {
+        static uint64_t *buf = nullptr;
+        static int64_t cap = 0;
+        if (arm) {
+            if (n_wg > cap) {
+                dfree(buf);
+                buf = dalloc<uint64_t>(n_wg * 8);
+                cap = n_wg;
+            }
+            SNK_HIP(hipMemset(buf, 0, n_wg * 8 * sizeof(uint64_t)));
+            SNK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dfr_clk), &buf, sizeof(buf)));
+            return;
+        }
+        SNK_HIP(hipDeviceSynchronize());
+        SNK_HIP(hipMemcpy(out_host, buf, n_wg * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    });
+}
+#endif

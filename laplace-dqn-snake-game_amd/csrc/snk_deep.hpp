@@ -425,6 +425,23 @@ __device__ __forceinline__ void dfr_pipeline(WF wfrag, XF xfrag, f32x4 (&acc)[NT
     }
 }
 
+// Profiling builds only (make clocks): per-workgroup sums of wave 0's time per phase over its
+// samples (0 boards into LDS + barrier, 1 L0 + barrier, 2 L1 offsets, 3 L1 epilogue and its two
+// barriers, 4 L2 offsets, 5 L2 epilogue: staging in LDS, two barriers, the a2 stores; 6 the sample
+// count), read by snk_dfr_debug_clocks
+#ifdef SNK_ENV_CLOCKS
+__device__ uint64_t *g_dfr_clk;
+#define DFR_CLK(k)                                                                                    \
+    do {                                                                                              \
+        if (tid == 0 && g_dfr_clk) {                                                                  \
+            const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                     \
+            dfr_acc[k] += t_ - dfr_t;                                                                 \
+            dfr_t = t_;                                                                               \
+        }                                                                                             \
+    } while (0)
+#else
+#define DFR_CLK(k) do { } while (0)
+#endif
 template <int C, int H, bool KEEP>
 __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const float *__restrict__ img0,
                                                          const uint16_t *__restrict__ wimg1,
@@ -481,27 +498,75 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
         i = 4 * (t % NB) + (r & 3);
         j = 4 * (t / NB) + (r >> 2);
     };
-    float bv[NBV];
+    int bv[NBV];   // raw: the int8 cell, or the float's bits (converted where stored, so no
+                   // wait follows the load)
+    // env frame ring (the act forward): the channels' ring slots come from the step counter,
+    // which no launch changes: read once, so a cell is one byte load (through src.load each cell
+    // was a counter load, a wait, the byte load and a wait)
+    const bool ring = !src.fbase && !src.idx;
+    const int8_t *cb[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) cb[c] = ring ? src.plane(0, c) : nullptr;
     auto bload = [&](int64_t s) __attribute__((always_inline)) {
+        int te = tid;   // opaque: the per-cell offsets stay in the loop (hoisted, they were
+        asm volatile("" : "+v"(te));   // spilled across it)
 #pragma unroll
         for (int u = 0; u < NBV; ++u) {
-            const int e = tid + u * 512;
-            if (e < C * M) bv[u] = src.load(s, e / M, e % M);
+            const int e = te + u * 512;
+            if (e < C * M) {
+                const int c = e / M, cell = e - c * M;
+                if (ring) {
+                    const int8_t *pl = cb[0];
+#pragma unroll
+                    for (int cc = 1; cc < C; ++cc) pl = c == cc ? cb[cc] : pl;
+                    bv[u] = pl[s * (int64_t)src.pitch + cell];
+                } else if (src.fbase) {
+                    bv[u] = __float_as_int(src.fbase[(s * C + c) * src.ncell + cell]);
+                } else {
+                    bv[u] = src.plane(s, c)[cell];
+                }
+            }
         }
     };
     int64_t s = blockIdx.x;
     if (s < S) bload(s);
     __syncthreads();
+    // the first boards landed: with this wait on the loop's entry path as on its back edge (the
+    // wait ahead of the a2 stores), the compiler puts no wait at the loop head
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+#ifdef SNK_ENV_CLOCKS
+    uint64_t dfr_acc[7] = {0, 0, 0, 0, 0, 0, 0}, dfr_t = __builtin_amdgcn_s_memrealtime();
+#endif
     for (; s < S; s += gridDim.x) {
 #pragma unroll
         for (int u = 0; u < NBV; ++u) {
             const int e = tid + u * 512;
             if (e < C * M) {
                 const int c = e / M, cell = e % M;
-                BD[c * PL + (cell % H + 1) + (cell / H + 1) * HB] = f2bf(bv[u]);
+                BD[c * PL + (cell % H + 1) + (cell / H + 1) * HB] = f2bf(src.fbase ? __int_as_float(bv[u]) : (float)bv[u]);
             }
         }
+        // the next sample's boards: in flight through this whole sample (waited for before the
+        // a2 stores below, so the wait above never waits for those stores)
+        if (s + gridDim.x < S) bload(s + gridDim.x);
         dfr_lds_barrier();   // boards in; X free (last read by the previous sample's L2)
+        if constexpr (!KEEP) {
+            // the previous sample's a2 staging (below) overwrote X's zero border (the 3x3
+            // convolutions' padding, which no epilogue writes): channels 0..31 of its positions
+            // zeroed again, beside L0's interior writes and ahead of L0's barrier
+            // rows 0 and HB-1 (2 HB positions), then columns 0 and HB-1 of rows 1..HB-2; four
+            // 16-byte pieces per position, one per thread
+            static_assert(4 * 4 * (HB - 1) <= 512, "one border piece per thread");
+            if (tid < 4 * 4 * (HB - 1)) {
+                int tz = tid;   // an opaque copy: the address stays in the loop (hoisted, it held
+                asm volatile("" : "+v"(tz));   // registers through L2 and the kernel spilled)
+                const int bp = tz >> 2, ch = tz & 3, rw = bp < 2 * HB;
+                const int x = rw ? bp % HB : (bp - 2 * HB) % 2 * (HB - 1);
+                const int y = rw ? bp / HB * (HB - 1) : 1 + (bp - 2 * HB) / 2;
+                *reinterpret_cast<u32x4 *>(X + (x + y * PJ) * XST + 8 * ch) = u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+        DFR_CLK(0);
         // ---- L0: column tile `half` of the SIMD's row tiles
         {
             const bf16x8 wa = as_bf(*reinterpret_cast<const u32x4 *>(W0s + half * 16 * 32 + wl));
@@ -532,6 +597,7 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
             }
         }
         dfr_lds_barrier();
+        DFR_CLK(1);
         // ---- L1: this half's share of the SIMD's row tiles, both column tiles; the
         // result replaces L0's in X after a barrier
         {
@@ -555,6 +621,7 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                     return as_bf(*reinterpret_cast<const u32x4 *>(X + xb[ii] + ((kk % 3) + (kk / 3) * PJ) * XST));
                 },
                 acc);
+            DFR_CLK(2);
             dfr_lds_barrier();   // every wave's L1 reads of X are done: X takes the L1 output
 #pragma unroll
             for (int ii = 0; ii < HALF; ++ii) {
@@ -575,7 +642,7 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
             }
         }
         dfr_lds_barrier();
-        if (s + gridDim.x < S) bload(s + gridDim.x);   // the next sample's boards, in flight through L2
+        DFR_CLK(3);
         // ---- L2: all the SIMD's row tiles, column tiles 2*half, 2*half + 1
         {
             f32x4 acc[TPS][2];
@@ -592,19 +659,74 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                     return as_bf(*reinterpret_cast<const u32x4 *>(X + xb[ii] + ((kk % 3) + (kk / 3) * PJ) * XST));
                 },
                 acc);
+            DFR_CLK(4);
+            // a2 leaves through LDS: the accumulators (8 bytes of one position per lane, four
+            // instructions per 128-byte position from two waves) go to a staging image in X,
+            // [position][64 channels], 8-byte slot s of position p at s ^ (p & 15) (the sixteen
+            // positions of a tile's store land on sixteen distinct bank pairs); then whole
+            // positions leave as 16-byte pieces, each 128-byte line written by one instruction
+            // (the scattered 8-byte stores took twice as long as the L2 offsets).
+            // (KEEP, the training forward at the update's batch: the direct 8-byte stores; the
+            // staging below spilled there, next to the a0 / a1 stores' registers)
+            if constexpr (KEEP) {
+                __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));   // the next boards (see below)
 #pragma unroll
-            for (int ii = 0; ii < TPS; ++ii) {
-                if (ii == TPS - 1 && !last_ok) continue;
-                int i, j;
-                tpos(simd + 4 * ii, i, j);
-                if (i >= H || j >= H) continue;
+                for (int ii = 0; ii < TPS; ++ii) {
+                    if (ii == TPS - 1 && !last_ok) continue;
+                    int i, j;
+                    tpos(simd + 4 * ii, i, j);
+                    if (i >= H || j >= H) continue;
 #pragma unroll
-                for (int c2 = 0; c2 < 2; ++c2)
-                    *reinterpret_cast<u32x2 *>(a2 + (s * M + i + j * H) * 64 + (2 * half + c2) * 16 + 4 * g) =
-                        relu_bf16x4(acc[ii][c2], b2[c2]);
+                    for (int c2 = 0; c2 < 2; ++c2)
+                        *reinterpret_cast<u32x2 *>(a2 + (s * M + i + j * H) * 64 + (2 * half + c2) * 16 + 4 * g) =
+                            relu_bf16x4(acc[ii][c2], b2[c2]);
+                }
+            } else {
+                dfr_lds_barrier();   // every wave's L2 reads of X are done
+#pragma unroll
+                for (int ii = 0; ii < TPS; ++ii) {
+                    if (ii == TPS - 1 && !last_ok) continue;
+                    int i, j;
+                    tpos(simd + 4 * ii, i, j);
+                    if (i >= H || j >= H) continue;
+                    const int p = i + j * H;
+#pragma unroll
+                    for (int c2 = 0; c2 < 2; ++c2)
+                        *reinterpret_cast<u32x2 *>(X + p * 64 + ((((2 * half + c2) * 4 + g) ^ (p & 15)) << 2)) =
+                            relu_bf16x4(acc[ii][c2], b2[c2]);
+                }
             }
         }
+        if constexpr (!KEEP) {
+            dfr_lds_barrier();
+            // the next sample's board loads landed long ago: waiting for them here, ahead of the
+            // a2 stores, keeps the compiler's wait at the loop head from draining those stores
+            __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+            {
+                static_assert(M * 64 <= Sh::X, "a2 staging fits X");
+                constexpr int NQ = M * 8, QT = (NQ + 511) / 512;   // 16-byte pieces of the sample's a2
+#pragma unroll 2
+                for (int u = 0; u < QT; ++u) {
+                    const int q = tid + u * 512;
+                    if (q < NQ) {
+                        const int p = q >> 3, k = q & 7, m = p & 15;
+                        const u32x4 v = *reinterpret_cast<const u32x4 *>(X + p * 64 + ((((2 * k) ^ m) & ~1) << 2));
+                        // the piece's two 8-byte halves, swapped back when the swizzle swapped them
+                        const u32x4 o = (m & 1) ? u32x4{v[2], v[3], v[0], v[1]} : v;
+                        *reinterpret_cast<u32x4 *>(a2 + (s * M + p) * 64 + 8 * k) = o;
+                    }
+                }
+            }
+        }
+        DFR_CLK(5);
+#ifdef SNK_ENV_CLOCKS
+        if (tid == 0) ++dfr_acc[6];
+#endif
     }
+#ifdef SNK_ENV_CLOCKS
+    if (tid == 0 && g_dfr_clk)
+        for (int k = 0; k < 7; ++k) g_dfr_clk[(int64_t)blockIdx.x * 8 + k] = dfr_acc[k];
+#endif
 }
 
 // ---------------------------------------------------------------- L3 (MFMA, two samples)
