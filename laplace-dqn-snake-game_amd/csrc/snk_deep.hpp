@@ -623,6 +623,13 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                 acc);
             DFR_CLK(2);
             dfr_lds_barrier();   // every wave's L1 reads of X are done: X takes the L1 output
+            // every tile's transposes first, then the stores (tile by tile, each transpose's LDS
+            // round trip was waited out before its store)
+            u32x2 ot[HALF][2];
+#pragma unroll
+            for (int ii = 0; ii < HALF; ++ii)
+#pragma unroll
+                for (int c2 = 0; c2 < 2; ++c2) ot[ii][c2] = dfr_tr44(relu_bf16x4(acc[ii][c2], b1[c2]), lane);
 #pragma unroll
             for (int ii = 0; ii < HALF; ++ii) {
                 const int i2 = half * HALF + ii, t = simd + 4 * i2;
@@ -632,12 +639,12 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                 const int ti = 4 * (t % NB) + (r & 3), tj = 4 * (t / NB) + g;   // the transposed store's position
 #pragma unroll
                 for (int c2 = 0; c2 < 2; ++c2) {
-                    const u32x2 o = relu_bf16x4(acc[ii][c2], b1[c2]);
                     if (KEEP && i < H && j < H)
-                        *reinterpret_cast<u32x2 *>(a1 + (s * M + i + j * H) * 32 + c2 * 16 + 4 * g) = o;
-                    const u32x2 ot = dfr_tr44(o, lane);
+                        *reinterpret_cast<u32x2 *>(a1 + (s * M + i + j * H) * 32 + c2 * 16 + 4 * g) =
+                            relu_bf16x4(acc[ii][c2], b1[c2]);
                     if (ti < H && tj < H)
-                        *reinterpret_cast<u32x2 *>(X + ((ti + 1) + (tj + 1) * PJ) * XST + c2 * 16 + 4 * (r >> 2)) = ot;
+                        *reinterpret_cast<u32x2 *>(X + ((ti + 1) + (tj + 1) * PJ) * XST + c2 * 16 + 4 * (r >> 2)) =
+                            ot[ii][c2];
                 }
             }
         }
