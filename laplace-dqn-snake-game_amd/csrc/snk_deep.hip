@@ -148,7 +148,7 @@ static void work_ensure(DeepNet &N, DeepWork &w, int64_t S, bool train) {
     w.a[0] = dalloc<uint16_t>(cap * nc * 32);
     w.a[1] = dalloc<uint16_t>(cap * nc * 32);
     w.a[2] = dalloc<uint16_t>(cap * nc * 64);
-    w.a[3] = dalloc<uint16_t>(cap * no * 64);
+    w.a[3] = dalloc<uint16_t>((cap + 15) / 16 * 16 * no * 64);   // whole 16-sample blocks (blocked layout)
     w.slab = dalloc<float>(slab);
     w.h1 = dalloc<float>(cap * 64);
     w.q = dalloc<float>(cap * 3);
@@ -193,7 +193,9 @@ static void conv_layers_bs(const DeepNet &N, const float *th, const uint16_t *im
         static_assert(Sh::LDS <= 160 * 1024, "deep L3 LDS");
         set_lds_limit((const void *)deep_conv3_kernel<BS>, Sh::LDS);
         const unsigned grid = (unsigned)std::min<int64_t>((S + 1) / 2, cu_count());
-        deep_conv3_kernel<BS><<<grid, 512, Sh::LDS, s>>>(w.a[2], img + D.img_w[3], th + D.off_b[3], w.a[3], S);
+        // a3 in the blocked layout deep_dense1_kernel<4, true> reads (the act forward's large batches)
+        deep_conv3_kernel<BS><<<grid, 512, Sh::LDS, s>>>(w.a[2], img + D.img_w[3], th + D.off_b[3], w.a[3], S,
+                                                         d1_rows(S) == 4 ? 1 : 0);
         launch_check("deep_conv3_kernel");
     }
 }
@@ -267,7 +269,7 @@ static int deep_layers(const DeepNet &N, const float *th, const uint16_t *img, c
     const int z = d1_splits(D, S, kc);
     if (lo <= 4 && hi >= 4) {
         if (d1_rows(S) == 4)
-            deep_dense1_kernel<4><<<dim3((unsigned)((S + 255) / 256), (unsigned)z), 256, 0, s>>>(w.a[3], img + D.img_d1,
+            deep_dense1_kernel<4, true><<<dim3((unsigned)((S + 255) / 256), (unsigned)z), 256, 0, s>>>(w.a[3], img + D.img_d1,
                                                                                                 S, D.K1, kc, w.slab);
         else
             deep_dense1_kernel<1><<<dim3((unsigned)((S + 63) / 64), (unsigned)z), 256, 0, s>>>(w.a[3], img + D.img_d1,

@@ -782,7 +782,7 @@ template <int H>
 __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restrict__ x,
                                                          const uint16_t *__restrict__ wimg,
                                                          const float *__restrict__ bias, uint16_t *__restrict__ y,
-                                                         int64_t S) {
+                                                         int64_t S, int blocked) {
     using Sh = DeepL3Shape<H>;
     constexpr int WO = Sh::WO, TILES = Sh::TILES, TPS = Sh::TPS, PJ = Sh::PJ;
     constexpr int APT = Sh::APT, APIECES = Sh::APIECES;
@@ -795,13 +795,17 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
     const int64_t npairs = (S + 1) / 2;
     // input piece q of pair p: sample 2p + q / (H*H*8) (clamped to S - 1), position, 16-byte chunk
     auto apiece = [&](int64_t p, int u) __attribute__((always_inline)) {
-        const int q = tid + u * 512;
+        int tq = tid;   // opaque: the per-piece offsets stay at the use (hoisted above the offset
+        asm volatile("" : "+v"(tq));   // loop, they were spilled across it)
+        const int q = tq + u * 512;
         const int smp = q / (H * H * 8), rem = q - smp * (H * H * 8);
         const int64_t sg = min(2 * p + smp, S - 1);
         return *reinterpret_cast<const u32x4 *>(x + (sg * H * H + (rem >> 3)) * 64 + (rem & 7) * 8);
     };
     auto apark = [&](int u, const u32x4 &v) __attribute__((always_inline)) {
-        const int q = tid + u * 512;
+        int tq = tid;   // opaque, as in apiece
+        asm volatile("" : "+v"(tq));
+        const int q = tq + u * 512;
         const int smp = q / (H * H * 8), rem = q - smp * (H * H * 8);
         const int pos = rem >> 3;   // rows are numbered across the pair (the swizzle uses the pair-wide row)
         *reinterpret_cast<u32x4 *>(As + dl3_slot(smp * (H * PJ) + (pos % H) + (pos / H) * PJ, rem & 7)) = v;
@@ -905,27 +909,86 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
 #pragma unroll
             for (int q = 0; q < 4; ++q) wcur[q] = wnext[q];
         }
-        // epilogue: bias + relu + bf16, 4 channels per lane
-#pragma unroll
-        for (int i = 0; i < TPS; ++i) {
-            const int t = simd + 4 * i;
-            if ((i == TPS - 1 && !last_ok) || r >= WO) continue;
-            const int64_t sg = 2 * p + t / WO;
-            if (sg >= S) continue;
-            const int o = r + (t % WO) * WO;
-#pragma unroll
-            for (int c2 = 0; c2 < 2; ++c2)
-                *reinterpret_cast<u32x2 *>(y + (sg * WO * WO + o) * 64 + (2 * half + c2) * 16 + 4 * g) =
-                    relu_bf16x4(acc[i][c2], bb[c2]);
-        }
         // LDS-only barriers (dfr_lds_barrier): a __syncthreads fence drained the pair's a3 stores
         // (and the ring's refills for the next pair) before the next pair's input loads were even
         // issued; the refills are counted by the offset loop's own vmcnt waits
-        dfr_lds_barrier();   // every wave is done reading this pair's inputs
-        if (more && SNK_DL3_VAR != 1) {   // the next pair's inputs
+        if (!blocked) {
+            // epilogue: bias + relu + bf16, 4 channels per lane, row-major a3 [sample][position][64]
 #pragma unroll
-            for (int u = 0; u < APT; ++u)
-                if (tid + u * 512 < APIECES) apark(u, apiece(pn, u));
+            for (int i = 0; i < TPS; ++i) {
+                const int t = simd + 4 * i;
+                if ((i == TPS - 1 && !last_ok) || r >= WO) continue;
+                const int64_t sg = 2 * p + t / WO;
+                if (sg >= S) continue;
+                const int o = r + (t % WO) * WO;
+#pragma unroll
+                for (int c2 = 0; c2 < 2; ++c2)
+                    *reinterpret_cast<u32x2 *>(y + (sg * WO * WO + o) * 64 + (2 * half + c2) * 16 + 4 * g) =
+                        relu_bf16x4(acc[i][c2], bb[c2]);
+            }
+            dfr_lds_barrier();   // every wave is done reading this pair's inputs
+            if (more && SNK_DL3_VAR != 1) {   // the next pair's inputs
+#pragma unroll
+                for (int u = 0; u < APT; ++u)
+                    if (tid + u * 512 < APIECES) apark(u, apiece(pn, u));
+            }
+        } else {
+            // blocked a3 (deep_dense1_kernel<4, true>'s reader): blocks of 16 samples x 32
+            // features, 1 KB each, [sample / 16][f / 32][sample % 16][f % 32]. The pair's two
+            // samples are two adjacent 64-byte rows of each block: the accumulators are staged in
+            // the (now dead) input region as [f / 32][pair sample][32], 8-byte slot k of each
+            // 128-byte unit b at k ^ ((b >> 1) & 15) (a store's sixteen positions on sixteen bank
+            // pairs), then leave as whole 128-byte lines, 16 bytes per lane. The next pair's input
+            // loads go out before those stores, and the wait for them counts the stores out.
+            constexpr int NU = WO * WO * 2;   // 128-byte units (blocks) per pair
+            static_assert(NU * 128 <= 2 * Sh::XS * 2, "a3 staging fits the input region");
+            dfr_lds_barrier();   // every wave is done reading this pair's inputs
+            int ln_ = lane, tq_ = tid;   // opaque: the addresses below are computed here (hoisted
+            asm volatile("" : "+v"(ln_), "+v"(tq_));   // above the offset loop, they were spilled)
+            const int r = ln_ & 15, g = ln_ >> 4;
+#pragma unroll
+            for (int i = 0; i < TPS; ++i) {
+                const int t = simd + 4 * i;
+                if ((i == TPS - 1 && !last_ok) || r >= WO) continue;
+                const int o = r + (t % WO) * WO, j = t / WO;
+#pragma unroll
+                for (int c2 = 0; c2 < 2; ++c2) {
+                    const int f = o * 64 + (2 * half + c2) * 16 + 4 * g, b = f >> 5;
+                    const int slot = (j * 8 + ((f & 31) >> 2)) ^ ((b >> 1) & 15);
+                    *reinterpret_cast<u32x2 *>(As + b * 64 + slot * 4) = relu_bf16x4(acc[i][c2], bb[c2]);
+                }
+            }
+            dfr_lds_barrier();
+            u32x4 av[APT];
+            if (more && SNK_DL3_VAR != 1) {
+#pragma unroll
+                for (int u = 0; u < APT; ++u)
+                    if (tid + u * 512 < APIECES) av[u] = apiece(pn, u);
+            }
+            asm volatile("" ::: "memory");   // the loads stay ahead of the stores (the counted wait)
+            constexpr int NQ = NU * 8, QT = (NQ + 511) / 512;   // 16-byte pieces
+            uint16_t *yb = y + ((2 * p) >> 4) * (int64_t)(NU * 512) + ((2 * p) & 15) * 32;
+            const bool both = 2 * p + 1 < S;   // an odd S: the last pair's second row stays unwritten
+#pragma unroll 2
+            for (int u = 0; u < QT; ++u) {
+                const int q = tq_ + u * 512;
+                if (q < NQ) {
+                    const int b = q >> 3, k = q & 7, m = (b >> 1) & 15;
+                    const u32x4 v = *reinterpret_cast<const u32x4 *>(As + b * 64 + (((2 * k) ^ m) & ~1) * 4);
+                    if (both || k < 4)   // pieces 0..3: the first sample's row
+                        *reinterpret_cast<u32x4 *>(yb + b * 512 + k * 8) = (m & 1) ? u32x4{v[2], v[3], v[0], v[1]} : v;
+                }
+            }
+            if (more && SNK_DL3_VAR != 1) {
+                // this wave's input loads landed (the stores after them may not): every wave issued
+                // at least MINST of them (the last wave the fewest)
+                constexpr int MINST = NQ > 448 ? (NQ - 449) / 512 + 1 : 0;
+                __builtin_amdgcn_s_waitcnt(waitcnt_vm(MINST));
+                dfr_lds_barrier();   // every wave's staging reads are done: the region takes the inputs
+#pragma unroll
+                for (int u = 0; u < APT; ++u)
+                    if (tid + u * 512 < APIECES) apark(u, av[u]);
+            }
         }
         dfr_lds_barrier();
     }
@@ -939,7 +1002,10 @@ __global__ __launch_bounds__(512) void deep_conv3_kernel(const uint16_t *__restr
 // in flight. NR row tiles per wave reuse each B fragment NR times: the B
 // stream from L2 is 1.8 MB per wave, so at 65,536 samples NR = 4 cuts it from
 // 7.4 GB (NR = 1) to 1.8 GB; small batches keep NR = 1 and split K instead.
-template <int NR>
+// BLOCKED: a4 in deep_conv3_kernel's blocked layout (16 samples x 32 features per 1 KB block):
+// each A fragment load reads one whole block, 1 KB contiguous, where the row-major layout gave
+// 16 rows x 64 bytes 28.8 KB apart (4.4 TB/s of HBM on the 1.89 GB a3 stream)
+template <int NR, bool BLOCKED = false>
 __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__restrict__ a4,
                                                           const uint16_t *__restrict__ w1img, int64_t S, int K1,
                                                           int kchunk, float *__restrict__ slab) {
@@ -949,7 +1015,13 @@ __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__rest
     const int k0 = blockIdx.y * kchunk, k1 = min(K1, k0 + kchunk);
     const uint16_t *pa[NR];
 #pragma unroll
-    for (int t = 0; t < NR; ++t) pa[t] = a4 + min(row0 + 16 * t + r, S - 1) * K1 + g * 8;
+    for (int t = 0; t < NR; ++t)
+        pa[t] = BLOCKED ? a4 + ((row0 + 16 * t) >> 4) * (int64_t)(K1 / 32) * 512 + r * 32 + g * 8
+                        : a4 + min(row0 + 16 * t + r, S - 1) * K1 + g * 8;
+    // the A fragment of k offset kk (a multiple of 32) of row tile t
+    auto aptr = [&](int t, int kk) __attribute__((always_inline)) {
+        return BLOCKED ? pa[t] + (int64_t)(kk >> 5) * 512 : pa[t] + kk;
+    };
     const uint16_t *pb = w1img + (int64_t)r * K1 + g * 8;
     f32x4 acc[NR][4];
 #pragma unroll
@@ -959,7 +1031,10 @@ __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__rest
     // 64-k steps through a ring of RING register sets, loaded RING - 1 steps ahead: the A
     // stream comes from HBM (a4 is written by L3 just before and is far larger than the
     // MALL), and two steps in flight per wave (one ahead) left it latency-bound
-    constexpr int RING = 4;
+#ifndef DEEP_D1_RING
+#define DEEP_D1_RING 6
+#endif
+    constexpr int RING = NR == 4 ? DEEP_D1_RING : 4;
     const int nst = (k1 - k0) / 64;
     u32x4 a[RING][NR][2], b[RING][2][4];
     auto load = [&](int st, u32x4 (&ar)[NR][2], u32x4 (&br)[2][4]) __attribute__((always_inline)) {
@@ -967,7 +1042,7 @@ __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__rest
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
-            for (int t = 0; t < NR; ++t) ar[t][u] = *reinterpret_cast<const u32x4 *>(pa[t] + kk + 32 * u);
+            for (int t = 0; t < NR; ++t) ar[t][u] = *reinterpret_cast<const u32x4 *>(aptr(t, kk + 32 * u));
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) br[u][nt] = *reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + kk + 32 * u);
         }
@@ -998,7 +1073,7 @@ __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__rest
         for (int nt = 0; nt < 4; ++nt) b[nt] = *reinterpret_cast<const u32x4 *>(pb + nt * 16 * (int64_t)K1 + k);
 #pragma unroll
         for (int t = 0; t < NR; ++t) {
-            const u32x4 a = *reinterpret_cast<const u32x4 *>(pa[t] + k);
+            const u32x4 a = *reinterpret_cast<const u32x4 *>(aptr(t, k));
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
                 acc[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a), as_bf(b[nt]), acc[t][nt], 0, 0, 0);
