@@ -488,7 +488,9 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const int k = 8 * g + e, kk = k / C, c = k - kk * C;
-        bofs[e] = k < 9 * C ? c * PL + kk % 3 + (kk / 3) * HB : -1;
+        // C == 2: k = 2 kk + c, so the pair (2 e2, 2 e2 + 1) is kernel offset 4g + e2, channels
+        // 0 and 1: bofs[2 e2] is its word (position) offset in the [position][channel] boards
+        bofs[e] = k < 9 * C ? (C == 2 ? kk % 3 + (kk / 3) * HB : c * PL + kk % 3 + (kk / 3) * HB) : -1;
     }
     static_assert(4 * (TPS - 1) < TILES, "tiles 0 .. TPS-2 of every SIMD exist");
     const bool last_ok = simd + 4 * (TPS - 1) < TILES;   // only a SIMD's last tile can be missing
@@ -543,7 +545,8 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
             const int e = tid + u * 512;
             if (e < C * M) {
                 const int c = e / M, cell = e % M;
-                BD[c * PL + (cell % H + 1) + (cell / H + 1) * HB] = f2bf(src.fbase ? __int_as_float(bv[u]) : (float)bv[u]);
+                const int bp = (cell % H + 1) + (cell / H + 1) * HB;   // C == 2: [position][channel]
+                BD[C == 2 ? 2 * bp + c : c * PL + bp] = f2bf(src.fbase ? __int_as_float(bv[u]) : (float)bv[u]);
             }
         }
         // the next sample's boards: in flight through this whole sample (waited for before the
@@ -567,33 +570,55 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
             }
         }
         DFR_CLK(0);
-        // ---- L0: column tile `half` of the SIMD's row tiles
+        // ---- L0: column tile `half` of the SIMD's row tiles, in three passes over the tiles
+        // (every gather, then every MFMA, then every epilogue: tile by tile, each tile's LDS
+        // reads, MFMA, transpose and store waited on one another). C == 2: the boards are
+        // [position][channel], so a k pair (channels 0, 1 of one kernel offset) is one u32 read
         {
             const bf16x8 wa = as_bf(*reinterpret_cast<const u32x4 *>(W0s + half * 16 * 32 + wl));
+            u32x4 xw[TPS];
+#pragma unroll
+            for (int ii = 0; ii < TPS; ++ii) {
+                // a missing last tile gathers the SIMD's tile 0 again (never stored)
+                const int t = simd + 4 * ((ii == TPS - 1 && !last_ok) ? 0 : ii);
+                int i, j;
+                tpos(t, i, j);
+                const int bb = min(i, H - 1) + min(j, H - 1) * HB;
+                if constexpr (C == 2) {
+                    const uint32_t *BD2 = reinterpret_cast<const uint32_t *>(BD);
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; ++e2) {
+                        const uint32_t w = BD2[bb + max(bofs[2 * e2], 0)];
+                        xw[ii][e2] = bofs[2 * e2] >= 0 ? w : 0u;
+                    }
+                } else {
+                    // branch-free gather: every lane loads (k past 9C reads cell 0 and is masked to zero)
+                    uint32_t v[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = BD[bb + max(bofs[e], 0)];
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; ++e2)
+                        xw[ii][e2] = (bofs[2 * e2] >= 0 ? v[2 * e2] : 0u) | ((bofs[2 * e2 + 1] >= 0 ? v[2 * e2 + 1] : 0u) << 16);
+                }
+            }
+            f32x4 a0v[TPS];
+#pragma unroll
+            for (int ii = 0; ii < TPS; ++ii)
+                a0v[ii] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, as_bf(xw[ii]), f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            u32x2 ot[TPS];
+#pragma unroll
+            for (int ii = 0; ii < TPS; ++ii) ot[ii] = dfr_tr44(relu_bf16x4(a0v[ii], b0), lane);   // quad r >> 2 of (r & 3, row g)
 #pragma unroll
             for (int ii = 0; ii < TPS; ++ii) {
                 const int t = simd + 4 * ii;
                 if (ii == TPS - 1 && !last_ok) continue;
                 int i, j;
                 tpos(t, i, j);
-                const int bb = min(i, H - 1) + min(j, H - 1) * HB;
-                // branch-free gather: every lane loads (k past 9C reads cell 0 and is masked to
-                // zero), all eight loads in flight before the first use
-                uint32_t w[4], v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = BD[bb + max(bofs[e], 0)];
-#pragma unroll
-                for (int e2 = 0; e2 < 4; ++e2)
-                    w[e2] = (bofs[2 * e2] >= 0 ? v[2 * e2] : 0u) | ((bofs[2 * e2 + 1] >= 0 ? v[2 * e2 + 1] : 0u) << 16);
-                const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, as_bf(u32x4{w[0], w[1], w[2], w[3]}),
-                                                                          f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                const u32x2 o = relu_bf16x4(acc, b0);
                 if (KEEP && i < H && j < H)
-                    *reinterpret_cast<u32x2 *>(a0 + (s * M + i + j * H) * 32 + half * 16 + 4 * g) = o;
-                const u32x2 ot = dfr_tr44(o, lane);   // quad r >> 2 of position (r & 3, row g)
+                    *reinterpret_cast<u32x2 *>(a0 + (s * M + i + j * H) * 32 + half * 16 + 4 * g) = relu_bf16x4(a0v[ii], b0);
                 const int ti = 4 * (t % NB) + (r & 3), tj = 4 * (t / NB) + g;
                 if (ti < H && tj < H)
-                    *reinterpret_cast<u32x2 *>(X + ((ti + 1) + (tj + 1) * PJ) * XST + half * 16 + 4 * (r >> 2)) = ot;
+                    *reinterpret_cast<u32x2 *>(X + ((ti + 1) + (tj + 1) * PJ) * XST + half * 16 + 4 * (r >> 2)) = ot[ii];
             }
         }
         dfr_lds_barrier();
