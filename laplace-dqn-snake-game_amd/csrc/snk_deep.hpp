@@ -442,6 +442,14 @@ __device__ uint64_t *g_dfr_clk;
 #else
 #define DFR_CLK(k) do { } while (0)
 #endif
+// measurement builds only (-DSNK_DFR_VAR=1 with SNK_ENV_CLOCKS; wrong results by design): the
+// a2 copy-out without its global stores
+#ifndef SNK_DFR_VAR
+#define SNK_DFR_VAR 0
+#endif
+#if SNK_DFR_VAR && !defined(SNK_ENV_CLOCKS)
+#error "SNK_DFR_VAR: measurement (clocks) builds only"
+#endif
 template <int C, int H, bool KEEP>
 __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const float *__restrict__ img0,
                                                          const uint16_t *__restrict__ wimg1,
@@ -745,7 +753,11 @@ __global__ __launch_bounds__(512) void deep_front_kernel(BoardSrc src, const flo
                         const u32x4 v = *reinterpret_cast<const u32x4 *>(X + p * 64 + ((((2 * k) ^ m) & ~1) << 2));
                         // the piece's two 8-byte halves, swapped back when the swizzle swapped them
                         const u32x4 o = (m & 1) ? u32x4{v[2], v[3], v[0], v[1]} : v;
+#if SNK_DFR_VAR == 1   // measurement builds: the copy-out without its global stores
+                        asm volatile("" :: "v"(o));
+#else
                         *reinterpret_cast<u32x4 *>(a2 + (s * M + p) * 64 + 8 * k) = o;
+#endif
                     }
                 }
             }
