@@ -8,10 +8,13 @@
 // partial-slab reduce). Both are reorganised around LDS-staged samples, in
 // one launch (blocks [0, S * 8) data gradient, the rest weight gradient):
 //
-//  * dW (grid: Z chunks of 2 samples x 9 groups of four kernel offsets, exact-fp32
+//  * dW (grid: Z chunks of 2 samples x C3_DWG = 8 groups, exact-fp32
 //    v_mfma_f32_32x32x2_f32):
 //    the chunk's a2 [2][bs^2][32] and dz3 [2][Wo^2][64] go to LDS once;
-//    wave w owns offset kk = 4*group + w, a 32 (ci) x 64 (co) tile. MFMA k-step
+//    the 72 tiles (kk, co half) of 32 (ci) x 32 (co) are 9 per group, two per wave
+//    and a third for wave 0 (8 groups, not 9 groups of four offsets: at B = 64 the
+//    grid is then 768 = 3 x 256 workgroups, one dispatch round on 256 CUs; with 800
+//    the last 32 started when the first finished and ran 3 us past the rest). MFMA k-step
 //    t = output position (io, jo), its two k lanes = the two samples:
 //    A[ci][s] = a2[s][(io + du, jo + dv)][ci], B[s][co] = dz3[s][(io, jo)][co],
 //    lane-consecutive LDS reads at wave-uniform offsets. The chunk's partial
@@ -58,6 +61,7 @@ struct Conv3BwdArgs {
     int S, bs, wo, nsc, Z, nW;
 };
 constexpr int C3_CG = 4;          // dX input channels per workgroup
+constexpr int C3_DWG = 8;         // dW workgroups per chunk (72 tiles of 32 ci x 32 co, 9 per workgroup)
 constexpr int C3_TLD = 148;       // LDS row stride of T in dX (tools/lds_banks.py: stores 1x, col2im reads 1.3x)
 
 __host__ __device__ inline int c3_dw_lds_floats(int bs, int wo, int nsc) {   // the chunk's a2 (dz3 in registers)
@@ -111,29 +115,47 @@ __device__ __forceinline__ void c3_dw_block(const Conv3BwdArgs &a, int z, int gr
                 ns * BS2 * 8);
     __syncthreads();
     C3B_CLK(1);
-    const int kk = grp * 4 + wave;
-    const int dv = kk / 6, du = kk - dv * 6;
-    const float *pa = A + ((hv ? h : 0) * BS2 + du + dv * BS) * 32 + r;
-    f32x16 acc[2];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int g = 0; g < 16; ++g) acc[nt][g] = 0.0f;
-#pragma unroll
-    for (int jo = 0; jo < WO; ++jo)
-#pragma unroll
-        for (int io = 0; io < WO; ++io) {
-            const float x = pa[(io + jo * BS) * 32];
-            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv ? x : 0.0f, y0[jo * WO + io], acc[0], 0, 0, 0);
-            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv ? x : 0.0f, y1[jo * WO + io], acc[1], 0, 0, 0);
-        }
-    C3B_CLK(2);
+    // tiles ht = 9 grp + wave + 4 c: offset kk = ht >> 1, output columns [32 (ht & 1), +32);
+    // wave 0 also takes 9 grp + 8. A wave's tiles share one column half (ht, ht + 4, ht + 8
+    // have one parity), so each k-step selects one dz3 column and feeds every chain
+    const int ht0 = 9 * grp + wave;
+    const bool odd = ht0 & 1;
     float *out = a.slab + (int64_t)z * 1153 * 64;
+    auto chains = [&](auto nch) {
+        constexpr int NCH = decltype(nch)::value;
+        const float *pa[NCH];
+        f32x16 acc[NCH];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
+        for (int c = 0; c < NCH; ++c) {
+            const int kk = (ht0 + 4 * c) >> 1, dv = kk / 6, du = kk - dv * 6;
+            pa[c] = A + ((hv ? h : 0) * BS2 + du + dv * BS) * 32 + r;
 #pragma unroll
-        for (int g = 0; g < 16; ++g) out[(kk * 32 + acc_row(g, lane)) * 64 + nt * 32 + r] = acc[nt][g];
-    if (grp == 0 && wave == 0) {   // bias row: column sums of the chunk's dz3, positions ascending per sample
+            for (int g = 0; g < 16; ++g) acc[c][g] = 0.0f;
+        }
+#pragma unroll
+        for (int jo = 0; jo < WO; ++jo)
+#pragma unroll
+            for (int io = 0; io < WO; ++io) {
+                const float y = odd ? y1[jo * WO + io] : y0[jo * WO + io];
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    const float x = pa[c][(io + jo * BS) * 32];
+                    acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(hv ? x : 0.0f, y, acc[c], 0, 0, 0);
+                }
+            }
+        C3B_CLK(2);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int kk = (ht0 + 4 * c) >> 1;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) out[(kk * 32 + acc_row(g, lane)) * 64 + (odd ? 32 : 0) + r] = acc[c][g];
+        }
+    };
+    if (wave == 0)
+        chains(std::integral_constant<int, 3>{});
+    else
+        chains(std::integral_constant<int, 2>{});
+    if (grp == 0 && wave == 3) {   // bias row: column sums of the chunk's dz3, positions ascending per sample
         float b0 = 0.0f, b1 = 0.0f;
 #pragma unroll
         for (int t = 0; t < WO2; ++t) {
@@ -318,7 +340,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WO >= 8 ? 2
     if (b < nX)
         c3_dx_block<WO>(a, b / (32 / C3_CG), b % (32 / C3_CG), c3sm);
     else
-        c3_dw_block<WO>(a, (b - nX) / 9, (b - nX) % 9, c3sm);
+        c3_dw_block<WO>(a, (b - nX) / C3_DWG, (b - nX) % C3_DWG, c3sm);
     C3B_CLK(4);
 }
 

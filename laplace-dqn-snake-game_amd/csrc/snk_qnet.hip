@@ -1537,7 +1537,7 @@ void qnet_backward(const QLayout &L, const float *th, const BoardSrc &src, int64
         // conv3: dW over rows (s, pout) | dX onto the bs x bs x 32 input (relu mask on a2)
         if (c3bwd_ok(L, S)) {
             float *c3d = dst(1, p.c3, L.off_w3, 1153 * 64, slab + sr.c3);
-            const Conv3BwdArgs ca{w.a2, w.dz3, th + L.off_w3, c3d, w.dz2, (int)S, bs, L.Wo, C3_NSC, p.c3.z, p.c3.z * 9};
+            const Conv3BwdArgs ca{w.a2, w.dz3, th + L.off_w3, c3d, w.dz2, (int)S, bs, L.Wo, C3_NSC, p.c3.z, p.c3.z * C3_DWG};
             const size_t lds = (size_t)std::max(c3_dw_lds_floats(bs, L.Wo, C3_NSC), c3_dx_lds_floats(L.Wo)) * 4;
             const unsigned nb = (unsigned)(ca.nW + S * (32 / C3_CG));
             auto go = [&](auto kern) {

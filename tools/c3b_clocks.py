@@ -20,7 +20,7 @@ tr = snk.Trainer(n_batches=10, n_envs=4096, board_size=12, n_frames=2, capacity=
 snk.fill_buffer_(tr, graph=False)
 tr.run(4, learn=True, graph=False)
 B, wo = 64, 7
-nW = (B + 1) // 2 * 9
+nW = (B + 1) // 2 * 8
 nwg = nW + B * 8
 nwg2 = B + 2 * B
 for f in (lib.snk_c3b_debug_clocks, lib.snk_c2b_debug_clocks):
@@ -38,7 +38,8 @@ out = {"grid_end_us": float(c[:, 4].max() - t0), "n_wg": nwg}
 
 
 def stats(v):
-    return {"median": float(np.median(v)), "max": float(v.max()), "min": float(v.min())}
+    return {"median": float(np.median(v)), "max": float(v.max()), "min": float(v.min()),
+            "p90": float(np.percentile(v, 90)), "p97": float(np.percentile(v, 97))}
 
 
 nX = B * 8   # data-gradient blocks come first in the grid
@@ -68,6 +69,14 @@ for _, dlt, k in ev:
     cur[k] += dlt
     peak = max(peak, cur[k])
 out["max_resident_per_cu"] = peak
+# blocks that started after the first dispatch round, and the end times of the blocks that
+# shared a CU with one of them
+late = c[:, 0] - t0 > 2.0
+late_cus = set(cu[late].tolist())
+shared = np.array([k in late_cus for k in cu.tolist()]) & ~late
+out["late_blocks"] = {"n": int(late.sum()), "dW": int(late[nX:].sum()),
+                      "end_of_cu_sharers": stats(c[shared, 4] - t0) if shared.any() else None,
+                      "end_of_others": stats(c[~shared & ~late, 4] - t0)}
 c2 = buf2[:, :5].astype(np.float64) / 100.0
 t2 = c2[:, 0].min()
 c2o = {"grid_end_us": float(c2[:, 4].max() - t2)}
