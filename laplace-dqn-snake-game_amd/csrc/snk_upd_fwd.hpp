@@ -219,6 +219,11 @@ constexpr int UPDF_SLOT = 3 * 32 * 32 * 2, UPDF_RING_MAX = 12, UPDF_RING_MIN = 6
 #ifndef UPDF_KS
 #define UPDF_KS 3
 #endif
+// phase 4's W1 rows: 0 = two batches of loads, D > 0 = a software pipeline D rows deep (8: the B = 64
+// update 0.0700 -> 0.0693 ms marginal, 16 / 24 / 32 no better; profiles/r06t_upd_d1_pipe.txt)
+#ifndef UPDF_D1_PIPE
+#define UPDF_D1_PIPE 8
+#endif
 __host__ __device__ constexpr int updf_ring(int hin, int C) {
     return (160 * 1024 - updf_base_bytes(hin, C)) / UPDF_SLOT >= UPDF_RING_MAX
                ? UPDF_RING_MAX
@@ -629,6 +634,22 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
             const int o4 = tid & 15, c = tid >> 4;   // outputs 4 o4 .. +3, channel c of this half
             const f32x4 *w1 = reinterpret_cast<const f32x4 *>(n.th + L.off_d1w + (int64_t)(32 * half + c) * 64 + 4 * o4);
             double z0 = 0.0, z1 = 0.0, z2 = 0.0, z3 = 0.0;
+#if UPDF_D1_PIPE
+            // software pipeline: row p + D is requested as row p is consumed
+            constexpr int D = UPDF_D1_PIPE < NO ? UPDF_D1_PIPE : NO;
+            f32x4 wv[NO];
+#pragma unroll
+            for (int k = 0; k < D; ++k) wv[k] = w1[(int64_t)k * 64 * 16];
+#pragma unroll
+            for (int k = 0; k < NO; ++k) {
+                if (k + D < NO) wv[k + D] = w1[(int64_t)(k + D) * 64 * 16];
+                const double av = (double)a3s[k * 32 + c];
+                z0 = __builtin_fma(av, (double)wv[k][0], z0);
+                z1 = __builtin_fma(av, (double)wv[k][1], z1);
+                z2 = __builtin_fma(av, (double)wv[k][2], z2);
+                z3 = __builtin_fma(av, (double)wv[k][3], z3);
+            }
+#else
             constexpr int PB = (NO + 1) / 2;   // W1 rows in flight per thread: two batches (L2 round trips)
             for (int p0 = 0; p0 < NO; p0 += PB) {
                 f32x4 wv[PB];
@@ -644,6 +665,7 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
                     z3 = __builtin_fma(av, (double)wv[k][3], z3);
                 }
             }
+#endif
             double *rd = red + c * 64 + 4 * o4;
             rd[0] = z0;
             rd[1] = z1;
