@@ -370,25 +370,37 @@ __global__ __launch_bounds__(UPDF_NT) void upd_fwd_kernel(UpdFwdArgs args) {
     };
 
     // ---- phase 1: conv1 (VALU), a1 and its split ---------------------------------------
-    for (int o = tid; o < NC * 16; o += UPDF_NT) {
-        const int p = o >> 4, co = o & 15;
+    // four output channels 4q .. 4q + 3 of position p per thread: one input read feeds four
+    // FMA chains (each in conv1_fwd_kernel's order), a1 leaves as one float4, the split as
+    // 8-byte pieces (one channel per thread read every input nine times per channel)
+    for (int o = tid; o < NC * 4; o += UPDF_NT) {
+        const int p = o >> 2, q = o & 3;
         const int j = p / HIN, i = p - j * HIN;
-        float acc = w1[9 * C * 16 + co];
+        float acc[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = w1[9 * C * 16 + 4 * q + e];
 #pragma unroll
         for (int kk = 0; kk < 9; ++kk) {
             const int du = kk % 3, dv = kk / 3;
 #pragma unroll
-            for (int c = 0; c < C; ++c)
-                acc = __builtin_fmaf(xin[c * NB + (i + du) + (j + dv) * BP], w1[(kk * C + c) * 16 + co], acc);
+            for (int c = 0; c < C; ++c) {
+                const float x = xin[c * NB + (i + du) + (j + dv) * BP];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(x, w1[(kk * C + c) * 16 + 4 * q + e], acc[e]);
+            }
         }
-        const float v = fmaxf(acc, 0.f);
-        if (wr && n.a1) n.a1[((int64_t)s * NC + p) * 16 + co] = v;
-        uint16_t h, m, l;
-        split3_scalar(v, h, m, l);
-        uint16_t *d = A1 + ((i + 1) + (j + 1) * BP) * UPDF_A1S + co;
-        d[0] = h;
-        d[16] = m;
-        d[32] = l;
+        f32x4 v4;
+        uint16_t h[4], m[4], l[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v4[e] = fmaxf(acc[e], 0.f);
+            split3_scalar(v4[e], h[e], m[e], l[e]);
+        }
+        if (wr && n.a1) *reinterpret_cast<f32x4 *>(n.a1 + ((int64_t)s * NC + p) * 16 + 4 * q) = v4;
+        u32x2 *d = reinterpret_cast<u32x2 *>(A1 + ((i + 1) + (j + 1) * BP) * UPDF_A1S + 4 * q);   // 8-byte aligned
+        d[0] = u32x2{(uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16)};
+        d[4] = u32x2{(uint32_t)m[0] | ((uint32_t)m[1] << 16), (uint32_t)m[2] | ((uint32_t)m[3] << 16)};
+        d[8] = u32x2{(uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16)};
     }
     __syncthreads();
     UPD_CLK(2);
