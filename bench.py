@@ -261,7 +261,7 @@ def configs2(args, snk, graph) -> dict:
     names = ["L0+L1+L2 conv 3x3 C->32->32->64 (deep_front_kernel, bf16 MFMA, fused in LDS)",
              "L1 (inside deep_front_kernel)", "L2 (inside deep_front_kernel)",
              "L3 conv 6x6 64->64 (deep_conv3_kernel, bf16 MFMA, two samples per step)",
-             "Dense1 (deep_dense1_kernel, bf16 MFMA)", "head (Dense2 + epsilon-greedy)"]
+             "Dense1 (deep_dense1_ldsb_kernel, bf16 MFMA)", "head (Dense2 + epsilon-greedy)"]
     flop = [flop[0] + flop[1] + flop[2], 0.0, 0.0] + flop[3:]
     d = int(np.argmax(ms[:5]))
     tf = flop[d] / (ms[d] * 1e-3) / 1e12

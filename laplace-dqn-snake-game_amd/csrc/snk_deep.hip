@@ -193,7 +193,8 @@ static void conv_layers_bs(const DeepNet &N, const float *th, const uint16_t *im
         static_assert(Sh::LDS <= 160 * 1024, "deep L3 LDS");
         set_lds_limit((const void *)deep_conv3_kernel<BS>, Sh::LDS);
         const unsigned grid = (unsigned)std::min<int64_t>((S + 1) / 2, cu_count());
-        // a3 in the blocked layout deep_dense1_kernel<4, true> reads (the act forward's large batches)
+        // a3 in the blocked layout deep_dense1_ldsb_kernel / deep_dense1_kernel<4, true> read (the act
+        // forward's large batches)
         deep_conv3_kernel<BS><<<grid, 512, Sh::LDS, s>>>(w.a[2], img + D.img_w[3], th + D.off_b[3], w.a[3], S,
                                                          d1_rows(S) == 4 ? 1 : 0);
         launch_check("deep_conv3_kernel");
@@ -268,13 +269,18 @@ static int deep_layers(const DeepNet &N, const float *th, const uint16_t *img, c
     int kc;
     const int z = d1_splits(D, S, kc);
     if (lo <= 4 && hi >= 4) {
-        if (d1_rows(S) == 4)
+#ifndef DEEP_D1_LDSB
+#define DEEP_D1_LDSB 1
+#endif
+        if (DEEP_D1_LDSB && d1_rows(S) == 4 && z == 1 && D.K1 % 64 == 0)
+            deep_dense1_ldsb_kernel<4><<<(unsigned)((S + 255) / 256), 256, 0, s>>>(w.a[3], img + D.img_d1, S, D.K1, w.slab);
+        else if (d1_rows(S) == 4)
             deep_dense1_kernel<4, true><<<dim3((unsigned)((S + 255) / 256), (unsigned)z), 256, 0, s>>>(w.a[3], img + D.img_d1,
                                                                                                 S, D.K1, kc, w.slab);
         else
             deep_dense1_kernel<1><<<dim3((unsigned)((S + 63) / 64), (unsigned)z), 256, 0, s>>>(w.a[3], img + D.img_d1,
                                                                                                S, D.K1, kc, w.slab);
-        launch_check("deep_dense1_kernel");
+        launch_check("deep_dense1 kernels");
     }
     return z;
 }

@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__rest
     const uint16_t *pa[NR];
 #pragma unroll
     for (int t = 0; t < NR; ++t)
-        pa[t] = BLOCKED ? a4 + ((row0 + 16 * t) >> 4) * (int64_t)(K1 / 32) * 512 + r * 32 + g * 8
+        pa[t] = BLOCKED ? a4 + min((row0 + 16 * t) >> 4, (S - 1) >> 4) * (int64_t)(K1 / 32) * 512 + r * 32 + g * 8
                         : a4 + min(row0 + 16 * t + r, S - 1) * K1 + g * 8;
     // the A fragment of k offset kk (a multiple of 32) of row tile t
     auto aptr = [&](int t, int kk) __attribute__((always_inline)) {
@@ -1125,6 +1125,117 @@ __global__ __launch_bounds__(256) void deep_dense1_kernel(const uint16_t *__rest
             for (int e = 0; e < 4; ++e) {
                 const int64_t row = row0 + 16 * t + 4 * g + e;
                 if (row < S) o[row * 64 + nt * 16 + r] = acc[t][nt][e];
+            }
+}
+
+// deep_dense1_ldsb_kernel: deep_dense1_kernel<NR, true> for an unsplit K (K1 % 64 == 0) with
+// the W1 (B) fragments of each 64-k step staged ONCE per workgroup in LDS by LDS-DMA (8 KB:
+// 64 output rows x 128 bytes, 16-byte chunk c of row n at c ^ (n & 7), so a fragment read's
+// eight-lane groups hit distinct banks), each wave issuing two of the step's eight 1 KB DMAs,
+// instead of each of the four waves loading all eight from L2 itself. A wave's vector-memory
+// queue (vmcnt <= 63) then holds the A (HBM) loads of D1L_RB - 1 steps ahead, where 16 loads a
+// step had left room for ~4; one LDS-only barrier per step publishes the step's B. Same
+// products and fp32 accumulation order as deep_dense1_kernel (per accumulator: k ascending).
+#ifndef DEEP_D1L_RB
+#define DEEP_D1L_RB 8
+#endif
+constexpr int D1L_RB = DEEP_D1L_RB;   // LDS slots = register ring entries; loads run D1L_RB - 1 steps ahead
+template <int NR>
+__global__ __launch_bounds__(256) void deep_dense1_ldsb_kernel(const uint16_t *__restrict__ a4,
+                                                               const uint16_t *__restrict__ w1img, int64_t S, int K1,
+                                                               float *__restrict__ slab) {
+    constexpr int RB = D1L_RB, SLOT = 64 * 64;   // halves per slot
+    static_assert(RB >= 3 && 10 * (RB - 2) <= 63, "the counted wait: vmcnt holds at most 63");
+    __shared__ __attribute__((aligned(16))) uint16_t Bs[RB * SLOT];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    const int64_t row0 = (int64_t)blockIdx.x * 64 * NR + wave * 16 * NR;
+    const uint16_t *pa[NR];
+#pragma unroll
+    for (int t = 0; t < NR; ++t)
+        pa[t] = a4 + min((row0 + 16 * t) >> 4, (S - 1) >> 4) * (int64_t)(K1 / 32) * 512 + r * 32 + g * 8;
+    // this lane's DMA sources: instruction j of this wave fills rows n = 8 (2 wave + j) + (lane >> 3),
+    // lane-linear slot chunk lane & 7 <- global chunk (lane & 7) ^ (n & 7)
+    const uint16_t *pbs[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = 8 * (2 * wave + j) + (lane >> 3);
+        pbs[j] = w1img + (int64_t)n * K1 + (((lane & 7) ^ (n & 7)) << 3);
+    }
+    // B[k = 32u + 8g + (0..7)][n = 16 nt + r]: row n, chunk 4u + g of the slot
+    int bo[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const int n = 16 * nt + r;
+            bo[u][nt] = n * 64 + (((4 * u + g) ^ (n & 7)) << 3);
+        }
+    f32x4 acc[NR][4];
+#pragma unroll
+    for (int t = 0; t < NR; ++t)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[t][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nst = K1 / 64;
+    u32x4 a[RB][NR][2];
+    // step st: this wave's two B DMAs into slot st % RB, then its A loads (10 vector-memory
+    // instructions, in this order, per step)
+    auto issue = [&](int st, int slot, u32x4 (&ar)[NR][2]) __attribute__((always_inline)) {
+        const int kk = 64 * st;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            __builtin_amdgcn_global_load_lds((const void *)(pbs[j] + kk),
+                                             (__attribute__((address_space(3))) void *)(Bs + slot * SLOT + (2 * wave + j) * 512),
+                                             16, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int t = 0; t < NR; ++t)
+                ar[t][u] = *reinterpret_cast<const u32x4 *>(pa[t] + (int64_t)((kk >> 5) + u) * 512);
+    };
+#pragma unroll
+    for (int o = 0; o < RB - 1; ++o)
+        if (o < nst) issue(o, o, a[o]);
+#pragma unroll 1
+    for (int st = 0; st < nst; st += RB) {
+#pragma unroll
+        for (int o = 0; o < RB; ++o) {
+            const int cs = st + o;
+            if (cs < nst) {   // wave-uniform
+                // step cs's loads landed (the RB - 2 later steps' may stay in flight), then every
+                // wave's: slot o holds step cs's B, and every wave's reads of step cs - 1 are done
+                if (cs + RB - 2 < nst)
+                    __builtin_amdgcn_s_waitcnt(waitcnt_vm(10 * (RB - 2)));
+                else
+                    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                __builtin_amdgcn_s_barrier();
+                // step cs + RB - 1 refills slot (o + RB - 1) % RB, last read at step cs - 1
+                if (cs + RB - 1 < nst) issue(cs + RB - 1, (o + RB - 1) % RB, a[(o + RB - 1) % RB]);
+                u32x4 b[2][4];
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) b[u][nt] = *reinterpret_cast<const u32x4 *>(Bs + o * SLOT + bo[u][nt]);
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int t = 0; t < NR; ++t)
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt)
+                            acc[t][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a[o][t][u]), as_bf(b[u][nt]),
+                                                                                 acc[t][nt], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NR; ++t)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t row = row0 + 16 * t + 4 * g + e;
+                if (row < S) slab[row * 64 + nt * 16 + r] = acc[t][nt][e];
             }
 }
 
