@@ -69,6 +69,25 @@ def test_deep_forward_large_batch_split_paths(snk):
     assert _err(q24, q[:24]) <= 1e-5, _err(q24, q[:24])
 
 
+def test_deep_forward_ragged_large_batch(snk):
+    """65,636 samples: not a multiple of the 256 rows of a deep_dense1_ldsb_kernel workgroup
+    (its last workgroup reads clamped a3 blocks and stores 100 rows) nor of L3's 16-sample
+    a3 blocks. Sampled rows across the batch and the ragged tail match the oracle; the
+    first 65,536 rows equal a 65,536-sample forward's bit for bit (every layer's per-sample
+    result, Dense1's unsplit K included, is independent of the batch size)."""
+    bs, C = 20, 2
+    m = snk.DQNModel(bs, 3, n_frames=C, seed=12, deep=True)
+    rng = np.random.default_rng(7)
+    p = _scaled(m, rng)
+    n = 65536 + 100
+    x = rng.integers(-1, 3, size=(n, C, bs * bs)).astype(np.float32)
+    q = m.forward(x)
+    sel = np.r_[np.linspace(0, n - 101, 12).astype(np.int64), np.arange(n - 100, n, 9), n - 1]
+    assert _close(q[sel], oracle.deep_forward(bs, C, p, x[sel]))
+    q0 = m.forward(x[:65536])
+    assert np.array_equal(q0, q[:65536])
+
+
 def _replay(snk, bs, C, n=64, T=10, seed=3):
     g = snk.SnakeGame(bs, C, n_envs=n, autoreset=True)
     rb = snk.ReplayBuffer(n * T, board_size=bs, n_frames=C, batch_size=64)
@@ -239,7 +258,7 @@ def test_configs2_trainer_graph_trajectory_vs_oracle(snk):
     deeper bf16 net, replay capacity 50,000 (each lockstep step overfills it: only the
     step's last 50,000 transitions survive, as sequential store! leaves them), B = 64,
     one captured graph of 4 iterations (deep_front_kernel / deep_conv3_kernel /
-    deep_dense1_kernel act forward over 65,536 states, the 20x20 step + store, the
+    deep_dense1_ldsb_kernel act forward over 65,536 states, the 20x20 step + store, the
     deep update: deep_conv3_small_kernel forward, the LDS-image backward kernels,
     RMSProp + images + target sync). epsilon 0.25, so most actions are greedy.
     The act / Q trace and the gradient trace make every iteration of the graph
