@@ -143,6 +143,9 @@ def parse():
     p.add_argument("--board-size", type=int, default=12)
     p.add_argument("--n-frames", type=int, default=2)
     p.add_argument("--updates-per-iter", type=int, default=1)
+    p.add_argument("--graph-unroll", type=int, default=8,
+                   help="lockstep iterations per captured hipGraph (each graph starts with the fresh "
+                        "weight splits and pays one graph launch)")
     p.add_argument("--epsilon", type=float, default=0.05)
     p.add_argument("--capacity", type=int, default=50000)
     p.add_argument("--settle-ms", type=float, default=300.0,
@@ -602,7 +605,7 @@ def main():
     n, bs, C = args.n_envs, args.board_size, args.n_frames
     tr = snk.Trainer(n_envs=n, board_size=bs, n_frames=C, capacity=args.capacity, batch_size=64,
                      epsilon=args.epsilon, epsilon_end=args.epsilon, decay=0.0,
-                     updates_per_iter=args.updates_per_iter, seed=1234 + rank)
+                     updates_per_iter=args.updates_per_iter, seed=1234 + rank, graph_unroll=args.graph_unroll)
     comm = None
     if world > 1:
         with _stdout_to_stderr():
