@@ -652,6 +652,17 @@ __global__ __launch_bounds__(512) void d1_bwd_kernel(const float *__restrict__ a
     const int b = blockIdx.x;
     const bool dx = b < nfb;
     const int f0 = (dx ? b : b - nfb) * D1B_F;
+    // dX blocks: the relu mask a3 of this lane's four outputs, loaded with the staging (read after
+    // the MFMAs it was one more round trip at the block's end)
+    float mk[4] = {0.f, 0.f, 0.f, 0.f};
+    if (dx) {
+        const int mt = wave >> 1, nt = wave & 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int s = 16 * mt + kq + 4 * i;
+            if (s < S) mk[i] = a3[(int64_t)s * K1 + f0 + 16 * nt + r];
+        }
+    }
     {   // staging: every float4 load first (dz1: 2 per thread, the W1 or a3 block: 1), then the LDS stores
         f32x4 vz[2], vx = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -700,10 +711,7 @@ __global__ __launch_bounds__(512) void d1_bwd_kernel(const float *__restrict__ a
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int s = 16 * mt + kq + 4 * i;
-            if (s < S) {
-                const int64_t o = (int64_t)s * K1 + f;
-                dz3[o] = a3[o] > 0.0f ? (float)acc[i] : 0.0f;
-            }
+            if (s < S) dz3[(int64_t)s * K1 + f] = mk[i] > 0.0f ? (float)acc[i] : 0.0f;
         }
     } else {    // tile = wave: f tile wave >> 2 (of 2), o tile wave & 3 (of 4)
         const int mt = wave >> 2, nt = wave & 3;
